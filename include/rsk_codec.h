@@ -1,0 +1,212 @@
+/*
+ * rsk_codec.h — C ABI of the MI355X framing codec (drop-in for rsock's per-packet codec path).
+ *
+ * Every entry point is extern "C", takes plain pointers and sizes, and returns 0 or a negative
+ * error code.  Batch entry points are stream-ordered (the `stream` argument is a hipStream_t,
+ * passed as void* so this header needs no HIP include; NULL = the legacy default stream) and take
+ * no ownership: the caller owns every device and host buffer.  All batch array pointers are
+ * DEVICE pointers unless a comment says otherwise.
+ *
+ * Reference interfaces replaced (paths relative to the rsock tree):
+ *   rsk_compute_hash      <- char* compute_hash(char*, const std::string&, const char*, int)   util/rhash.h:17, util/rhash.cpp:20-41
+ *   rsk_hash_equal        <- bool hash_equal(const char*, const std::string&, const char*, int) util/rhash.h:13, util/rhash.cpp:71-92
+ *   rsk_enchead_enc2buf   <- char* EncHead::Enc2Buf(char*, int)                               bean/EncHead.h:40, bean/EncHead.cpp:9-24
+ *   rsk_enchead_decodebuf <- static const char* EncHead::DecodeBuf(EncHead&, const char*, int) bean/EncHead.h:38, bean/EncHead.cpp:39-55
+ *   rsk_encode_batch      <- int RConn::Output(ssize_t, const rbuf_t&), framing part          conn/RConn.h:37, conn/RConn.cpp:87-105
+ *   rsk_decode_batch      <- int RConn::OnRecv(ssize_t, const rbuf_t&)                        conn/RConn.h:34, conn/RConn.cpp:64-85
+ *   rsk_parse_decode_batch<- int RawTcp::RawInput(u_char*, const pcap_pkthdr*, const u_char*) conn/RawTcp.h:38, conn/RawTcp.cpp:138-237
+ *                            + RawTcp::cap2uv size check (RawTcp.cpp:239-244) fused with RConn::OnRecv
+ *   rsk_tcpinfo_encode_batch <- char* TcpInfo::Encode(char*, int) (21-B hand-off record)      bean/TcpInfo.cpp:20-32, bean/ConnInfo.cpp:12-20
+ *   rsk_key_for_tcp/udp   <- KeyGenerator::KeyForTcp / KeyForUdp                              src/util/KeyGenerator.cpp:16-36
+ */
+#ifndef RSK_CODEC_H
+#define RSK_CODEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- wire constants (include/rstype.h:11-12, include/rscomm.h:19, conn/RConn.cpp:20) ---------- */
+#define RSK_HASH_BUF_SIZE 8     /* tag bytes = last 8 bytes of the MD5 digest             */
+#define RSK_ID_BUF_SIZE 8       /* IdBuf bytes                                            */
+#define RSK_ENC_HEAD_SIZE 23    /* EncHead wire size: len,cmd,id[8],conv u32,key u64,rsvd */
+#define RSK_HEAD_SIZE 31        /* RConn::HEAD_SIZE = 8 + 23                              */
+#define RSK_MAX_PKT_SIZE 1500   /* OM_MAX_PKT_SIZE                                         */
+#define RSK_MAX_PAYLOAD (RSK_MAX_PKT_SIZE - RSK_HEAD_SIZE) /* 1469                          */
+#define RSK_TCPINFO_WIRE_SIZE 21 /* TcpInfo::Encode record: src,dst,sp,dp,seq,ack,flag      */
+
+/* EncHead::TYPE (bean/EncHead.h:14-20) */
+#define RSK_CMD_DATA 0
+#define RSK_CMD_CONV_RST 1
+#define RSK_CMD_NETCONN_RST 2
+#define RSK_CMD_KEEP_ALIVE_REQ 3
+#define RSK_CMD_KEEP_ALIVE_RESP 4
+
+/* TCP flag bits as RawTcp reads them (tcp[13]) */
+#define RSK_TH_FIN 0x01
+#define RSK_TH_SYN 0x02
+#define RSK_TH_RST 0x04
+#define RSK_TH_PUSH 0x08
+#define RSK_TH_ACK 0x10
+
+/* pcap datalink types accepted by RawTcp::RawInput (RawTcp.cpp:144-165) */
+#define RSK_DLT_NULL 0
+#define RSK_DLT_EN10MB 1
+
+/* ---- error codes returned by every entry point --------------------------------------------- */
+#define RSK_OK 0
+#define RSK_EINVAL (-22)   /* bad argument (NULL where required, n too large, bad datalink)  */
+#define RSK_ENOMEM (-12)   /* device/host allocation failed                                   */
+#define RSK_EDEVICE (-5)   /* a HIP runtime call failed (see rsk_last_error())                */
+
+/* ---- per-packet status codes ---------------------------------------------------------------- */
+/* Encode (RConn::Output, RConn.cpp:87-128): status[i] = 31 + P (frame length) when the frame was
+ * written; RSK_SEND_OVERSIZE (-1) when 31 + P > 1500 (RConn.cpp:94-98, nothing written);
+ * RSK_SEND_RESET (0) when P == 0 (the reference calls RConnReset::SendReset instead of framing,
+ * RConn.cpp:119-123; nothing written, the caller sends the reset). */
+#define RSK_SEND_OVERSIZE (-1)
+#define RSK_SEND_RESET 0
+
+/* Decode (RConn::OnRecv, RConn.cpp:64-85): */
+#define RSK_RECV_VALID 1   /* tag verified; payload forwarded to IGroup::OnRecv (:73-75)      */
+#define RSK_RECV_CLOSE 0   /* nread <= 31 on TCP with FIN|RST: NotifyTcpFinOrRst, return 0    */
+#define RSK_RECV_DROP (-1) /* everything else: return -1                                      */
+
+/* Parse (RawTcp::RawInput, RawTcp.cpp:138-237 + cap2uv :239-244): */
+#define RSK_PARSE_DROP 0      /* silently dropped (reference returns 0 before delivery)       */
+#define RSK_PARSE_DELIVER 1   /* handed to cap2uv -> syncInput -> RConn::OnRecv               */
+#define RSK_PARSE_SYN 2       /* SYN with an ack pool: TcpAckPool::AddInfoFromPeer, return 0   */
+#define RSK_PARSE_MALFORMED 3 /* header runs past cap_len, or negative payload_len with FIN|RST
+                                 (the reference memcpy's a negative length there: UB,
+                                 RawTcp.cpp:251) — defined here as a drop                      */
+
+/* parse flags */
+#define RSK_PARSE_HAS_ACK_POOL 0x1 /* RawTcp::mTcpAckPool != nullptr                          */
+#define RSK_PARSE_IS_SERVER 0x2    /* RawTcp::mIsServer: SYN info is Reverse()d (:222-224)     */
+
+/* ---- context -------------------------------------------------------------------------------- */
+typedef struct rsk_ctx rsk_ctx;
+
+/* Create a codec context bound to HIP device `device` for hash key `key` (host pointer, key_len
+ * bytes, any length; rsock's default is "hello135", bean/RConfig.h:44).  The key's MD5 message
+ * schedule is precomputed here (chaining state of the whole-key blocks, the constant words of the
+ * block that carries the payload byte, and the padding block when one is needed), so the kernels
+ * compress 1 block per tag for key_len <= 54 and 2 blocks otherwise.  Returns NULL on failure. */
+rsk_ctx *rsk_create(const uint8_t *key, uint32_t key_len, int device);
+void rsk_destroy(rsk_ctx *ctx);
+
+/* Pre-size the context's device workspace (decode compaction scratch) for batches of up to n
+ * packets.  Batch calls grow it on demand, which allocates and synchronises; call this first if
+ * batch calls will be captured into a hipGraph. */
+int rsk_reserve(rsk_ctx *ctx, uint32_t n_max);
+
+/* Text of the last HIP error seen by this thread (static storage). */
+const char *rsk_last_error(void);
+
+/* Library version string, e.g. "rsk 0.1 gfx950". */
+const char *rsk_version(void);
+
+/* ---- batch encode (RConn::Output framing) --------------------------------------------------- */
+typedef struct rsk_encode_in {
+    const uint8_t *payload_arena; /* device bytes                                           */
+    const uint64_t *pay_off;      /* [n] byte offset of packet i's payload in payload_arena  */
+    const uint16_t *pay_len;      /* [n] P = nread                                           */
+    const uint8_t *cmd;           /* [n] EncHead cmd                                         */
+    const uint32_t *conv;         /* [n] EncHead conv                                        */
+    const uint64_t *conn_key;     /* [n] EncHead connKey                                     */
+    const uint8_t *id;            /* [n*8] per-packet IdBuf, or NULL to use id_uniform       */
+    uint8_t id_uniform[8];        /* IdBuf used for every packet when id == NULL             */
+} rsk_encode_in;
+
+typedef struct rsk_encode_out {
+    uint8_t *frame_arena;     /* device bytes                                              */
+    const uint64_t *frame_off;/* [n] where frame i starts (16-B aligned offsets take the
+                                 vector path; any offset is correct)                        */
+    int32_t *status;          /* [n] 31+P, RSK_SEND_OVERSIZE or RSK_SEND_RESET              */
+} rsk_encode_out;
+
+/* frame_i = tag(8) | EncHead(23) | payload(P), written to frame_arena + frame_off[i].
+ * Frames must not overlap each other or the payload arena. */
+int rsk_encode_batch(rsk_ctx *ctx, uint32_t n, const rsk_encode_in *in, const rsk_encode_out *out,
+                     void *stream);
+
+/* ---- batch decode + verify (RConn::OnRecv) --------------------------------------------------- */
+typedef struct rsk_decode_out {
+    uint8_t *hlen;       /* [n] EncHead len byte as received (payload starts at 8 + hlen)      */
+    uint8_t *cmd;        /* [n]                                                               */
+    uint8_t *id;         /* [n*8]                                                             */
+    uint32_t *conv;      /* [n]                                                               */
+    uint64_t *conn_key;  /* [n]                                                               */
+    uint16_t *pay_off;   /* [n] payload offset relative to the frame start (= 8 + hlen)       */
+    uint16_t *pay_len;   /* [n] nread - 8 - hlen                                              */
+    int8_t *status;      /* [n] RSK_RECV_*                                                    */
+    uint32_t *valid_idx; /* [n] order-stable list of i with status == RSK_RECV_VALID (may be NULL) */
+    uint32_t *n_valid;   /* [1] number of entries in valid_idx (device; may be NULL)            */
+} rsk_decode_out;
+/* For packets whose status is not RSK_RECV_VALID, hlen/cmd/id/conv/conn_key/pay_off/pay_len are
+ * written as zero (the reference never exposes fields of a dropped frame). */
+
+/* frame i = frame_len[i] bytes at frame_arena + frame_off[i]; is_tcp_close[i] != 0 marks a frame
+ * that arrived on fake TCP with FIN or RST set (TcpInfo::HasCloseFlag, bean/TcpInfo.h:31); NULL
+ * means "UDP / no close flag" for all packets. */
+int rsk_decode_batch(rsk_ctx *ctx, uint32_t n, const uint8_t *frame_arena, const uint64_t *frame_off,
+                     const uint16_t *frame_len, const uint8_t *is_tcp_close, const rsk_decode_out *out,
+                     void *stream);
+
+/* ---- fused pcap parse + decode (RawTcp::RawInput -> cap2uv -> RConn::OnRecv) ----------------- */
+typedef struct rsk_tcpinfo_out {
+    uint32_t *src;  /* [n] ip_dst as stored (network byte order bytes, read LE) — "self" view   */
+    uint32_t *dst;  /* [n] ip_src as stored                                                    */
+    uint16_t *sp;   /* [n] ntohs(th_dport)                                                     */
+    uint16_t *dp;   /* [n] ntohs(th_sport)                                                     */
+    uint32_t *seq;  /* [n] ntohl(th_seq) (+ payload_len when delivered)                        */
+    uint32_t *ack;  /* [n] ntohl(th_ack)                                                       */
+    uint8_t *flag;  /* [n] th_flags                                                            */
+    int8_t *parse_status; /* [n] RSK_PARSE_*                                                   */
+    uint16_t *cap_pay_off; /* [n] payload (= frame) offset inside the captured packet          */
+    uint16_t *cap_pay_len; /* [n] payload_len (0 unless delivered)                             */
+} rsk_tcpinfo_out;
+/* TcpInfo fields are written for RSK_PARSE_DELIVER and RSK_PARSE_SYN, zero otherwise.  The decode
+ * outputs (`dec`) follow rsk_decode_batch on the delivered payload with is_tcp_close = flag &
+ * (FIN|RST); packets that were not delivered get dec->status = RSK_RECV_DROP and zero fields. */
+int rsk_parse_decode_batch(rsk_ctx *ctx, uint32_t n, const uint8_t *cap_arena, const uint64_t *cap_off,
+                           const uint32_t *wire_len, const uint32_t *cap_len, int datalink, int flags,
+                           const rsk_tcpinfo_out *tcp, const rsk_decode_out *dec, void *stream);
+
+/* ---- TcpInfo hand-off records (cap2uv's 21-B TcpInfo::Encode) ---------------- */
+/* rec[21*i ..] = src LE32 | dst LE32 | sp LE16 | dp LE16 | seq LE32 | ack LE32 | flag. */
+int rsk_tcpinfo_encode_batch(rsk_ctx *ctx, uint32_t n, const uint32_t *src, const uint32_t *dst,
+                             const uint16_t *sp, const uint16_t *dp, const uint32_t *seq,
+                             const uint32_t *ack, const uint8_t *flag, uint8_t *rec, void *stream);
+
+/* ---- single-packet shims with the reference signatures (host pointers) ----------------------- */
+/* These run the same HIP kernels on a batch of one (device round trip, synchronous), so a caller
+ * can swap them in per call.  They are a compatibility surface, not a fast path. */
+/* Writes the 8-byte tag for data[0] to tag_out; returns tag_out + 8 (NULL if data_len <= 0). */
+uint8_t *rsk_compute_hash(rsk_ctx *ctx, uint8_t *tag_out, const uint8_t *data, int data_len);
+/* 1 if tag == MD5(key || data[0])[8..15], 0 otherwise (0 when data == NULL or data_len <= 0). */
+int rsk_hash_equal(rsk_ctx *ctx, const uint8_t *tag, const uint8_t *data, int data_len);
+/* Writes the 23-byte EncHead; returns p + 23, or NULL when p == NULL or buf_len < 23. */
+uint8_t *rsk_enchead_enc2buf(rsk_ctx *ctx, uint8_t *p, int buf_len, uint8_t cmd, const uint8_t id[8],
+                             uint32_t conv, uint64_t conn_key);
+/* Decodes fields; returns p + len (len = p[0]), or NULL when p == NULL, buf_len < 23 or len > buf_len.
+ * Any output pointer may be NULL. */
+const uint8_t *rsk_enchead_decodebuf(rsk_ctx *ctx, const uint8_t *p, int buf_len, uint8_t *len,
+                                     uint8_t *cmd, uint8_t id[8], uint32_t *conv, uint64_t *conn_key);
+
+/* ---- connKey helpers (host, pure integer arithmetic) ---------------------------------------- */
+/* KeyForTcp: 0x10000000 | (dp << 16) | sp — the type bit overlaps dp bit 12, reproduced as-is. */
+uint64_t rsk_key_for_tcp(uint16_t sp, uint16_t dp);
+uint64_t rsk_key_for_udp(uint16_t sp, uint16_t dp);
+
+/* ---- synthetic workload generator (device; used by bench/tests, not by the codec) ------------ */
+/* Fills n bytes at dst with the splitmix64 stream: 8-byte word w = splitmix64(seed + w) (LE). */
+int rsk_fill_splitmix(void *dst, uint64_t nbytes, uint64_t seed, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RSK_CODEC_H */

@@ -1,0 +1,135 @@
+"""ctypes mirror of include/rsk_codec.h.
+
+Loads the in-tree ``rsock_amd/librsk.so`` (built by ``__graft_entry__.build()`` /
+``make -C rsock_amd``).  There is no fallback: if the library is missing or fails to load, importing
+this module raises, so nothing can silently run a non-HIP path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librsk.so")
+
+# ---- constants (include/rsk_codec.h) ------------------------------------------------------------
+HASH_BUF_SIZE = 8
+ID_BUF_SIZE = 8
+ENC_HEAD_SIZE = 23
+HEAD_SIZE = 31
+MAX_PKT_SIZE = 1500
+MAX_PAYLOAD = MAX_PKT_SIZE - HEAD_SIZE
+TCPINFO_WIRE_SIZE = 21
+
+CMD_DATA, CMD_CONV_RST, CMD_NETCONN_RST, CMD_KEEP_ALIVE_REQ, CMD_KEEP_ALIVE_RESP = 0, 1, 2, 3, 4
+TH_FIN, TH_SYN, TH_RST, TH_PUSH, TH_ACK = 0x01, 0x02, 0x04, 0x08, 0x10
+DLT_NULL, DLT_EN10MB = 0, 1
+
+OK, EINVAL, ENOMEM, EDEVICE = 0, -22, -12, -5
+SEND_OVERSIZE, SEND_RESET = -1, 0
+RECV_VALID, RECV_CLOSE, RECV_DROP = 1, 0, -1
+PARSE_DROP, PARSE_DELIVER, PARSE_SYN, PARSE_MALFORMED = 0, 1, 2, 3
+PARSE_HAS_ACK_POOL, PARSE_IS_SERVER = 0x1, 0x2
+
+_vp = ctypes.c_void_p
+_u8p = ctypes.c_void_p  # all arrays passed as raw addresses
+
+
+class EncodeIn(ctypes.Structure):
+    _fields_ = [
+        ("payload_arena", _vp),
+        ("pay_off", _vp),
+        ("pay_len", _vp),
+        ("cmd", _vp),
+        ("conv", _vp),
+        ("conn_key", _vp),
+        ("id", _vp),
+        ("id_uniform", ctypes.c_uint8 * 8),
+    ]
+
+
+class EncodeOut(ctypes.Structure):
+    _fields_ = [("frame_arena", _vp), ("frame_off", _vp), ("status", _vp)]
+
+
+class DecodeOut(ctypes.Structure):
+    _fields_ = [
+        ("hlen", _vp),
+        ("cmd", _vp),
+        ("id", _vp),
+        ("conv", _vp),
+        ("conn_key", _vp),
+        ("pay_off", _vp),
+        ("pay_len", _vp),
+        ("status", _vp),
+        ("valid_idx", _vp),
+        ("n_valid", _vp),
+    ]
+
+
+class TcpInfoOut(ctypes.Structure):
+    _fields_ = [
+        ("src", _vp),
+        ("dst", _vp),
+        ("sp", _vp),
+        ("dp", _vp),
+        ("seq", _vp),
+        ("ack", _vp),
+        ("flag", _vp),
+        ("parse_status", _vp),
+        ("cap_pay_off", _vp),
+        ("cap_pay_len", _vp),
+    ]
+
+
+# (name, restype, argtypes) for every symbol the header declares
+SIGNATURES = [
+    ("rsk_create", _vp, [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_int]),
+    ("rsk_destroy", None, [_vp]),
+    ("rsk_reserve", ctypes.c_int, [_vp, ctypes.c_uint32]),
+    ("rsk_last_error", ctypes.c_char_p, []),
+    ("rsk_version", ctypes.c_char_p, []),
+    ("rsk_encode_batch", ctypes.c_int,
+     [_vp, ctypes.c_uint32, ctypes.POINTER(EncodeIn), ctypes.POINTER(EncodeOut), _vp]),
+    ("rsk_decode_batch", ctypes.c_int,
+     [_vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, ctypes.POINTER(DecodeOut), _vp]),
+    ("rsk_parse_decode_batch", ctypes.c_int,
+     [_vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, ctypes.c_int, ctypes.c_int,
+      ctypes.POINTER(TcpInfoOut), ctypes.POINTER(DecodeOut), _vp]),
+    ("rsk_tcpinfo_encode_batch", ctypes.c_int,
+     [_vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("rsk_compute_hash", _vp, [_vp, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]),
+    ("rsk_hash_equal", ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]),
+    ("rsk_enchead_enc2buf", _vp,
+     [_vp, ctypes.c_char_p, ctypes.c_int, ctypes.c_uint8, ctypes.c_char_p, ctypes.c_uint32,
+      ctypes.c_uint64]),
+    ("rsk_enchead_decodebuf", _vp,
+     [_vp, ctypes.c_char_p, ctypes.c_int, _vp, _vp, _vp, _vp, _vp]),
+    ("rsk_key_for_tcp", ctypes.c_uint64, [ctypes.c_uint16, ctypes.c_uint16]),
+    ("rsk_key_for_udp", ctypes.c_uint64, [ctypes.c_uint16, ctypes.c_uint16]),
+    ("rsk_fill_splitmix", ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint64, _vp]),
+]
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    if not os.path.exists(path):
+        raise ImportError(
+            f"rsock_amd: HIP library {path} not built; run `python -c 'import __graft_entry__ as g; g.build()'`"
+        )
+    lib = ctypes.CDLL(path)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)  # AttributeError here = header/library mismatch
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+def header_symbols(header_path: str | None = None) -> list[str]:
+    """Names of every function declared in include/rsk_codec.h (used by the ABI test)."""
+    import re
+
+    if header_path is None:
+        header_path = os.path.join(os.path.dirname(_HERE), "include", "rsk_codec.h")
+    text = open(header_path).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(rsk_[a-z0-9_]+)\s*\(", text)))

@@ -1,0 +1,234 @@
+"""Host-side mirror of rsock's codec surface over the HIP C-ABI.
+
+Names follow the reference:
+  * ``Codec.compute_hash`` / ``Codec.hash_equal``   <- util/rhash.h:13-17
+  * ``Codec.enc2buf`` / ``Codec.decodebuf``          <- EncHead::Enc2Buf / DecodeBuf (bean/EncHead.h:38-40)
+  * ``Codec.output_batch`` (RConn::Output framing)   <- conn/RConn.cpp:87-105
+  * ``Codec.onrecv_batch`` (RConn::OnRecv)           <- conn/RConn.cpp:64-85
+  * ``Codec.rawinput_batch`` (RawTcp::RawInput + OnRecv) <- conn/RawTcp.cpp:138-244
+Batch arguments are torch tensors on the codec's device (torch is used only for memory and
+streams).  Every call goes through ``rsock_amd/librsk.so``; there is no CPU path here.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, fields
+
+import torch
+
+from . import _abi
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        _lib = _abi.load()
+    return _lib
+
+
+def _ptr(t) -> int | None:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def _stream(stream) -> int | None:
+    if stream is None:
+        return torch.cuda.current_stream().cuda_stream
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+class RskError(RuntimeError):
+    pass
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        err = lib().rsk_last_error()
+        raise RskError(f"{what} failed: rc={rc} ({err.decode() if err else ''})")
+
+
+@dataclass
+class DecodeBuffers:
+    """SoA outputs of RConn::OnRecv for n frames (rsk_decode_out)."""
+
+    hlen: torch.Tensor
+    cmd: torch.Tensor
+    id: torch.Tensor  # n*8 bytes
+    conv: torch.Tensor  # int32 storage of u32
+    conn_key: torch.Tensor  # int64 storage of u64
+    pay_off: torch.Tensor  # int16 storage of u16
+    pay_len: torch.Tensor  # int16 storage of u16
+    status: torch.Tensor  # int8
+    valid_idx: torch.Tensor  # int32 storage of u32
+    n_valid: torch.Tensor  # int32 [1]
+
+    @classmethod
+    def alloc(cls, n: int, device) -> "DecodeBuffers":
+        e = lambda k, dt: torch.empty(k, dtype=dt, device=device)  # noqa: E731
+        return cls(
+            hlen=e(n, torch.uint8),
+            cmd=e(n, torch.uint8),
+            id=e(n * 8, torch.uint8),
+            conv=e(n, torch.int32),
+            conn_key=e(n, torch.int64),
+            pay_off=e(n, torch.int16),
+            pay_len=e(n, torch.int16),
+            status=e(n, torch.int8),
+            valid_idx=e(max(n, 1), torch.int32),
+            n_valid=e(1, torch.int32),
+        )
+
+    def abi(self, compact: bool = True) -> _abi.DecodeOut:
+        return _abi.DecodeOut(
+            _ptr(self.hlen), _ptr(self.cmd), _ptr(self.id), _ptr(self.conv), _ptr(self.conn_key),
+            _ptr(self.pay_off), _ptr(self.pay_len), _ptr(self.status),
+            _ptr(self.valid_idx) if compact else None, _ptr(self.n_valid) if compact else None,
+        )
+
+    def to_host(self) -> dict:
+        out = {}
+        for f in fields(self):
+            out[f.name] = getattr(self, f.name).cpu().numpy()
+        return out
+
+
+@dataclass
+class TcpInfoBuffers:
+    """SoA TcpInfo outputs of RawTcp::RawInput for n captured packets (rsk_tcpinfo_out)."""
+
+    src: torch.Tensor
+    dst: torch.Tensor
+    sp: torch.Tensor
+    dp: torch.Tensor
+    seq: torch.Tensor
+    ack: torch.Tensor
+    flag: torch.Tensor
+    parse_status: torch.Tensor
+    cap_pay_off: torch.Tensor
+    cap_pay_len: torch.Tensor
+
+    @classmethod
+    def alloc(cls, n: int, device) -> "TcpInfoBuffers":
+        e = lambda dt: torch.empty(n, dtype=dt, device=device)  # noqa: E731
+        return cls(
+            src=e(torch.int32), dst=e(torch.int32), sp=e(torch.int16), dp=e(torch.int16),
+            seq=e(torch.int32), ack=e(torch.int32), flag=e(torch.uint8),
+            parse_status=e(torch.int8), cap_pay_off=e(torch.int16), cap_pay_len=e(torch.int16),
+        )
+
+    def abi(self) -> _abi.TcpInfoOut:
+        return _abi.TcpInfoOut(*[_ptr(getattr(self, f.name)) for f in fields(self)])
+
+    def to_host(self) -> dict:
+        return {f.name: getattr(self, f.name).cpu().numpy() for f in fields(self)}
+
+
+class Codec:
+    """One rsk_ctx: a hash key bound to a HIP device."""
+
+    def __init__(self, key: bytes = b"hello135", device: int = 0):
+        self.key = bytes(key)
+        self.device = int(device)
+        self._ctx = lib().rsk_create(self.key, len(self.key), self.device)
+        if not self._ctx:
+            raise RskError(f"rsk_create failed: {lib().rsk_last_error().decode()}")
+
+    def close(self) -> None:
+        if self._ctx:
+            lib().rsk_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reserve(self, n_max: int) -> None:
+        _check(lib().rsk_reserve(self._ctx, n_max), "rsk_reserve")
+
+    # ---- batch paths ---------------------------------------------------------------------
+    def output_batch(self, payload, pay_off, pay_len, cmd, conv, conn_key, frame, frame_off, status,
+                     id=None, id_uniform: bytes = b"\0" * 8, stream=None) -> None:
+        """RConn::Output framing for n packets (rsk_encode_batch)."""
+        n = pay_len.numel()
+        ein = _abi.EncodeIn(_ptr(payload), _ptr(pay_off), _ptr(pay_len), _ptr(cmd), _ptr(conv),
+                            _ptr(conn_key), _ptr(id),
+                            (ctypes.c_uint8 * 8)(*bytes(id_uniform)[:8].ljust(8, b"\0")))
+        eout = _abi.EncodeOut(_ptr(frame), _ptr(frame_off), _ptr(status))
+        _check(lib().rsk_encode_batch(self._ctx, n, ctypes.byref(ein), ctypes.byref(eout),
+                                      _stream(stream)), "rsk_encode_batch")
+
+    def onrecv_batch(self, frame, frame_off, frame_len, out: DecodeBuffers, is_tcp_close=None,
+                     compact: bool = True, stream=None) -> None:
+        """RConn::OnRecv for n frames (rsk_decode_batch)."""
+        n = frame_len.numel()
+        dout = out.abi(compact)
+        _check(lib().rsk_decode_batch(self._ctx, n, _ptr(frame), _ptr(frame_off), _ptr(frame_len),
+                                      _ptr(is_tcp_close), ctypes.byref(dout), _stream(stream)),
+               "rsk_decode_batch")
+
+    def rawinput_batch(self, cap, cap_off, wire_len, cap_len, datalink: int, flags: int,
+                       tcp: TcpInfoBuffers, out: DecodeBuffers, compact: bool = True,
+                       stream=None) -> None:
+        """RawTcp::RawInput -> cap2uv -> RConn::OnRecv for n captured packets."""
+        n = wire_len.numel()
+        tout = tcp.abi()
+        dout = out.abi(compact)
+        _check(lib().rsk_parse_decode_batch(self._ctx, n, _ptr(cap), _ptr(cap_off), _ptr(wire_len),
+                                            _ptr(cap_len), datalink, flags, ctypes.byref(tout),
+                                            ctypes.byref(dout), _stream(stream)),
+               "rsk_parse_decode_batch")
+
+    def tcpinfo_encode_batch(self, src, dst, sp, dp, seq, ack, flag, rec, stream=None) -> None:
+        n = src.numel()
+        _check(lib().rsk_tcpinfo_encode_batch(self._ctx, n, _ptr(src), _ptr(dst), _ptr(sp), _ptr(dp),
+                                              _ptr(seq), _ptr(ack), _ptr(flag), _ptr(rec),
+                                              _stream(stream)), "rsk_tcpinfo_encode_batch")
+
+    # ---- reference single-call signatures (GPU round trip each) -----------------------------
+    def compute_hash(self, data: bytes) -> bytes | None:
+        tag = ctypes.create_string_buffer(8)
+        r = lib().rsk_compute_hash(self._ctx, tag, bytes(data), len(data))
+        return tag.raw if r else None
+
+    def hash_equal(self, tag: bytes, data: bytes) -> bool:
+        return bool(lib().rsk_hash_equal(self._ctx, bytes(tag), bytes(data), len(data)))
+
+    def enc2buf(self, cmd: int, id: bytes, conv: int, conn_key: int, buf_len: int = 1492) -> bytes | None:
+        buf = ctypes.create_string_buffer(max(buf_len, 23))
+        r = lib().rsk_enchead_enc2buf(self._ctx, buf, buf_len, cmd, bytes(id)[:8].ljust(8, b"\0"),
+                                      conv & 0xFFFFFFFF, conn_key & 0xFFFFFFFFFFFFFFFF)
+        return buf.raw[:23] if r else None
+
+    def decodebuf(self, buf: bytes, buf_len: int | None = None):
+        """-> (len, cmd, id, conv, conn_key) or None (EncHead::DecodeBuf returned nullptr)."""
+        if buf_len is None:
+            buf_len = len(buf)
+        b = bytes(buf).ljust(23, b"\0")
+        ln, cmd = ctypes.c_uint8(), ctypes.c_uint8()
+        idb = ctypes.create_string_buffer(8)
+        conv, key = ctypes.c_uint32(), ctypes.c_uint64()
+        r = lib().rsk_enchead_decodebuf(self._ctx, b, buf_len, ctypes.byref(ln), ctypes.byref(cmd),
+                                        idb, ctypes.byref(conv), ctypes.byref(key))
+        if not r:
+            return None
+        return ln.value, cmd.value, idb.raw, conv.value, key.value
+
+
+def key_for_tcp(sp: int, dp: int) -> int:
+    return lib().rsk_key_for_tcp(sp, dp)
+
+
+def key_for_udp(sp: int, dp: int) -> int:
+    return lib().rsk_key_for_udp(sp, dp)
+
+
+def fill_splitmix(t: torch.Tensor, seed: int, stream=None) -> None:
+    _check(lib().rsk_fill_splitmix(_ptr(t), t.numel() * t.element_size(), seed & (2**64 - 1),
+                                   _stream(stream)), "rsk_fill_splitmix")

@@ -1,0 +1,80 @@
+// rsk_device.h — byte-movement and header helpers shared by the codec kernels (gfx950).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rsk {
+
+// bytes [r, r+4) of the 8-byte little-endian pair {hi:lo}  (v_alignbyte_b32)
+__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t r) {
+    return __builtin_amdgcn_alignbyte(hi, lo, r);
+}
+
+// 16 bytes starting at byte `sh` (0..15) of the 32-byte little-endian concatenation A||B.
+// sh is uniform per packet, so the switch is a scalar branch.
+__device__ __forceinline__ uint4 funnel16(const uint4 &A, const uint4 &B, uint32_t sh) {
+    const uint32_t r = sh & 3u;
+    uint4 o;
+    switch (sh >> 2) {
+        case 0:
+            o.x = funnel(A.y, A.x, r); o.y = funnel(A.z, A.y, r);
+            o.z = funnel(A.w, A.z, r); o.w = funnel(B.x, A.w, r);
+            break;
+        case 1:
+            o.x = funnel(A.z, A.y, r); o.y = funnel(A.w, A.z, r);
+            o.z = funnel(B.x, A.w, r); o.w = funnel(B.y, B.x, r);
+            break;
+        case 2:
+            o.x = funnel(A.w, A.z, r); o.y = funnel(B.x, A.w, r);
+            o.z = funnel(B.y, B.x, r); o.w = funnel(B.z, B.y, r);
+            break;
+        default:
+            o.x = funnel(B.x, A.w, r); o.y = funnel(B.y, B.x, r);
+            o.z = funnel(B.z, B.y, r); o.w = funnel(B.w, B.z, r);
+            break;
+    }
+    return o;
+}
+
+// Store bytes [0, lim) of v at p (p 16-byte aligned, 0 < lim < 16): dword stores for whole
+// dwords, byte stores for the tail.  Neighbouring frames may own the rest of the 16-B chunk.
+__device__ __forceinline__ void store_partial16(uint8_t *p, const uint4 &v, int lim) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const int lo = 4 * d;
+        if (lo + 4 <= lim) {
+            *reinterpret_cast<uint32_t *>(p + lo) = w[d];
+        } else if (lo < lim) {
+#pragma unroll
+            for (int b = 0; b < 3; ++b)
+                if (lo + b < lim) p[lo + b] = (uint8_t)(w[d] >> (8 * b));
+        }
+    }
+}
+
+// NW dwords of bytes starting at an arbitrary byte address p; aligned dwords whose address is
+// past `last` (the last byte the caller may touch) are not loaded (read as 0).  An aligned dword
+// that contains a valid byte never crosses a page, so no load can fault.
+template <int NW>
+__device__ __forceinline__ void load_window(const uint8_t *p, const uint8_t *last, uint32_t (&w)[NW]) {
+    const uint32_t r = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3u);
+    const uint32_t *q = reinterpret_cast<const uint32_t *>(p - r);  // keeps the global AS
+    const intptr_t lim = last - (p - r);                             // last valid byte, rel. to q
+    uint32_t raw[NW + 1];
+#pragma unroll
+    for (int j = 0; j <= NW; ++j) raw[j] = (4 * j <= lim) ? q[j] : 0u;
+#pragma unroll
+    for (int j = 0; j < NW; ++j) w[j] = funnel(raw[j + 1], raw[j], r);
+}
+
+__device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xffu) << 8) | ((x >> 8) & 0xffu); }
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+// byte k (0..31) of an 8-word little-endian window, k compile-time
+template <int K>
+__device__ __forceinline__ uint32_t byte_of(const uint32_t (&w)[8]) {
+    return (w[K >> 2] >> (8 * (K & 3))) & 0xffu;
+}
+
+}  // namespace rsk

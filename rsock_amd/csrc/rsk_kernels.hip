@@ -1,0 +1,937 @@
+// rsk_kernels.hip — MI355X (gfx950) HIP implementation of the rsock framing codec + its C ABI.
+//
+// Kernels (DESIGN.md §Kernels has the roofline and the algorithmic bytes of each):
+//   k_encode        RConn::Output framing (conn/RConn.cpp:87-105): per 64-packet tile, one lane per
+//                   packet computes status, the MD5 tag and the 31 header bytes; then the whole wave
+//                   streams each frame as 16-B chunks (wave-cooperative, coalesced, funnel-shifted
+//                   payload loads, v_alignbyte).
+//   k_decode        RConn::OnRecv (conn/RConn.cpp:64-85): one lane per frame, 32-B header window,
+//                   MD5 verify, SoA field stores, per-wave ballot mask + per-block count.
+//   k_parse_decode  RawTcp::RawInput (conn/RawTcp.cpp:138-244) fused with k_decode's body.
+//   k_scan/k_scatter order-stable compaction of the VALID indices from the ballot masks.
+//   k_tcpinfo_encode 21-B TcpInfo hand-off records (bean/TcpInfo.cpp:20-32), staged through LDS.
+//   k_fill_splitmix synthetic workload generator (bench/tests only).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "../../include/rsk_codec.h"
+#include "rsk_device.h"
+#include "rsk_md5.h"
+
+using rsk::KeySched;
+
+namespace {
+
+constexpr int kBlock = 256;  // 4 waves of 64
+constexpr int kWavesPerBlock = kBlock / 64;
+
+thread_local char g_last_error[256] = "";
+
+void set_error(const char *what, hipError_t e) {
+    snprintf(g_last_error, sizeof g_last_error, "%s: %s", what, hipGetErrorString(e));
+}
+
+// ---------------------------------------------------------------------------------------------
+// Encode
+// ---------------------------------------------------------------------------------------------
+struct EncArgs {
+    const uint8_t *payload;
+    const uint64_t *pay_off;
+    const uint16_t *pay_len;
+    const uint8_t *cmd;
+    const uint32_t *conv;
+    const uint64_t *conn_key;
+    const uint8_t *id;  // n*8, 8-byte aligned, or null
+    uint8_t *frame;
+    const uint64_t *frame_off;
+    int32_t *status;
+    uint32_t id_lo, id_hi;
+    uint32_t n;
+};
+
+__device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t j) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)j);
+}
+__device__ __forceinline__ uint64_t rdl64(uint64_t v, uint32_t j) {
+    return (uint64_t)rdl((uint32_t)v, j) | ((uint64_t)rdl((uint32_t)(v >> 32), j) << 32);
+}
+
+// Frame bytes 8..31 as words H[2..7] (bean/EncHead.cpp:9-24 field order; byte 30 reserved = 0,
+// byte 31 = payload[0], which belongs to the payload but shares the word).
+__device__ __forceinline__ void head_words(uint32_t cmd, uint32_t id0, uint32_t id1, uint32_t conv,
+                                           uint64_t key, uint32_t b0, uint32_t (&H)[8]) {
+    H[2] = (uint32_t)RSK_ENC_HEAD_SIZE | (cmd << 8) | (id0 << 16);
+    H[3] = (id0 >> 16) | (id1 << 16);
+    H[4] = (id1 >> 16) | (conv << 16);
+    H[5] = (conv >> 16) | ((uint32_t)key << 16);
+    H[6] = (uint32_t)(key >> 16);
+    H[7] = (uint32_t)(key >> 48) | (b0 << 24);
+}
+
+__global__ __launch_bounds__(kBlock) void k_encode(EncArgs a, KeySched ks) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t base = ((uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * 64u;
+    if (base >= a.n) return;  // wave-uniform
+    const uint64_t i = base + lane;
+
+    // ---- phase 1: one lane per packet — status, tag, header words ----
+    int32_t st = 0;
+    uint32_t P = 0;
+    uint64_t po = 0, fo = 0;
+    uint32_t H[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (i < a.n) {
+        po = a.pay_off[i];
+        P = a.pay_len[i];
+        fo = a.frame_off[i];
+        st = P == 0 ? RSK_SEND_RESET
+                    : (P > RSK_MAX_PAYLOAD ? RSK_SEND_OVERSIZE : (int32_t)(RSK_HEAD_SIZE + P));
+        if (st > 0) {
+            const uint32_t b0 = a.payload[po];
+            rsk::md5_tag(ks, b0, H[0], H[1]);
+            uint32_t id0 = a.id_lo, id1 = a.id_hi;
+            if (a.id) {
+                const uint2 v = *reinterpret_cast<const uint2 *>(a.id + 8 * i);
+                id0 = v.x;
+                id1 = v.y;
+            }
+            head_words(a.cmd[i], id0, id1, a.conv[i], a.conn_key[i], b0, H);
+        }
+        a.status[i] = st;
+    }
+
+    // ---- phase 2: the wave streams each framed packet of the tile ----
+    const uint32_t cnt = (uint32_t)min<uint64_t>(64u, a.n - base);
+    for (uint32_t j = 0; j < cnt; ++j) {
+        const int32_t sj = (int32_t)rdl((uint32_t)st, j);
+        if (sj <= 0) continue;
+        const uint32_t flen = (uint32_t)sj;  // 31 + P
+        const uint32_t Pj = flen - RSK_HEAD_SIZE;
+        const uint8_t *src = a.payload + rdl64(po, j);
+        uint8_t *dst = a.frame + rdl64(fo, j);
+        uint32_t Hj[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) Hj[q] = rdl(H[q], j);
+
+        if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
+            // vector path: chunk k holds frame bytes [16k, 16k+16)
+            const uint32_t nch = (flen + 15u) >> 4;
+            // chunk k >= 2 takes payload bytes [16k-31, 16k-15): 16-B aligned source chunks A, B
+            // at src_al + 16(k-2) and + 16, funnel-shifted by sh (uniform per packet)
+            const uint32_t sh = (uint32_t)((reinterpret_cast<uintptr_t>(src) + 1u) & 15u);
+            const uint8_t *src_al = src + 1 - sh;          // pointer arithmetic keeps global AS
+            const int32_t last_rel = (int32_t)Pj - 1 + (int32_t)sh - 1;  // last valid byte - src_al
+            for (uint32_t k = lane; k < nch; k += 64u) {
+                uint4 v;
+                if (k >= 2u) {
+                    const uint32_t ro = 16u * (k - 2u);
+                    const uint4 A = *reinterpret_cast<const uint4 *>(src_al + ro);
+                    uint4 B = make_uint4(0u, 0u, 0u, 0u);
+                    if (sh != 0u && (int32_t)(ro + 16u) <= last_rel)
+                        B = *reinterpret_cast<const uint4 *>(src_al + ro + 16u);
+                    v = rsk::funnel16(A, B, sh);
+                } else if (k == 0u) {
+                    v = make_uint4(Hj[0], Hj[1], Hj[2], Hj[3]);
+                } else {
+                    v = make_uint4(Hj[4], Hj[5], Hj[6], Hj[7]);
+                }
+                const int lim = (int)flen - 16 * (int)k;
+                uint8_t *d = dst + 16u * k;
+                if (lim >= 16) *reinterpret_cast<uint4 *>(d) = v;
+                else rsk::store_partial16(d, v, lim);
+            }
+        } else {
+            // generic path (frame not 16-B aligned): byte stores
+            for (uint32_t f = lane; f < flen; f += 64u) {
+                uint32_t byte;
+                if (f < (uint32_t)RSK_HEAD_SIZE) {
+                    uint32_t w = Hj[0];
+#pragma unroll
+                    for (int q = 1; q < 8; ++q)
+                        if ((f >> 2) == (uint32_t)q) w = Hj[q];
+                    byte = (w >> (8u * (f & 3u))) & 0xffu;
+                } else {
+                    byte = src[f - RSK_HEAD_SIZE];
+                }
+                dst[f] = (uint8_t)byte;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Decode (shared by k_decode and k_parse_decode)
+// ---------------------------------------------------------------------------------------------
+struct Dec {
+    uint32_t hlen, cmd, id0, id1, conv;
+    uint64_t key;
+    uint32_t poff, plen;
+    int32_t st;
+};
+
+// RConn::OnRecv on frame bytes [base, base + nread)  (conn/RConn.cpp:64-85, EncHead.cpp:39-55,
+// util/rhash.cpp:71-92).
+__device__ __forceinline__ Dec decode_frame(const uint8_t *base, int nread, bool close,
+                                            const KeySched &ks) {
+    Dec o = {0, 0, 0, 0, 0, 0, 0, 0, RSK_RECV_DROP};
+    if (nread > RSK_HEAD_SIZE) {
+        uint32_t w[8];
+        if ((reinterpret_cast<uintptr_t>(base) & 15u) == 0) {
+            const uint4 A = reinterpret_cast<const uint4 *>(base)[0];
+            const uint4 B = reinterpret_cast<const uint4 *>(base)[1];
+            w[0] = A.x; w[1] = A.y; w[2] = A.z; w[3] = A.w;
+            w[4] = B.x; w[5] = B.y; w[6] = B.z; w[7] = B.w;
+        } else {
+            rsk::load_window<8>(base, base + nread - 1, w);
+        }
+        const uint32_t len = w[2] & 0xffu;                 // EncHead len byte (frame[8])
+        const int dl = nread - 8 - (int)len;                // data_len handed to hash_equal
+        if ((int)len <= nread - 8 && dl > 0) {              // DecodeBuf ok, hash_equal len > 0
+            const uint32_t b = len == (uint32_t)RSK_ENC_HEAD_SIZE ? (w[7] >> 24) : base[8 + len];
+            uint32_t t0, t1;
+            rsk::md5_tag(ks, b, t0, t1);
+            if (t0 == w[0] && t1 == w[1]) {
+                o.st = RSK_RECV_VALID;
+                o.hlen = len;
+                o.cmd = (w[2] >> 8) & 0xffu;
+                o.id0 = (w[2] >> 16) | (w[3] << 16);
+                o.id1 = (w[3] >> 16) | (w[4] << 16);
+                o.conv = (w[4] >> 16) | (w[5] << 16);
+                o.key = (uint64_t)((w[5] >> 16) | (w[6] << 16)) |
+                        ((uint64_t)((w[6] >> 16) | (w[7] << 16)) << 32);
+                o.poff = 8u + len;
+                o.plen = (uint32_t)dl;
+            }
+        }
+    } else if (close) {
+        o.st = RSK_RECV_CLOSE;
+    }
+    return o;
+}
+
+struct DecOut {
+    uint8_t *hlen, *cmd, *id;
+    uint32_t *conv;
+    uint64_t *key;
+    uint16_t *pay_off, *pay_len;
+    int8_t *status;
+    uint64_t *masks;   // workspace: one ballot mask per wave (null: no compaction)
+    uint32_t *counts;  // workspace: VALID count per block
+};
+
+__device__ __forceinline__ void store_dec(const DecOut &d, uint64_t i, const Dec &o) {
+    d.hlen[i] = (uint8_t)o.hlen;
+    d.cmd[i] = (uint8_t)o.cmd;
+    *reinterpret_cast<uint2 *>(d.id + 8 * i) = make_uint2(o.id0, o.id1);
+    d.conv[i] = o.conv;
+    d.key[i] = o.key;
+    d.pay_off[i] = (uint16_t)o.poff;
+    d.pay_len[i] = (uint16_t)o.plen;
+    d.status[i] = (int8_t)o.st;
+}
+
+// Per-wave ballot of VALID + per-block count, consumed by k_scan / k_scatter.
+__device__ __forceinline__ void compact_epilogue(const DecOut &d, bool valid) {
+    __shared__ uint32_t wc[kWavesPerBlock];
+    const uint64_t m = __ballot(valid);
+    const uint32_t w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63u) == 0) {
+        d.masks[(uint64_t)blockIdx.x * kWavesPerBlock + w] = m;
+        wc[w] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t s = 0;
+#pragma unroll
+        for (int q = 0; q < kWavesPerBlock; ++q) s += wc[q];
+        d.counts[blockIdx.x] = s;
+    }
+}
+
+struct DecArgs {
+    const uint8_t *frame;
+    const uint64_t *frame_off;
+    const uint16_t *frame_len;
+    const uint8_t *close;
+    uint32_t n;
+};
+
+__global__ __launch_bounds__(kBlock) void k_decode(DecArgs a, DecOut d, KeySched ks) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    bool valid = false;
+    if (i < a.n) {
+        const Dec o = decode_frame(a.frame + a.frame_off[i], (int)a.frame_len[i],
+                                   a.close ? a.close[i] != 0 : false, ks);
+        store_dec(d, i, o);
+        valid = o.st == RSK_RECV_VALID;
+    }
+    if (d.masks) compact_epilogue(d, valid);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused pcap parse + decode  (conn/RawTcp.cpp:138-244, cap/cap_headers.h:16-32)
+// ---------------------------------------------------------------------------------------------
+struct ParseArgs {
+    const uint8_t *cap;
+    const uint64_t *cap_off;
+    const uint32_t *wire_len;
+    const uint32_t *cap_len;
+    uint32_t *src, *dst;
+    uint16_t *sp, *dp;
+    uint32_t *seq, *ack;
+    uint8_t *flag;
+    int8_t *pst;
+    uint16_t *cpo, *cpl;
+    int datalink, flags;
+    uint32_t n;
+};
+
+__global__ __launch_bounds__(kBlock) void k_parse_decode(ParseArgs a, DecOut d, KeySched ks) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    bool valid = false;
+    if (i < a.n) {
+        const uint8_t *pkt = a.cap + a.cap_off[i];
+        const uint32_t wl = a.wire_len[i], cl = a.cap_len[i];
+        int ps = RSK_PARSE_DROP;
+        uint32_t src = 0, dst = 0, sp = 0, dp = 0, seq = 0, ack = 0, fl = 0, payo = 0, plen = 0;
+        Dec o = {0, 0, 0, 0, 0, 0, 0, 0, RSK_RECV_DROP};
+        do {
+            if (wl < 44u) break;                                   // :139
+            const uint8_t *last = pkt + (cl ? cl - 1u : 0u);
+            uint32_t ipo;
+            if (a.datalink == RSK_DLT_EN10MB) {                     // :144-151
+                if (cl < 14u) { ps = RSK_PARSE_MALFORMED; break; }
+                uint32_t w[4];
+                rsk::load_window<4>(pkt, last, w);
+                if ((w[3] & 0xffffu) != 0x0008u) break;            // OM_PROTO_IP read LE
+                ipo = 14;
+            } else {                                                // DLT_NULL :152-160
+                if (cl < 4u) { ps = RSK_PARSE_MALFORMED; break; }
+                uint32_t w[1];
+                rsk::load_window<1>(pkt, last, w);
+                if (w[0] != 2u) break;
+                ipo = 4;
+            }
+            if (cl < ipo + 20u) { ps = RSK_PARSE_MALFORMED; break; }
+            uint32_t ip[5];
+            rsk::load_window<5>(pkt + ipo, last, ip);
+            if (((ip[2] >> 8) & 0xffu) != 6u) break;               // ip_p :167-172
+            const uint32_t ihl = (ip[0] & 15u) * 4u;
+            const uint32_t tcpo = ipo + ihl;
+            if (cl < tcpo + 20u) { ps = RSK_PARSE_MALFORMED; break; }
+            uint32_t th[4];
+            rsk::load_window<4>(pkt + tcpo, last, th);
+            const uint32_t thl = ((th[3] & 0xffu) >> 4) * 4u;
+            payo = tcpo + thl;
+            const int payload_len = (int)rsk::bswap16(ip[0] >> 16) - (int)(ihl + thl);  // :177
+            fl = (th[3] >> 8) & 0xffu;
+            src = ip[4];                                            // ip_dst.s_addr :213
+            dst = ip[3];                                            // ip_src.s_addr :215
+            sp = rsk::bswap16(th[0] >> 16);                         // ntohs(th_dport)
+            dp = rsk::bswap16(th[0] & 0xffffu);                     // ntohs(th_sport)
+            seq = rsk::bswap32(th[1]);
+            ack = rsk::bswap32(th[2]);
+            if ((fl & RSK_TH_SYN) && (a.flags & RSK_PARSE_HAS_ACK_POOL)) {  // :221-228
+                if (a.flags & RSK_PARSE_IS_SERVER) {
+                    uint32_t t = src; src = dst; dst = t;
+                    t = sp; sp = dp; dp = t;
+                    t = seq; seq = ack; ack = t;
+                }
+                ps = RSK_PARSE_SYN;
+                break;
+            }
+            const bool close = (fl & (RSK_TH_FIN | RSK_TH_RST)) != 0;
+            if (payload_len < RSK_HASH_BUF_SIZE + 1 && !close) break;            // :232-234
+            if (payload_len < -32) break;                          // cap2uv size_t wrap :240
+            if (payload_len < 0) { ps = RSK_PARSE_MALFORMED; break; }
+            if (payload_len + 32 > RSK_MAX_PKT_SIZE) break;        // cap2uv :240-244
+            if ((uint64_t)payo + (uint64_t)payload_len > cl) { ps = RSK_PARSE_MALFORMED; break; }
+            seq += (uint32_t)payload_len;                           // :235
+            plen = (uint32_t)payload_len;
+            ps = RSK_PARSE_DELIVER;
+            o = decode_frame(pkt + payo, payload_len, close, ks);
+        } while (false);
+        const bool keep = ps == RSK_PARSE_DELIVER || ps == RSK_PARSE_SYN;
+        a.src[i] = keep ? src : 0u;
+        a.dst[i] = keep ? dst : 0u;
+        a.sp[i] = (uint16_t)(keep ? sp : 0u);
+        a.dp[i] = (uint16_t)(keep ? dp : 0u);
+        a.seq[i] = keep ? seq : 0u;
+        a.ack[i] = keep ? ack : 0u;
+        a.flag[i] = (uint8_t)(keep ? fl : 0u);
+        a.pst[i] = (int8_t)ps;
+        a.cpo[i] = (uint16_t)(keep ? payo : 0u);
+        a.cpl[i] = (uint16_t)plen;
+        store_dec(d, i, o);
+        valid = o.st == RSK_RECV_VALID;
+    }
+    if (d.masks) compact_epilogue(d, valid);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Order-stable compaction of VALID indices
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_scan(const uint32_t *counts, uint32_t *offsets, uint32_t nb,
+                                               uint32_t *n_valid) {
+    __shared__ uint32_t s[1024];
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = (nb + 1023u) / 1024u;
+    const uint32_t lo = min(t * per, nb), hi = min(lo + per, nb);
+    uint32_t sum = 0;
+    for (uint32_t k = lo; k < hi; ++k) sum += counts[k];
+    s[t] = sum;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024u; off <<= 1) {
+        const uint32_t v = t >= off ? s[t - off] : 0u;
+        __syncthreads();
+        s[t] += v;
+        __syncthreads();
+    }
+    uint32_t run = s[t] - sum;
+    for (uint32_t k = lo; k < hi; ++k) {
+        offsets[k] = run;
+        run += counts[k];
+    }
+    if (t == 1023u && n_valid) *n_valid = s[1023];
+}
+
+__global__ __launch_bounds__(kBlock) void k_scatter(const uint64_t *masks, const uint32_t *offsets,
+                                                    uint32_t *valid_idx) {
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint64_t *mb = masks + (uint64_t)blockIdx.x * kWavesPerBlock;
+    uint32_t pos = offsets[blockIdx.x];
+    for (uint32_t q = 0; q < w; ++q) pos += (uint32_t)__popcll(mb[q]);
+    const uint64_t m = mb[w];
+    if ((m >> lane) & 1ull) {
+        pos += (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        valid_idx[pos] = blockIdx.x * (uint32_t)kBlock + threadIdx.x;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// TcpInfo 21-B records, staged through LDS so the global stores are 16-B and coalesced
+// ---------------------------------------------------------------------------------------------
+struct TcpRecArgs {
+    const uint32_t *src, *dst;
+    const uint16_t *sp, *dp;
+    const uint32_t *seq, *ack;
+    const uint8_t *flag;
+    uint8_t *rec;
+    uint32_t n;
+};
+
+__global__ __launch_bounds__(kBlock) void k_tcpinfo_encode(TcpRecArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t s[kBlock * RSK_TCPINFO_WIRE_SIZE];
+    const uint32_t t = threadIdx.x;
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + t;
+    if (i < a.n) {
+        uint8_t *r = s + RSK_TCPINFO_WIRE_SIZE * t;
+        const uint32_t v32[4] = {a.src[i], a.dst[i], a.seq[i], a.ack[i]};
+        const uint32_t v16[2] = {a.sp[i], a.dp[i]};
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            r[0 + b] = (uint8_t)(v32[0] >> (8 * b));
+            r[4 + b] = (uint8_t)(v32[1] >> (8 * b));
+            r[12 + b] = (uint8_t)(v32[2] >> (8 * b));
+            r[16 + b] = (uint8_t)(v32[3] >> (8 * b));
+        }
+        r[8] = (uint8_t)v16[0];
+        r[9] = (uint8_t)(v16[0] >> 8);
+        r[10] = (uint8_t)v16[1];
+        r[11] = (uint8_t)(v16[1] >> 8);
+        r[20] = a.flag[i];
+    }
+    __syncthreads();
+    const uint64_t first = (uint64_t)blockIdx.x * kBlock;
+    const uint32_t cnt = (uint32_t)min<uint64_t>(kBlock, a.n - first);
+    const uint32_t bytes = cnt * RSK_TCPINFO_WIRE_SIZE;
+    uint8_t *out = a.rec + first * RSK_TCPINFO_WIRE_SIZE;
+    if ((reinterpret_cast<uintptr_t>(out) & 15u) == 0) {
+        for (uint32_t c = t; 16u * c < bytes; c += kBlock) {
+            if (16u * c + 16u <= bytes) {
+                *reinterpret_cast<uint4 *>(out + 16u * c) = *reinterpret_cast<const uint4 *>(s + 16u * c);
+            } else {
+                for (uint32_t b = 16u * c; b < bytes; ++b) out[b] = s[b];
+            }
+        }
+    } else {
+        for (uint32_t b = t; b < bytes; b += kBlock) out[b] = s[b];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Single-packet shims (compatibility surface for the reference's per-call signatures)
+// ---------------------------------------------------------------------------------------------
+struct ShimIO {
+    uint8_t buf[64];   // in: op-specific input bytes; out: op-specific output bytes
+    int32_t ret;
+};
+
+__global__ void k_shim(ShimIO *io, int op, int len_arg, KeySched ks) {
+    if (threadIdx.x != 0) return;
+    uint8_t *b = io->buf;
+    if (op == 0) {  // compute_hash: b[0] = data[0] -> b[8..16) = tag
+        uint32_t t0, t1;
+        rsk::md5_tag(ks, b[0], t0, t1);
+        for (int k = 0; k < 4; ++k) { b[8 + k] = (uint8_t)(t0 >> (8 * k)); b[12 + k] = (uint8_t)(t1 >> (8 * k)); }
+        io->ret = 8;
+    } else if (op == 1) {  // hash_equal: b[0..8) tag, b[8] = data[0]
+        uint32_t t0, t1;
+        rsk::md5_tag(ks, b[8], t0, t1);
+        uint32_t e0 = 0, e1 = 0;
+        for (int k = 0; k < 4; ++k) { e0 |= (uint32_t)b[k] << (8 * k); e1 |= (uint32_t)b[4 + k] << (8 * k); }
+        io->ret = (t0 == e0 && t1 == e1) ? 1 : 0;
+    } else if (op == 2) {  // enc2buf: b[0]=cmd, b[1..9)=id, b[12..16)=conv, b[16..24)=key -> b[32..55)
+        uint32_t id0 = 0, id1 = 0, conv = 0;
+        uint64_t key = 0;
+        for (int k = 0; k < 4; ++k) {
+            id0 |= (uint32_t)b[1 + k] << (8 * k);
+            id1 |= (uint32_t)b[5 + k] << (8 * k);
+            conv |= (uint32_t)b[12 + k] << (8 * k);
+        }
+        for (int k = 0; k < 8; ++k) key |= (uint64_t)b[16 + k] << (8 * k);
+        uint32_t H[8];
+        head_words(b[0], id0, id1, conv, key, 0u, H);
+        for (int q = 0; q < 23; ++q) {
+            const int f = 8 + q;
+            b[32 + q] = (uint8_t)(H[f >> 2] >> (8 * (f & 3)));
+        }
+        io->ret = RSK_ENC_HEAD_SIZE;
+    } else {  // decodebuf: b[0..23) header, len_arg = buf_len -> fields in b[32..)
+        const uint32_t len = b[0];
+        if (len_arg < RSK_ENC_HEAD_SIZE || (int)len > len_arg) {
+            io->ret = -1;
+            return;
+        }
+        for (int q = 0; q < 23; ++q) b[32 + q] = b[q];
+        io->ret = (int)len;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Synthetic workload generator
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix64_at(uint64_t seed, uint64_t i) {
+    uint64_t z = seed + (i + 1u) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(kBlock) void k_fill_splitmix(uint8_t *dst, uint64_t nbytes, uint64_t seed) {
+    const uint64_t nw = nbytes / 8u;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t w = (uint64_t)blockIdx.x * kBlock + threadIdx.x; w < nw; w += stride) {
+        const uint64_t v = splitmix64_at(seed, w);
+        if ((reinterpret_cast<uintptr_t>(dst) & 7u) == 0) {
+            reinterpret_cast<uint64_t *>(dst)[w] = v;
+        } else {
+            for (int b = 0; b < 8; ++b) dst[8 * w + b] = (uint8_t)(v >> (8 * b));
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0 && nw * 8u < nbytes) {
+        const uint64_t v = splitmix64_at(seed, nw);
+        for (uint64_t b = nw * 8u; b < nbytes; ++b) dst[b] = (uint8_t)(v >> (8u * (b - nw * 8u)));
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Host helpers
+// ---------------------------------------------------------------------------------------------
+void build_sched(const uint8_t *key, uint32_t klen, KeySched &ks) {
+    std::memset(&ks, 0, sizeof ks);
+    uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+    const uint32_t nfull = klen / 64u;  // blocks made only of key bytes
+    auto words = [](const uint8_t *p, uint32_t (&m)[16]) {
+        for (int w = 0; w < 16; ++w)
+            m[w] = (uint32_t)p[4 * w] | ((uint32_t)p[4 * w + 1] << 8) | ((uint32_t)p[4 * w + 2] << 16) |
+                   ((uint32_t)p[4 * w + 3] << 24);
+    };
+    for (uint32_t b = 0; b < nfull; ++b) {
+        uint32_t m[16];
+        words(key + 64u * b, m);
+        rsk::md5_compress(st, m);
+    }
+    std::memcpy(ks.mid, st, sizeof st);
+    uint8_t tail[128];
+    std::memset(tail, 0, sizeof tail);
+    const uint32_t rem = klen - 64u * nfull;
+    if (rem) std::memcpy(tail, key + 64u * nfull, rem);
+    tail[rem] = 0;      // payload[0] slot
+    tail[rem + 1] = 0x80;
+    const bool two = rem + 2u + 8u > 64u;
+    const uint32_t tl = two ? 128u : 64u;
+    const uint64_t bits = ((uint64_t)klen + 1u) * 8u;
+    for (int k = 0; k < 8; ++k) tail[tl - 8 + k] = (uint8_t)(bits >> (8 * k));
+    uint32_t m[16];
+    words(tail, m);
+    std::memcpy(ks.blk, m, sizeof m);
+    if (two) {
+        words(tail + 64, m);
+        std::memcpy(ks.pad, m, sizeof m);
+    }
+    ks.bword = (int32_t)(rem / 4u);
+    ks.bshift = (int32_t)(8u * (rem % 4u));
+    ks.two_blocks = two ? 1 : 0;
+}
+
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = true;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) {
+            hipError_t e = hipSetDevice(dev);
+            if (e != hipSuccess) {
+                set_error("hipSetDevice", e);
+                ok = false;
+            }
+        }
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+inline unsigned grid_for(uint64_t threads) { return (unsigned)((threads + kBlock - 1) / kBlock); }
+
+}  // namespace
+
+struct rsk_ctx {
+    int device = 0;
+    std::vector<uint8_t> key;
+    KeySched ks;
+    // compaction workspace
+    void *ws = nullptr;
+    uint32_t ws_n = 0;
+    // single-packet shim buffers
+    ShimIO *shim_dev = nullptr;
+    ShimIO *shim_host = nullptr;
+    hipStream_t shim_stream = nullptr;
+    std::mutex shim_mu;
+};
+
+namespace {
+
+size_t ws_bytes(uint32_t n) {
+    const uint64_t nb = (n + kBlock - 1ull) / kBlock;
+    return nb * kWavesPerBlock * sizeof(uint64_t) + 2 * nb * sizeof(uint32_t) + 256;
+}
+
+int ensure_ws(rsk_ctx *c, uint32_t n) {
+    if (n <= c->ws_n && c->ws) return RSK_OK;
+    if (c->ws) {
+        hipError_t e = hipDeviceSynchronize();
+        if (e != hipSuccess) { set_error("hipDeviceSynchronize", e); return RSK_EDEVICE; }
+        (void)hipFree(c->ws);
+        c->ws = nullptr;
+        c->ws_n = 0;
+    }
+    hipError_t e = hipMalloc(&c->ws, ws_bytes(n));
+    if (e != hipSuccess) { set_error("hipMalloc(workspace)", e); return RSK_ENOMEM; }
+    c->ws_n = n;
+    return RSK_OK;
+}
+
+void ws_split(rsk_ctx *c, uint32_t n, uint64_t *&masks, uint32_t *&counts, uint32_t *&offsets) {
+    const uint64_t nb = (n + kBlock - 1ull) / kBlock;
+    masks = reinterpret_cast<uint64_t *>(c->ws);
+    counts = reinterpret_cast<uint32_t *>(masks + nb * kWavesPerBlock);
+    offsets = counts + nb;
+}
+
+int launch_check(const char *what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) { set_error(what, e); return RSK_EDEVICE; }
+    return RSK_OK;
+}
+
+int run_compaction(rsk_ctx *c, uint32_t n, uint64_t *masks, uint32_t *counts, uint32_t *offsets,
+                   const rsk_decode_out *out, hipStream_t s) {
+    const uint32_t nb = (uint32_t)((n + kBlock - 1ull) / kBlock);
+    (void)c;
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, counts, offsets, nb, out->n_valid);
+    int r = launch_check("k_scan");
+    if (r) return r;
+    if (out->valid_idx) {
+        hipLaunchKernelGGL(k_scatter, dim3(nb), dim3(kBlock), 0, s, masks, offsets, out->valid_idx);
+        r = launch_check("k_scatter");
+    }
+    return r;
+}
+
+bool dec_out_ok(const rsk_decode_out *o) {
+    return o && o->hlen && o->cmd && o->id && o->conv && o->conn_key && o->pay_off && o->pay_len &&
+           o->status && ((reinterpret_cast<uintptr_t>(o->id) & 7u) == 0);
+}
+
+DecOut make_dec_out(const rsk_decode_out *o, uint64_t *masks, uint32_t *counts) {
+    DecOut d;
+    d.hlen = o->hlen; d.cmd = o->cmd; d.id = o->id; d.conv = o->conv; d.key = o->conn_key;
+    d.pay_off = o->pay_off; d.pay_len = o->pay_len; d.status = o->status;
+    d.masks = masks; d.counts = counts;
+    return d;
+}
+
+}  // namespace
+
+// =============================================================================================
+// C ABI
+// =============================================================================================
+extern "C" {
+
+const char *rsk_last_error(void) { return g_last_error; }
+
+const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
+
+rsk_ctx *rsk_create(const uint8_t *key, uint32_t key_len, int device) {
+    if (!key && key_len) { snprintf(g_last_error, sizeof g_last_error, "rsk_create: null key"); return nullptr; }
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev <= 0) {
+        set_error("hipGetDeviceCount", e == hipSuccess ? hipErrorNoDevice : e);
+        return nullptr;
+    }
+    if (device < 0 || device >= ndev) {
+        snprintf(g_last_error, sizeof g_last_error, "rsk_create: device %d out of range", device);
+        return nullptr;
+    }
+    rsk_ctx *c = new rsk_ctx();
+    c->device = device;
+    c->key.assign(key, key + key_len);
+    build_sched(c->key.data(), key_len, c->ks);
+    return c;
+}
+
+void rsk_destroy(rsk_ctx *c) {
+    if (!c) return;
+    DeviceGuard g(c->device);
+    if (c->ws) (void)hipFree(c->ws);
+    if (c->shim_dev) (void)hipFree(c->shim_dev);
+    if (c->shim_host) (void)hipHostFree(c->shim_host);
+    if (c->shim_stream) (void)hipStreamDestroy(c->shim_stream);
+    delete c;
+}
+
+int rsk_reserve(rsk_ctx *c, uint32_t n_max) {
+    if (!c) return RSK_EINVAL;
+    DeviceGuard g(c->device);
+    if (!g.ok) return RSK_EDEVICE;
+    return ensure_ws(c, n_max);
+}
+
+int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_encode_out *out,
+                     void *stream) {
+    if (!c || !in || !out) return RSK_EINVAL;
+    if (n == 0) return RSK_OK;
+    if (!in->payload_arena || !in->pay_off || !in->pay_len || !in->cmd || !in->conv || !in->conn_key ||
+        !out->frame_arena || !out->frame_off || !out->status)
+        return RSK_EINVAL;
+    if (in->id && (reinterpret_cast<uintptr_t>(in->id) & 7u)) return RSK_EINVAL;
+    DeviceGuard g(c->device);
+    if (!g.ok) return RSK_EDEVICE;
+    EncArgs a;
+    a.payload = in->payload_arena; a.pay_off = in->pay_off; a.pay_len = in->pay_len; a.cmd = in->cmd;
+    a.conv = in->conv; a.conn_key = in->conn_key; a.id = in->id;
+    a.frame = out->frame_arena; a.frame_off = out->frame_off; a.status = out->status;
+    std::memcpy(&a.id_lo, in->id_uniform, 4);
+    std::memcpy(&a.id_hi, in->id_uniform + 4, 4);
+    a.n = n;
+    const uint64_t waves = (n + 63ull) / 64ull;
+    const unsigned grid = (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
+    hipLaunchKernelGGL(k_encode, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, a, c->ks);
+    return launch_check("k_encode");
+}
+
+int rsk_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *frame_arena, const uint64_t *frame_off,
+                     const uint16_t *frame_len, const uint8_t *is_tcp_close, const rsk_decode_out *out,
+                     void *stream) {
+    if (!c || !frame_arena || !frame_off || !frame_len || !dec_out_ok(out)) return RSK_EINVAL;
+    if (n == 0) {
+        if (out->n_valid) {
+            DeviceGuard g(c->device);
+            hipError_t e = hipMemsetAsync(out->n_valid, 0, sizeof(uint32_t), (hipStream_t)stream);
+            if (e != hipSuccess) { set_error("hipMemsetAsync", e); return RSK_EDEVICE; }
+        }
+        return RSK_OK;
+    }
+    DeviceGuard g(c->device);
+    if (!g.ok) return RSK_EDEVICE;
+    const bool compact = out->valid_idx || out->n_valid;
+    uint64_t *masks = nullptr;
+    uint32_t *counts = nullptr, *offsets = nullptr;
+    if (compact) {
+        int r = ensure_ws(c, n);
+        if (r) return r;
+        ws_split(c, n, masks, counts, offsets);
+    }
+    DecArgs a{frame_arena, frame_off, frame_len, is_tcp_close, n};
+    DecOut d = make_dec_out(out, masks, counts);
+    hipLaunchKernelGGL(k_decode, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, a, d, c->ks);
+    int r = launch_check("k_decode");
+    if (r || !compact) return r;
+    return run_compaction(c, n, masks, counts, offsets, out, (hipStream_t)stream);
+}
+
+int rsk_parse_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *cap_arena, const uint64_t *cap_off,
+                           const uint32_t *wire_len, const uint32_t *cap_len, int datalink, int flags,
+                           const rsk_tcpinfo_out *tcp, const rsk_decode_out *dec, void *stream) {
+    if (!c || !cap_arena || !cap_off || !wire_len || !cap_len || !tcp || !dec_out_ok(dec)) return RSK_EINVAL;
+    if (datalink != RSK_DLT_EN10MB && datalink != RSK_DLT_NULL) return RSK_EINVAL;  // RawTcp.cpp:161-164
+    if (!tcp->src || !tcp->dst || !tcp->sp || !tcp->dp || !tcp->seq || !tcp->ack || !tcp->flag ||
+        !tcp->parse_status || !tcp->cap_pay_off || !tcp->cap_pay_len)
+        return RSK_EINVAL;
+    DeviceGuard g(c->device);
+    if (!g.ok) return RSK_EDEVICE;
+    if (n == 0) {
+        if (dec->n_valid) {
+            hipError_t e = hipMemsetAsync(dec->n_valid, 0, sizeof(uint32_t), (hipStream_t)stream);
+            if (e != hipSuccess) { set_error("hipMemsetAsync", e); return RSK_EDEVICE; }
+        }
+        return RSK_OK;
+    }
+    const bool compact = dec->valid_idx || dec->n_valid;
+    uint64_t *masks = nullptr;
+    uint32_t *counts = nullptr, *offsets = nullptr;
+    if (compact) {
+        int r = ensure_ws(c, n);
+        if (r) return r;
+        ws_split(c, n, masks, counts, offsets);
+    }
+    ParseArgs a;
+    a.cap = cap_arena; a.cap_off = cap_off; a.wire_len = wire_len; a.cap_len = cap_len;
+    a.src = tcp->src; a.dst = tcp->dst; a.sp = tcp->sp; a.dp = tcp->dp; a.seq = tcp->seq; a.ack = tcp->ack;
+    a.flag = tcp->flag; a.pst = tcp->parse_status; a.cpo = tcp->cap_pay_off; a.cpl = tcp->cap_pay_len;
+    a.datalink = datalink; a.flags = flags; a.n = n;
+    DecOut d = make_dec_out(dec, masks, counts);
+    hipLaunchKernelGGL(k_parse_decode, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, a, d, c->ks);
+    int r = launch_check("k_parse_decode");
+    if (r || !compact) return r;
+    return run_compaction(c, n, masks, counts, offsets, dec, (hipStream_t)stream);
+}
+
+int rsk_tcpinfo_encode_batch(rsk_ctx *c, uint32_t n, const uint32_t *src, const uint32_t *dst,
+                             const uint16_t *sp, const uint16_t *dp, const uint32_t *seq,
+                             const uint32_t *ack, const uint8_t *flag, uint8_t *rec, void *stream) {
+    if (!c || !src || !dst || !sp || !dp || !seq || !ack || !flag || !rec) return RSK_EINVAL;
+    if (n == 0) return RSK_OK;
+    DeviceGuard g(c->device);
+    if (!g.ok) return RSK_EDEVICE;
+    TcpRecArgs a{src, dst, sp, dp, seq, ack, flag, rec, n};
+    hipLaunchKernelGGL(k_tcpinfo_encode, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, a);
+    return launch_check("k_tcpinfo_encode");
+}
+
+int rsk_fill_splitmix(void *dst, uint64_t nbytes, uint64_t seed, void *stream) {
+    if (!dst && nbytes) return RSK_EINVAL;
+    if (nbytes == 0) return RSK_OK;
+    const uint64_t nw = nbytes / 8u + 1u;
+    const unsigned grid = (unsigned)std::min<uint64_t>((nw + kBlock - 1) / kBlock, 8192u);
+    hipLaunchKernelGGL(k_fill_splitmix, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream,
+                       reinterpret_cast<uint8_t *>(dst), nbytes, seed);
+    return launch_check("k_fill_splitmix");
+}
+
+uint64_t rsk_key_for_tcp(uint16_t sp, uint16_t dp) {
+    return 0x10000000ull | ((uint64_t)dp << 16) | (uint64_t)sp;  // KeyGenerator.cpp:16-25
+}
+uint64_t rsk_key_for_udp(uint16_t sp, uint16_t dp) {
+    return 0x20000000ull | ((uint64_t)dp << 16) | (uint64_t)sp;  // KeyGenerator.cpp:27-36
+}
+
+}  // extern "C"
+
+// ---- single-packet shims ----------------------------------------------------------------------
+namespace {
+int shim_init(rsk_ctx *c) {
+    if (c->shim_dev && c->shim_host && c->shim_stream) return RSK_OK;
+    DeviceGuard g(c->device);
+    if (!g.ok) return RSK_EDEVICE;
+    hipError_t e;
+    if (!c->shim_dev && (e = hipMalloc(&c->shim_dev, sizeof(ShimIO))) != hipSuccess) { set_error("hipMalloc", e); return RSK_ENOMEM; }
+    if (!c->shim_host && (e = hipHostMalloc(&c->shim_host, sizeof(ShimIO))) != hipSuccess) { set_error("hipHostMalloc", e); return RSK_ENOMEM; }
+    if (!c->shim_stream && (e = hipStreamCreateWithFlags(&c->shim_stream, hipStreamNonBlocking)) != hipSuccess) {
+        set_error("hipStreamCreate", e);
+        return RSK_EDEVICE;
+    }
+    return RSK_OK;
+}
+
+int shim_run(rsk_ctx *c, int op, int len_arg) {
+    DeviceGuard g(c->device);
+    if (!g.ok) return RSK_EDEVICE;
+    hipError_t e;
+    if ((e = hipMemcpyAsync(c->shim_dev, c->shim_host, sizeof(ShimIO), hipMemcpyHostToDevice, c->shim_stream)) != hipSuccess) {
+        set_error("hipMemcpyAsync", e);
+        return RSK_EDEVICE;
+    }
+    hipLaunchKernelGGL(k_shim, dim3(1), dim3(64), 0, c->shim_stream, c->shim_dev, op, len_arg, c->ks);
+    if (launch_check("k_shim")) return RSK_EDEVICE;
+    if ((e = hipMemcpyAsync(c->shim_host, c->shim_dev, sizeof(ShimIO), hipMemcpyDeviceToHost, c->shim_stream)) != hipSuccess) {
+        set_error("hipMemcpyAsync", e);
+        return RSK_EDEVICE;
+    }
+    if ((e = hipStreamSynchronize(c->shim_stream)) != hipSuccess) { set_error("hipStreamSynchronize", e); return RSK_EDEVICE; }
+    return RSK_OK;
+}
+}  // namespace
+
+extern "C" {
+
+uint8_t *rsk_compute_hash(rsk_ctx *c, uint8_t *tag_out, const uint8_t *data, int data_len) {
+    if (!c || !tag_out || !data || data_len <= 0) return nullptr;  // rhash.cpp:21 asserts this
+    std::lock_guard<std::mutex> lk(c->shim_mu);
+    if (shim_init(c) != RSK_OK) return nullptr;
+    c->shim_host->buf[0] = data[0];
+    if (shim_run(c, 0, 0) != RSK_OK) return nullptr;
+    std::memcpy(tag_out, c->shim_host->buf + 8, 8);
+    return tag_out + RSK_HASH_BUF_SIZE;
+}
+
+int rsk_hash_equal(rsk_ctx *c, const uint8_t *tag, const uint8_t *data, int data_len) {
+    if (!c || !tag || !data || data_len <= 0) return 0;  // rhash.cpp:73-75
+    std::lock_guard<std::mutex> lk(c->shim_mu);
+    if (shim_init(c) != RSK_OK) return 0;
+    std::memcpy(c->shim_host->buf, tag, 8);
+    c->shim_host->buf[8] = data[0];
+    if (shim_run(c, 1, 0) != RSK_OK) return 0;
+    return c->shim_host->ret;
+}
+
+uint8_t *rsk_enchead_enc2buf(rsk_ctx *c, uint8_t *p, int buf_len, uint8_t cmd, const uint8_t id[8],
+                             uint32_t conv, uint64_t conn_key) {
+    if (!c || !p || buf_len < RSK_ENC_HEAD_SIZE || !id) return nullptr;  // EncHead.cpp:10
+    std::lock_guard<std::mutex> lk(c->shim_mu);
+    if (shim_init(c) != RSK_OK) return nullptr;
+    uint8_t *b = c->shim_host->buf;
+    b[0] = cmd;
+    std::memcpy(b + 1, id, 8);
+    std::memcpy(b + 12, &conv, 4);
+    std::memcpy(b + 16, &conn_key, 8);
+    if (shim_run(c, 2, 0) != RSK_OK) return nullptr;
+    std::memcpy(p, c->shim_host->buf + 32, RSK_ENC_HEAD_SIZE);
+    return p + RSK_ENC_HEAD_SIZE;
+}
+
+const uint8_t *rsk_enchead_decodebuf(rsk_ctx *c, const uint8_t *p, int buf_len, uint8_t *len,
+                                     uint8_t *cmd, uint8_t id[8], uint32_t *conv, uint64_t *conn_key) {
+    if (!c || !p || buf_len < RSK_ENC_HEAD_SIZE) return nullptr;  // EncHead.cpp:40
+    std::lock_guard<std::mutex> lk(c->shim_mu);
+    if (shim_init(c) != RSK_OK) return nullptr;
+    std::memcpy(c->shim_host->buf, p, RSK_ENC_HEAD_SIZE);
+    if (shim_run(c, 3, buf_len) != RSK_OK || c->shim_host->ret < 0) return nullptr;
+    const uint8_t *h = c->shim_host->buf + 32;
+    if (len) *len = h[0];
+    if (cmd) *cmd = h[1];
+    if (id) std::memcpy(id, h + 2, 8);
+    if (conv) std::memcpy(conv, h + 10, 4);
+    if (conn_key) std::memcpy(conn_key, h + 14, 8);
+    return p + c->shim_host->ret;
+}
+
+}  // extern "C"

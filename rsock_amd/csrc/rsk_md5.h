@@ -1,0 +1,105 @@
+// rsk_md5.h — MD5 compression (RFC 1321 §3.4) for the tag path, host + device.
+//
+// The tag is MD5(key || payload[0])[8..15] (util/rhash.cpp:20-41).  On the device the key part of
+// the message schedule is uniform per launch (kernel arguments -> SGPRs) and only the word holding
+// payload[0] differs per lane, so one tag costs one compression for key_len <= 54 (two otherwise).
+// Round constants and rotations are compile-time literals: after full unrolling every K[i] is an
+// instruction immediate, which needs no LDS traffic and no VGPRs ("MD5
+// constants: immediates vs LDS").
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rsk {
+
+struct Md5Consts {
+    static constexpr uint32_t K[64] = {
+        0xd76aa478, 0xe8c7b756, 0x242070db, 0xc1bdceee, 0xf57c0faf, 0x4787c62a, 0xa8304613, 0xfd469501,
+        0x698098d8, 0x8b44f7af, 0xffff5bb1, 0x895cd7be, 0x6b901122, 0xfd987193, 0xa679438e, 0x49b40821,
+        0xf61e2562, 0xc040b340, 0x265e5a51, 0xe9b6c7aa, 0xd62f105d, 0x02441453, 0xd8a1e681, 0xe7d3fbc8,
+        0x21e1cde6, 0xc33707d6, 0xf4d50d87, 0x455a14ed, 0xa9e3e905, 0xfcefa3f8, 0x676f02d9, 0x8d2a4c8a,
+        0xfffa3942, 0x8771f681, 0x6d9d6122, 0xfde5380c, 0xa4beea44, 0x4bdecfa9, 0xf6bb4b60, 0xbebfbc70,
+        0x289b7ec6, 0xeaa127fa, 0xd4ef3085, 0x04881d05, 0xd9d4d039, 0xe6db99e5, 0x1fa27cf8, 0xc4ac5665,
+        0xf4292244, 0x432aff97, 0xab9423a7, 0xfc93a039, 0x655b59c3, 0x8f0ccc92, 0xffeff47d, 0x85845dd1,
+        0x6fa87e4f, 0xfe2ce6e0, 0xa3014314, 0x4e0811a1, 0xf7537e82, 0xbd3af235, 0x2ad7d2bb, 0xeb86d391};
+};
+
+__host__ __device__ __forceinline__ uint32_t rotl(uint32_t x, int s) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_alignbit(x, x, 32 - s);  // v_alignbit_b32: funnel shift == rotate
+#else
+    return (x << s) | (x >> (32 - s));
+#endif
+}
+
+// One MD5 step; the round function and message index are resolved at compile time.
+template <int I>
+__host__ __device__ __forceinline__ void md5_step(uint32_t &a, uint32_t b, uint32_t c, uint32_t d,
+                                                  const uint32_t (&m)[16]) {
+    constexpr int R = I / 16;
+    constexpr int G = R == 0 ? I : R == 1 ? (5 * I + 1) & 15 : R == 2 ? (3 * I + 5) & 15 : (7 * I) & 15;
+    constexpr int S0[4] = {7, 12, 17, 22}, S1[4] = {5, 9, 14, 20}, S2[4] = {4, 11, 16, 23},
+                  S3[4] = {6, 10, 15, 21};
+    constexpr int S = R == 0 ? S0[I & 3] : R == 1 ? S1[I & 3] : R == 2 ? S2[I & 3] : S3[I & 3];
+    uint32_t f;
+    if constexpr (R == 0) f = d ^ (b & (c ^ d));        // F = (b&c) | (~b&d)
+    else if constexpr (R == 1) f = c ^ (d & (b ^ c));   // G = (b&d) | (c&~d)
+    else if constexpr (R == 2) f = b ^ c ^ d;           // H
+    else f = c ^ (b | ~d);                              // I
+    a = b + rotl(a + f + Md5Consts::K[I] + m[G], S);
+}
+
+template <int I>
+__host__ __device__ __forceinline__ void md5_steps(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d,
+                                                   const uint32_t (&m)[16]) {
+    if constexpr (I < 64) {
+        // state rotation a<-d, d<-c, c<-b, b<-new: expressed by rotating the argument roles
+        md5_step<I + 0>(a, b, c, d, m);
+        md5_step<I + 1>(d, a, b, c, m);
+        md5_step<I + 2>(c, d, a, b, m);
+        md5_step<I + 3>(b, c, d, a, m);
+        md5_steps<I + 4>(a, b, c, d, m);
+    }
+}
+
+// st <- compress(st, m)
+__host__ __device__ __forceinline__ void md5_compress(uint32_t (&st)[4], const uint32_t (&m)[16]) {
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
+    md5_steps<0>(a, b, c, d, m);
+    st[0] += a;
+    st[1] += b;
+    st[2] += c;
+    st[3] += d;
+}
+
+// Per-key message schedule, precomputed on the host by rsk_create (rsk_kernels.hip).
+struct KeySched {
+    uint32_t mid[4];   // chaining state after every block that holds only key bytes
+    uint32_t blk[16];  // words of the block that holds payload[0], with that byte = 0
+    uint32_t pad[16];  // the following padding/length block (used when two_blocks)
+    int32_t bword;     // word index of payload[0] inside blk
+    int32_t bshift;    // bit position of payload[0] inside that word
+    int32_t two_blocks;
+    int32_t _pad0;
+};
+
+// Tag words (digest bytes 8..11 and 12..15, little-endian) for payload byte b.
+__host__ __device__ __forceinline__ void md5_tag(const KeySched &ks, uint32_t b, uint32_t &t0,
+                                                 uint32_t &t1) {
+    uint32_t m[16];
+    const uint32_t bb = b << ks.bshift;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) m[w] = ks.blk[w] | (w == ks.bword ? bb : 0u);
+    uint32_t st[4] = {ks.mid[0], ks.mid[1], ks.mid[2], ks.mid[3]};
+    md5_compress(st, m);
+    if (ks.two_blocks) {
+        uint32_t p[16];
+#pragma unroll
+        for (int w = 0; w < 16; ++w) p[w] = ks.pad[w];
+        md5_compress(st, p);
+    }
+    t0 = st[2];
+    t1 = st[3];
+}
+
+}  // namespace rsk

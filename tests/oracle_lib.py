@@ -1,0 +1,283 @@
+"""TEST INFRASTRUCTURE: ctypes wrappers over oracle/liboracle.so (clean-room C restatement) and
+oracle/_ref/librsk_ref.so (the reference's own codec sources compiled here).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this module.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle.so")
+REF_SO = os.path.join(ROOT, "oracle", "_ref", "librsk_ref.so")
+
+_vp = ctypes.c_void_p
+
+
+def _p(a: np.ndarray | None):
+    return None if a is None else a.ctypes.data
+
+
+class OrcDec(ctypes.Structure):
+    _fields_ = [("hlen", ctypes.c_uint8), ("cmd", ctypes.c_uint8), ("id", ctypes.c_uint8 * 8),
+                ("conv", ctypes.c_uint32), ("conn_key", ctypes.c_uint64), ("pay_off", ctypes.c_uint16),
+                ("pay_len", ctypes.c_uint16), ("status", ctypes.c_int8)]
+
+
+class OrcTcpInfo(ctypes.Structure):
+    _fields_ = [("src", ctypes.c_uint32), ("dst", ctypes.c_uint32), ("sp", ctypes.c_uint16),
+                ("dp", ctypes.c_uint16), ("seq", ctypes.c_uint32), ("ack", ctypes.c_uint32),
+                ("flag", ctypes.c_uint8), ("parse_status", ctypes.c_int8),
+                ("cap_pay_off", ctypes.c_uint16), ("cap_pay_len", ctypes.c_uint16)]
+
+
+class Oracle:
+    def __init__(self, path: str = ORACLE_SO):
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} missing: run `make -C oracle`")
+        L = self.L = ctypes.CDLL(path)
+        L.orc_md5.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]
+        L.orc_compute_hash.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint8]
+        L.orc_hash_equal.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
+                                     ctypes.c_int]
+        L.orc_enchead_encode.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_uint8, ctypes.c_char_p,
+                                         ctypes.c_uint32, ctypes.c_uint64]
+        L.orc_enchead_decode.argtypes = [ctypes.c_char_p, ctypes.c_int, _vp, _vp, _vp, _vp, _vp]
+        L.orc_rconn_output.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_int,
+                                       ctypes.c_uint8, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint64,
+                                       ctypes.c_char_p]
+        L.orc_rconn_onrecv.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_int,
+                                       ctypes.c_int, ctypes.POINTER(OrcDec)]
+        L.orc_rawinput.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+                                   ctypes.c_int, ctypes.POINTER(OrcTcpInfo)]
+        L.orc_tcpinfo_encode.argtypes = [ctypes.POINTER(OrcTcpInfo), ctypes.c_char_p]
+        L.orc_tcpinfo_decode.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(OrcTcpInfo)]
+        L.orc_key_for_tcp.restype = ctypes.c_uint64
+        L.orc_key_for_tcp.argtypes = [ctypes.c_uint16, ctypes.c_uint16]
+        L.orc_key_for_udp.restype = ctypes.c_uint64
+        L.orc_key_for_udp.argtypes = [ctypes.c_uint16, ctypes.c_uint16]
+        L.orc_splitmix64_at.restype = ctypes.c_uint64
+        L.orc_splitmix64_at.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
+        L.orc_fill_splitmix.argtypes = [_vp, ctypes.c_uint64, ctypes.c_uint64]
+        L.orc_encode_batch.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32] + [_vp] * 11 + [ctypes.c_int]
+        L.orc_decode_batch.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32] + [_vp] * 14 + [ctypes.c_int]
+        L.orc_parse_decode_batch.argtypes = ([ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, _vp, _vp, _vp,
+                                              _vp, ctypes.c_int, ctypes.c_int] + [_vp] * 20)
+
+    # ---- scalar ----
+    def md5(self, msg: bytes) -> bytes:
+        out = ctypes.create_string_buffer(16)
+        self.L.orc_md5(msg, len(msg), out)
+        return out.raw
+
+    def tag(self, key: bytes, b: int) -> bytes:
+        out = ctypes.create_string_buffer(8)
+        self.L.orc_compute_hash(out, key, len(key), b)
+        return out.raw
+
+    def hash_equal(self, tag: bytes, key: bytes, data: bytes | None, data_len: int) -> bool:
+        return bool(self.L.orc_hash_equal(tag, key, len(key), data, data_len))
+
+    def enchead_encode(self, buf_len: int, cmd: int, idb: bytes, conv: int, key: int):
+        out = ctypes.create_string_buffer(max(buf_len, 23))
+        r = self.L.orc_enchead_encode(out, buf_len, cmd, idb, conv, key)
+        return None if r < 0 else out.raw[:23]
+
+    def enchead_decode(self, buf: bytes, buf_len: int):
+        ln, cmd = ctypes.c_uint8(), ctypes.c_uint8()
+        idb = ctypes.create_string_buffer(8)
+        conv, key = ctypes.c_uint32(), ctypes.c_uint64()
+        r = self.L.orc_enchead_decode(bytes(buf), buf_len, ctypes.addressof(ln), ctypes.addressof(cmd),
+                                      ctypes.addressof(idb), ctypes.addressof(conv), ctypes.addressof(key))
+        if r < 0:
+            return None
+        return ln.value, cmd.value, idb.raw, conv.value, key.value
+
+    def rconn_output(self, key: bytes, payload: bytes, cmd: int, idb: bytes, conv: int, ckey: int):
+        frame = ctypes.create_string_buffer(1600)
+        st = self.L.orc_rconn_output(key, len(key), payload, len(payload), cmd, idb, conv, ckey, frame)
+        return st, (frame.raw[:st] if st > 0 else b"")
+
+    def rconn_onrecv(self, key: bytes, frame: bytes, nread: int | None = None, close: bool = False) -> OrcDec:
+        d = OrcDec()
+        if nread is None:
+            nread = len(frame)
+        self.L.orc_rconn_onrecv(key, len(key), bytes(frame), nread, int(close), ctypes.byref(d))
+        return d
+
+    def rawinput(self, pkt: bytes, wire_len: int, cap_len: int, datalink: int, flags: int) -> OrcTcpInfo:
+        t = OrcTcpInfo()
+        self.L.orc_rawinput(bytes(pkt), wire_len, cap_len, datalink, flags, ctypes.byref(t))
+        return t
+
+    def tcpinfo_encode(self, t: OrcTcpInfo) -> bytes:
+        out = ctypes.create_string_buffer(21)
+        self.L.orc_tcpinfo_encode(ctypes.byref(t), out)
+        return out.raw
+
+    def key_for_tcp(self, sp: int, dp: int) -> int:
+        return self.L.orc_key_for_tcp(sp, dp)
+
+    def key_for_udp(self, sp: int, dp: int) -> int:
+        return self.L.orc_key_for_udp(sp, dp)
+
+    def splitmix_bytes(self, seed: int, n: int) -> np.ndarray:
+        out = np.empty(n, np.uint8)
+        self.L.orc_fill_splitmix(_p(out), n, seed)
+        return out
+
+    # ---- batch (numpy SoA) ----
+    def encode_batch(self, key: bytes, payload: np.ndarray, d, id_uniform: bytes, nthreads: int = 8,
+                     frame_bytes: int | None = None, idarr: np.ndarray | None = None):
+        n = d.n
+        if frame_bytes is None:
+            frame_bytes = n * d.frame_pitch
+        frames = np.zeros(frame_bytes, np.uint8)
+        status = np.zeros(n, np.int32)
+        idu = np.frombuffer(bytes(id_uniform)[:8].ljust(8, b"\0"), np.uint8).copy()
+        arrs = [np.ascontiguousarray(x) for x in (payload, d.pay_off.astype(np.uint64), d.pay_len.astype(np.uint16),
+                                                   d.cmd.astype(np.uint8), d.conv.astype(np.uint32),
+                                                   d.conn_key.astype(np.uint64))]
+        fo = np.ascontiguousarray(d.frame_off.astype(np.uint64))  # keep alive across the call
+        self.L.orc_encode_batch(key, len(key), n, *[_p(a) for a in arrs], _p(idarr), _p(idu), _p(frames),
+                                _p(fo), _p(status), nthreads)
+        return frames, status
+
+    def decode_batch(self, key: bytes, frames: np.ndarray, frame_off: np.ndarray, frame_len: np.ndarray,
+                     is_tcp_close: np.ndarray | None = None, nthreads: int = 8) -> dict:
+        n = len(frame_len)
+        out = {
+            "hlen": np.zeros(n, np.uint8), "cmd": np.zeros(n, np.uint8), "id": np.zeros(8 * n, np.uint8),
+            "conv": np.zeros(n, np.uint32), "conn_key": np.zeros(n, np.uint64),
+            "pay_off": np.zeros(n, np.uint16), "pay_len": np.zeros(n, np.uint16),
+            "status": np.zeros(n, np.int8), "valid_idx": np.zeros(max(n, 1), np.uint32),
+        }
+        nv = ctypes.c_uint32()
+        fo = np.ascontiguousarray(frame_off.astype(np.uint64))
+        fl = np.ascontiguousarray(frame_len.astype(np.uint16))
+        cl = None if is_tcp_close is None else np.ascontiguousarray(is_tcp_close.astype(np.uint8))
+        self.L.orc_decode_batch(key, len(key), n, _p(frames), _p(fo), _p(fl), _p(cl),
+                                *[_p(out[k]) for k in ("hlen", "cmd", "id", "conv", "conn_key", "pay_off",
+                                                       "pay_len", "status", "valid_idx")],
+                                ctypes.addressof(nv), nthreads)
+        out["n_valid"] = nv.value
+        return out
+
+    def parse_decode_batch(self, key: bytes, cap: np.ndarray, cap_off, wire_len, cap_len, datalink: int,
+                           flags: int) -> dict:
+        n = len(wire_len)
+        spec = [("src", np.uint32), ("dst", np.uint32), ("sp", np.uint16), ("dp", np.uint16),
+                ("seq", np.uint32), ("ack", np.uint32), ("flag", np.uint8), ("parse_status", np.int8),
+                ("cap_pay_off", np.uint16), ("cap_pay_len", np.uint16), ("hlen", np.uint8), ("cmd", np.uint8)]
+        out = {k: np.zeros(n, dt) for k, dt in spec}
+        out["id"] = np.zeros(8 * n, np.uint8)
+        for k, dt in (("conv", np.uint32), ("conn_key", np.uint64), ("pay_off", np.uint16),
+                      ("pay_len", np.uint16), ("status", np.int8)):
+            out[k] = np.zeros(n, dt)
+        out["valid_idx"] = np.zeros(max(n, 1), np.uint32)
+        nv = ctypes.c_uint32()
+        co = np.ascontiguousarray(np.asarray(cap_off, np.uint64))
+        wl = np.ascontiguousarray(np.asarray(wire_len, np.uint32))
+        cl = np.ascontiguousarray(np.asarray(cap_len, np.uint32))
+        order = ["src", "dst", "sp", "dp", "seq", "ack", "flag", "parse_status", "cap_pay_off", "cap_pay_len",
+                 "hlen", "cmd", "id", "conv", "conn_key", "pay_off", "pay_len", "status", "valid_idx"]
+        self.L.orc_parse_decode_batch(key, len(key), n, _p(cap), _p(co), _p(wl), _p(cl), datalink, flags,
+                                      *[_p(out[k]) for k in order], ctypes.addressof(nv))
+        out["n_valid"] = nv.value
+        return out
+
+
+class RefOracle:
+    """The reference's own functions (oracle/_ref/librsk_ref.so), for pinning and the CPU baseline."""
+
+    def __init__(self, path: str = REF_SO):
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        L = self.L = ctypes.CDLL(path)
+        L.ref_compute_hash.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+        L.ref_hash_equal.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+        L.ref_enc2buf.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_uint8, ctypes.c_char_p, ctypes.c_uint32,
+                                  ctypes.c_uint64]
+        L.ref_decodebuf.argtypes = [ctypes.c_char_p, ctypes.c_int, _vp, _vp, _vp, _vp]
+        L.ref_rconn_output.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_uint8,
+                                       ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_char_p]
+        L.ref_rconn_onrecv.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
+                                       _vp, _vp, _vp, _vp, _vp, _vp, _vp]
+        L.ref_key_for_tcp.restype = ctypes.c_uint64
+        L.ref_key_for_tcp.argtypes = [ctypes.c_uint16, ctypes.c_uint16]
+        L.ref_key_for_udp.restype = ctypes.c_uint64
+        L.ref_key_for_udp.argtypes = [ctypes.c_uint16, ctypes.c_uint16]
+        L.ref_tcpinfo_encode.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint16, ctypes.c_uint16,
+                                         ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint8, ctypes.c_char_p,
+                                         ctypes.c_int]
+        L.ref_tcpinfo_decode.argtypes = [ctypes.c_char_p, ctypes.c_int, _vp]
+        L.ref_bench_codec.restype = ctypes.c_uint64
+        L.ref_bench_codec.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_uint32] + [_vp] * 9 + [ctypes.c_int]
+
+    def tag(self, key: bytes, data: bytes) -> bytes:
+        out = ctypes.create_string_buffer(8)
+        self.L.ref_compute_hash(out, key, len(key), data, len(data))
+        return out.raw
+
+    def hash_equal(self, tag: bytes, key: bytes, data: bytes | None, data_len: int) -> bool:
+        return bool(self.L.ref_hash_equal(tag, key, len(key), data, data_len))
+
+    def enc2buf(self, buf_len: int, cmd: int, idb: bytes, conv: int, key: int):
+        out = ctypes.create_string_buffer(max(buf_len, 23))
+        r = self.L.ref_enc2buf(out, buf_len, cmd, idb, conv, key)
+        return None if r < 0 else out.raw[:r]
+
+    def decodebuf(self, buf: bytes, buf_len: int):
+        cmd = ctypes.c_uint8()
+        idb = ctypes.create_string_buffer(8)
+        conv, key = ctypes.c_uint32(), ctypes.c_uint64()
+        r = self.L.ref_decodebuf(bytes(buf), buf_len, ctypes.addressof(cmd), ctypes.addressof(idb),
+                                 ctypes.addressof(conv), ctypes.addressof(key))
+        if r < 0:
+            return None
+        return bytes(buf)[0], cmd.value, idb.raw, conv.value, key.value
+
+    def rconn_output(self, key: bytes, payload: bytes, cmd: int, idb: bytes, conv: int, ckey: int):
+        frame = ctypes.create_string_buffer(1600)
+        st = self.L.ref_rconn_output(key, len(key), payload, len(payload), cmd, idb, conv, ckey, frame)
+        return st, (frame.raw[:st] if st > 0 else b"")
+
+    def rconn_onrecv(self, key: bytes, frame: bytes, nread: int | None = None, close: bool = False):
+        if nread is None:
+            nread = len(frame)
+        hlen, cmd = ctypes.c_uint8(), ctypes.c_uint8()
+        idb = ctypes.create_string_buffer(8)
+        conv, ckey = ctypes.c_uint32(), ctypes.c_uint64()
+        po, pl = ctypes.c_int(), ctypes.c_int()
+        st = self.L.ref_rconn_onrecv(key, len(key), bytes(frame), nread, int(close), ctypes.addressof(hlen),
+                                     ctypes.addressof(cmd), ctypes.addressof(idb), ctypes.addressof(conv),
+                                     ctypes.addressof(ckey), ctypes.addressof(po), ctypes.addressof(pl))
+        if st != 1:
+            return st, None
+        return st, (hlen.value, cmd.value, idb.raw, conv.value, ckey.value, po.value, pl.value)
+
+    def key_for_tcp(self, sp: int, dp: int) -> int:
+        return self.L.ref_key_for_tcp(sp, dp)
+
+    def key_for_udp(self, sp: int, dp: int) -> int:
+        return self.L.ref_key_for_udp(sp, dp)
+
+    def tcpinfo_encode(self, src, dst, sp, dp, seq, ack, flag) -> bytes:
+        out = ctypes.create_string_buffer(64)
+        r = self.L.ref_tcpinfo_encode(src, dst, sp, dp, seq, ack, flag, out, 64)
+        return out.raw[:r]
+
+    def bench_codec(self, key: bytes, payload: np.ndarray, d, idb: bytes, frames: np.ndarray, nthreads: int) -> int:
+        arrs = [np.ascontiguousarray(x) for x in (d.pay_off.astype(np.uint64), d.pay_len.astype(np.uint16),
+                                                   d.cmd.astype(np.uint8), d.conv.astype(np.uint32),
+                                                   d.conn_key.astype(np.uint64))]
+        fo = np.ascontiguousarray(d.frame_off.astype(np.uint64))
+        return self.L.ref_bench_codec(key, len(key), d.n, _p(payload), *[_p(a) for a in arrs], idb, _p(frames),
+                                      _p(fo), nthreads)
+
+
+def ref_available() -> bool:
+    return os.path.exists(REF_SO)
