@@ -1,0 +1,237 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident EncHead+MD5 encode then decode+verify+compact (BASELINE.json metric).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3] [--no-cpu-baseline]
+
+One step = one pass of the hot path over one batch: k_encode (RConn::Output framing of every
+packet) followed by k_decode + compaction (RConn::OnRecv of every frame), inputs resident in HBM.
+N > 1 runs under torch.distributed.run, one rank per GPU, each rank on its own shard of packets
+(weak scaling, no data-path collective; the only collectives are the timing barrier/max).
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Mpkt/s + GiB/s device-resident EncHead+MD5 encode/decode at 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def enc_bytes_per_pkt(p: int) -> int:
+    """Algorithmic bytes of k_encode per packet: reads payload P, cmd 1,
+    conv 4, connKey 8, pay_len 2, pay_off 8, frame_off 8; writes frame 31+P, status 4."""
+    return p + 1 + 4 + 8 + 2 + 8 + 8 + (31 + p) + 4
+
+
+def dec_bytes_per_pkt() -> int:
+    """Algorithmic bytes of decode per packet: reads frame[0..32) 32, frame_off 8, frame_len 2;
+    writes hlen 1, cmd 1, id 8, conv 4, connKey 8, pay_off 2, pay_len 2, status 1, valid_idx 4
+    (+ the ballot mask, 1/8 B per packet, rounded out)."""
+    return 32 + 8 + 2 + 1 + 1 + 8 + 4 + 8 + 2 + 2 + 1 + 4
+
+
+def load_traffic(cfg: str, n: int) -> dict | None:
+    """HBM traffic per k_encode launch measured by tools/pmc_traffic.py (separate rocprofv3 --pmc
+    passes, gfx950 FETCH_SIZE x2 correction), if a matching record exists under profiles/."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        rec = json.load(open(path))
+    except Exception:
+        return None
+    if rec.get("config") != cfg or int(rec.get("packets", -1)) != n:
+        return None
+    return rec
+
+
+def cpu_baseline(cfg: str, n_sample: int, min_seconds: float) -> dict:
+    """The reference's own codec (oracle/_ref, compiled from /root/reference sources) or, if that
+    was not built, the C restatement, timed on this host's cores over a bounded sample."""
+    from rsock_amd import workload
+    from tests import oracle_lib
+
+    threads = min(16, len(os.sched_getaffinity(0)))
+    d = workload.describe(cfg, 0, n_sample)
+    payload = workload.payload_bytes_np(d)
+    frames = np.zeros(d.n * d.frame_pitch, np.uint8)
+    key = b"hello135"
+    if oracle_lib.ref_available():
+        ref = oracle_lib.RefOracle()
+        run = lambda: ref.bench_codec(key, payload, d, workload.ID_UNIFORM, frames, threads)  # noqa: E731
+        kind = "reference"
+    else:
+        orc = oracle_lib.Oracle()
+
+        def run():
+            fr, st = orc.encode_batch(key, payload, d, workload.ID_UNIFORM, nthreads=threads)
+            orc.decode_batch(key, fr, d.frame_off, d.frame_len, nthreads=threads)
+
+        kind = "port"
+    run()  # warm (page faults on the frame arena)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        run()
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= min_seconds:
+            break
+    pkts = reps * d.n
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {
+        "value": round(pkts / el / 1e6, 3),
+        "unit": "Mpkt/s",
+        "cores": threads,
+        "kind": kind,
+        "sample": f"{d.n} packets of {cfg.upper()} ({int(d.pay_len[0])}-B payloads) x {reps} passes, "
+                  f"{el:.1f} s wall; per packet: RConn::Output framing (compute_hash + Enc2Buf + memcpy into "
+                  f"a zeroed 1500-B buffer) then DecodeBuf + hash_equal; {threads} threads; {cpu_model}",
+    }
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4"])
+    ap.add_argument("--packets", type=int, default=0, help="packets per GPU (default: the config's)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=1 << 20)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from rsock_amd import codec as rc
+    from rsock_amd import workload
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    cfg = args.config
+    n = args.packets or workload.CONFIGS[cfg][1]
+    # weak scaling: rank r owns packets [r*n, (r+1)*n) of the config's global stream
+    d = workload.describe(cfg, rank * n, (rank + 1) * n, n=world * n)
+    w = workload.DeviceWorkload(d, dev)
+    cx = rc.Codec(b"hello135", local)
+    cx.reserve(d.n)
+    stream = torch.cuda.current_stream()
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        cx.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
+                        w.status, id_uniform=workload.ID_UNIFORM, stream=stream)
+        if ev is not None:
+            ev[1].record(stream)
+        cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, w.dec, stream=stream)
+        if ev is not None:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # correctness gate on the measured data: every packet must verify
+    nv = int(w.dec.n_valid.item())
+    expect_valid = int(((d.pay_len >= 1) & (d.pay_len <= 1469)).sum())
+    if nv != expect_valid:
+        raise SystemExit(f"bench: decode verified {nv} of {expect_valid} packets")
+
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed_max = float(t.item())
+
+    enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    total_pkts = world * d.n * args.steps
+    mpkts = total_pkts / elapsed_max / 1e6
+    p = int(d.pay_len[0]) if workload.CONFIGS[cfg][2] == workload.CONFIGS[cfg][3] else int(d.pay_len.mean())
+    bytes_step = d.n * (enc_bytes_per_pkt(p) + dec_bytes_per_pkt())
+    enc_bytes = d.n * enc_bytes_per_pkt(p)
+    achieved = enc_bytes / (enc_ms * 1e-3) / 1e9
+
+    if rank == 0:
+        tr = load_traffic(cfg, d.n)
+        line = {
+            "metric": METRIC,
+            "value": round(mpkts, 2),
+            "unit": "Mpkt/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (splitmix64 payloads/fields, SURVEY.md §8d)",
+            "config": {
+                "workload": f"{cfg.upper()}: {d.n} packets/GPU, {p}-B payloads, encode(tag+EncHead+copy) then "
+                            f"decode+verify+compact, device-resident",
+                "packets_per_gpu": d.n,
+                "payload_bytes": p,
+                "key": "hello135",
+                "parallelism": f"shard{world} (no collective)",
+            },
+            "gib_per_s": round(world * bytes_step * args.steps / elapsed_max / 2**30, 2),
+            "kernels_ms": {"k_encode": round(enc_ms, 4), "decode+compact": round(dec_ms, 4)},
+            "roofline": {
+                "kernel": "k_encode",
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None if tr is None else tr["bytes_per_launch"],
+                "algorithmic_bytes_per_launch": enc_bytes,
+            },
+        }
+        if tr is not None:
+            line["roofline"]["traffic_source"] = tr.get("source", "profiles/traffic.json")
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(cfg, min(args.cpu_sample, d.n), args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    cx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -126,7 +126,16 @@ typedef struct rsk_encode_out {
     const uint64_t *frame_off;/* [n] where frame i starts (16-B aligned offsets take the
                                  vector path; any offset is correct)                        */
     int32_t *status;          /* [n] 31+P, RSK_SEND_OVERSIZE or RSK_SEND_RESET              */
+    uint32_t flags;           /* RSK_ENC_* below; 0 = write exactly 31+P bytes per frame      */
 } rsk_encode_out;
+
+/* RSK_ENC_ZERO_PAD16: the encoder may also write zeros from each frame's end (31+P) up to the
+ * next 16-byte boundary of the arena address.  The caller asserts those bytes belong to no other
+ * frame (e.g. frames in 16-B-multiple slots).  This mirrors the reference, whose frames sit in a
+ * zeroed 1500-B buffer (RConn.cpp:100), and lets every 16-B chunk of a slot be written whole —
+ * no byte stores and no partially written cache lines, which the memory side otherwise services
+ * with read-modify-write. */
+#define RSK_ENC_ZERO_PAD16 0x1u
 
 /* frame_i = tag(8) | EncHead(23) | payload(P), written to frame_arena + frame_off[i].
  * Frames must not overlap each other or the payload arena. */

@@ -49,7 +49,10 @@ class EncodeIn(ctypes.Structure):
 
 
 class EncodeOut(ctypes.Structure):
-    _fields_ = [("frame_arena", _vp), ("frame_off", _vp), ("status", _vp)]
+    _fields_ = [("frame_arena", _vp), ("frame_off", _vp), ("status", _vp), ("flags", ctypes.c_uint32)]
+
+
+ENC_ZERO_PAD16 = 0x1
 
 
 class DecodeOut(ctypes.Structure):

@@ -149,18 +149,26 @@ class Codec:
         except Exception:
             pass
 
+    def set_encode_variant(self, v: int) -> None:
+        """Internal tuning knob (not in the public header): 0 flat<4> (default), 1 per-packet,
+        2 flat<2>, 3 flat<8>.  Every variant is parity-tested; used for in-process A/B."""
+        fn = lib().rsk__set_encode_variant
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        _check(fn(self._ctx, v), "rsk__set_encode_variant")
+
     def reserve(self, n_max: int) -> None:
         _check(lib().rsk_reserve(self._ctx, n_max), "rsk_reserve")
 
     # ---- batch paths ---------------------------------------------------------------------
     def output_batch(self, payload, pay_off, pay_len, cmd, conv, conn_key, frame, frame_off, status,
-                     id=None, id_uniform: bytes = b"\0" * 8, stream=None) -> None:
-        """RConn::Output framing for n packets (rsk_encode_batch)."""
+                     id=None, id_uniform: bytes = b"\0" * 8, pad16: bool = False, stream=None) -> None:
+        """RConn::Output framing for n packets (rsk_encode_batch).  pad16 sets RSK_ENC_ZERO_PAD16."""
         n = pay_len.numel()
         ein = _abi.EncodeIn(_ptr(payload), _ptr(pay_off), _ptr(pay_len), _ptr(cmd), _ptr(conv),
                             _ptr(conn_key), _ptr(id),
                             (ctypes.c_uint8 * 8)(*bytes(id_uniform)[:8].ljust(8, b"\0")))
-        eout = _abi.EncodeOut(_ptr(frame), _ptr(frame_off), _ptr(status))
+        eout = _abi.EncodeOut(_ptr(frame), _ptr(frame_off), _ptr(status),
+                              _abi.ENC_ZERO_PAD16 if pad16 else 0)
         _check(lib().rsk_encode_batch(self._ctx, n, ctypes.byref(ein), ctypes.byref(eout),
                                       _stream(stream)), "rsk_encode_batch")
 

@@ -53,6 +53,23 @@ __device__ __forceinline__ void store_partial16(uint8_t *p, const uint4 &v, int 
     }
 }
 
+// v with bytes [lim, 16) cleared (0 < lim < 16)
+__device__ __forceinline__ uint4 keep_bytes16(const uint4 &v, int lim) {
+    auto m = [lim](int d) -> uint32_t {
+        const int k = lim - 4 * d;
+        return k >= 4 ? 0xffffffffu : (k <= 0 ? 0u : ((1u << (8 * k)) - 1u));
+    };
+    return make_uint4(v.x & m(0), v.y & m(1), v.z & m(2), v.w & m(3));
+}
+
+// Store the last chunk of a frame: bytes [0, lim) of v at p (16-B aligned).  With pad, the whole
+// chunk is written with the tail zeroed (RSK_ENC_ZERO_PAD16); without, only [0, lim).
+__device__ __forceinline__ void store_tail16(uint8_t *p, const uint4 &v, int lim, bool pad) {
+    if (lim >= 16) *reinterpret_cast<uint4 *>(p) = v;
+    else if (pad) *reinterpret_cast<uint4 *>(p) = keep_bytes16(v, lim);
+    else store_partial16(p, v, lim);
+}
+
 // NW dwords of bytes starting at an arbitrary byte address p; aligned dwords whose address is
 // past `last` (the last byte the caller may touch) are not loaded (read as 0).  An aligned dword
 // that contains a valid byte never crosses a page, so no load can fault.

@@ -52,6 +52,7 @@ struct EncArgs {
     int32_t *status;
     uint32_t id_lo, id_hi;
     uint32_t n;
+    uint32_t pad;  // RSK_ENC_ZERO_PAD16
 };
 
 __device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t j) {
@@ -73,94 +74,300 @@ __device__ __forceinline__ void head_words(uint32_t cmd, uint32_t id0, uint32_t 
     H[7] = (uint32_t)(key >> 48) | (b0 << 24);
 }
 
-__global__ __launch_bounds__(kBlock) void k_encode(EncArgs a, KeySched ks) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t base = ((uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * 64u;
-    if (base >= a.n) return;  // wave-uniform
-    const uint64_t i = base + lane;
+// ---- phase 1: one lane per packet ---------------------------------------------------------------
+// status (RConn.cpp:88-98), tag (rhash.cpp:20-41 via md5_tag), frame words 0..7 (tag + EncHead +
+// payload[0]); `slow` marks a framed packet whose frame is not 16-B aligned (byte path).
+struct Lane1 {
+    int32_t st;
+    uint64_t po, fo;
+    uint32_t H[8];
+    bool slow;
+};
 
-    // ---- phase 1: one lane per packet — status, tag, header words ----
-    int32_t st = 0;
-    uint32_t P = 0;
-    uint64_t po = 0, fo = 0;
-    uint32_t H[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+__device__ __forceinline__ Lane1 encode_phase1(const EncArgs &a, const KeySched &ks, uint64_t i) {
+    Lane1 L;
+    L.st = 0;
+    L.po = 0;
+    L.fo = 0;
+    L.slow = false;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) L.H[q] = 0;
     if (i < a.n) {
-        po = a.pay_off[i];
-        P = a.pay_len[i];
-        fo = a.frame_off[i];
-        st = P == 0 ? RSK_SEND_RESET
-                    : (P > RSK_MAX_PAYLOAD ? RSK_SEND_OVERSIZE : (int32_t)(RSK_HEAD_SIZE + P));
-        if (st > 0) {
-            const uint32_t b0 = a.payload[po];
-            rsk::md5_tag(ks, b0, H[0], H[1]);
+        L.po = a.pay_off[i];
+        const uint32_t P = a.pay_len[i];
+        L.fo = a.frame_off[i];
+        L.st = P == 0 ? RSK_SEND_RESET
+                      : (P > RSK_MAX_PAYLOAD ? RSK_SEND_OVERSIZE : (int32_t)(RSK_HEAD_SIZE + P));
+        if (L.st > 0) {
+            const uint32_t b0 = a.payload[L.po];
+            rsk::md5_tag(ks, b0, L.H[0], L.H[1]);
             uint32_t id0 = a.id_lo, id1 = a.id_hi;
             if (a.id) {
                 const uint2 v = *reinterpret_cast<const uint2 *>(a.id + 8 * i);
                 id0 = v.x;
                 id1 = v.y;
             }
-            head_words(a.cmd[i], id0, id1, a.conv[i], a.conn_key[i], b0, H);
+            head_words(a.cmd[i], id0, id1, a.conv[i], a.conn_key[i], b0, L.H);
+            L.slow = (reinterpret_cast<uintptr_t>(a.frame + L.fo) & 15u) != 0;
         }
-        a.status[i] = st;
+        a.status[i] = L.st;
     }
+    return L;
+}
 
-    // ---- phase 2: the wave streams each framed packet of the tile ----
-    const uint32_t cnt = (uint32_t)min<uint64_t>(64u, a.n - base);
-    for (uint32_t j = 0; j < cnt; ++j) {
-        const int32_t sj = (int32_t)rdl((uint32_t)st, j);
-        if (sj <= 0) continue;
-        const uint32_t flen = (uint32_t)sj;  // 31 + P
-        const uint32_t Pj = flen - RSK_HEAD_SIZE;
-        const uint8_t *src = a.payload + rdl64(po, j);
-        uint8_t *dst = a.frame + rdl64(fo, j);
-        uint32_t Hj[8];
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <int NT>
+__device__ __forceinline__ uint4 ld16(const uint8_t *p) {
+    if constexpr (NT & 1) {
+        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+        return make_uint4(v.x, v.y, v.z, v.w);
+    } else {
+        return *reinterpret_cast<const uint4 *>(p);
+    }
+}
+template <int NT>
+__device__ __forceinline__ void st16(uint8_t *p, const uint4 &v) {
+    if constexpr (NT & 2) {
+        const u32x4 w = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(w, reinterpret_cast<u32x4 *>(p));
+    } else {
+        *reinterpret_cast<uint4 *>(p) = v;
+    }
+}
+template <int NT>
+__device__ __forceinline__ void store_last16(uint8_t *d, const uint4 &v, int lim, bool pad) {
+    if (lim >= 16) st16<NT>(d, v);
+    else if (pad) st16<NT>(d, rsk::keep_bytes16(v, lim));
+    else rsk::store_partial16(d, v, lim);
+}
+
+// ---- per-packet copy: the wave streams the frames of the packets in `vm` (16-B aligned), PU
+// packets per iteration.  A frame has at most 94 16-B chunks (1500 B), so chunk slots
+// k = lane and k = lane + 64 cover it; all PU x 2 slots' loads are issued before any store. -------
+template <int PU, int NT>
+__device__ __forceinline__ void copy_pkt(const EncArgs &a, const Lane1 &L, uint32_t lane, uint64_t vm) {
+    while (vm) {
+        uint32_t js[PU];
+        bool on[PU];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) Hj[q] = rdl(H[q], j);
-
-        if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
-            // vector path: chunk k holds frame bytes [16k, 16k+16)
-            const uint32_t nch = (flen + 15u) >> 4;
-            // chunk k >= 2 takes payload bytes [16k-31, 16k-15): 16-B aligned source chunks A, B
-            // at src_al + 16(k-2) and + 16, funnel-shifted by sh (uniform per packet)
-            const uint32_t sh = (uint32_t)((reinterpret_cast<uintptr_t>(src) + 1u) & 15u);
-            const uint8_t *src_al = src + 1 - sh;          // pointer arithmetic keeps global AS
-            const int32_t last_rel = (int32_t)Pj - 1 + (int32_t)sh - 1;  // last valid byte - src_al
-            for (uint32_t k = lane; k < nch; k += 64u) {
+        for (int p = 0; p < PU; ++p) {
+            on[p] = vm != 0ull;
+            js[p] = on[p] ? (uint32_t)__builtin_ctzll(vm) : 0u;
+            if (on[p]) vm &= vm - 1ull;
+        }
+        uint4 A[PU][2], B[PU][2];
+        const uint8_t *srcp[PU];
+        uint8_t *dstp[PU];
+        uint32_t flen[PU], sh[PU];
+        int32_t last_rel[PU];
+#pragma unroll
+        for (int p = 0; p < PU; ++p) {
+            flen[p] = on[p] ? rdl((uint32_t)L.st, js[p]) : 0u;
+            const uint8_t *src = a.payload + rdl64(L.po, js[p]);
+            dstp[p] = a.frame + rdl64(L.fo, js[p]);
+            sh[p] = (uint32_t)((reinterpret_cast<uintptr_t>(src) + 1u) & 15u);
+            srcp[p] = src + 1 - sh[p];  // chunk k >= 2 = payload bytes [16k-31, 16k-15)
+            last_rel[p] = (int32_t)flen[p] - RSK_HEAD_SIZE + (int32_t)sh[p] - 2;
+            const uint32_t nch = (flen[p] + 15u) >> 4;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const uint32_t k = lane + 64u * q;
+                A[p][q] = make_uint4(0u, 0u, 0u, 0u);
+                B[p][q] = make_uint4(0u, 0u, 0u, 0u);
+                if (k >= 2u && k < nch) {
+                    const uint32_t ro = 16u * (k - 2u);
+                    A[p][q] = ld16<NT>(srcp[p] + ro);
+                    if (sh[p] != 0u && (int32_t)(ro + 16u) <= last_rel[p]) B[p][q] = ld16<NT>(srcp[p] + ro + 16u);
+                }
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < PU; ++p) {
+            if (!on[p]) continue;
+            const uint32_t nch = (flen[p] + 15u) >> 4;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const uint32_t k = lane + 64u * q;
+                if (k >= nch) continue;
                 uint4 v;
                 if (k >= 2u) {
-                    const uint32_t ro = 16u * (k - 2u);
-                    const uint4 A = *reinterpret_cast<const uint4 *>(src_al + ro);
-                    uint4 B = make_uint4(0u, 0u, 0u, 0u);
-                    if (sh != 0u && (int32_t)(ro + 16u) <= last_rel)
-                        B = *reinterpret_cast<const uint4 *>(src_al + ro + 16u);
-                    v = rsk::funnel16(A, B, sh);
-                } else if (k == 0u) {
-                    v = make_uint4(Hj[0], Hj[1], Hj[2], Hj[3]);
+                    v = rsk::funnel16(A[p][q], B[p][q], sh[p]);
                 } else {
-                    v = make_uint4(Hj[4], Hj[5], Hj[6], Hj[7]);
-                }
-                const int lim = (int)flen - 16 * (int)k;
-                uint8_t *d = dst + 16u * k;
-                if (lim >= 16) *reinterpret_cast<uint4 *>(d) = v;
-                else rsk::store_partial16(d, v, lim);
-            }
-        } else {
-            // generic path (frame not 16-B aligned): byte stores
-            for (uint32_t f = lane; f < flen; f += 64u) {
-                uint32_t byte;
-                if (f < (uint32_t)RSK_HEAD_SIZE) {
-                    uint32_t w = Hj[0];
+                    uint32_t Hj[8];  // uniform: readlane every word, then select per lane
 #pragma unroll
-                    for (int q = 1; q < 8; ++q)
-                        if ((f >> 2) == (uint32_t)q) w = Hj[q];
-                    byte = (w >> (8u * (f & 3u))) & 0xffu;
-                } else {
-                    byte = src[f - RSK_HEAD_SIZE];
+                    for (int t = 0; t < 8; ++t) Hj[t] = rdl(L.H[t], js[p]);
+                    v = k == 0u ? make_uint4(Hj[0], Hj[1], Hj[2], Hj[3]) : make_uint4(Hj[4], Hj[5], Hj[6], Hj[7]);
                 }
-                dst[f] = (uint8_t)byte;
+                store_last16<NT>(dstp[p] + 16u * k, v, (int)flen[p] - 16 * (int)k, a.pad != 0u);
             }
         }
     }
+}
+
+// ---- flat copy: the payload chunks (k >= 2) of every packet in `vm` as one list of 16-B chunks;
+// lane l of iteration t takes chunk g = 64(U t + u) + l and finds its packet by a 6-step binary
+// search over the tile's prefix sums in this wave's LDS slice.  Chunks 0 and 1 (frame bytes
+// [0, 32): tag, EncHead, payload[0]) are stored by the packet's own lane.  Wave-local: no block
+// barrier, so waves of one block may take different copy paths. --------------------------------
+struct alignas(16) CopyRec {
+    const uint8_t *src_al;  // 16-B aligned source of chunk 2 (payload + 1 - sh)
+    uint8_t *dst;           // frame start (16-B aligned)
+    uint32_t cstart;        // first flat chunk index of this packet within the tile
+    uint32_t sh;            // funnel shift: (payload + 1) mod 16
+    int32_t last_rel;       // last payload byte, relative to src_al
+    uint32_t flen;          // 31 + P
+};
+
+// 16 bytes at byte offset sh (0..15, per lane) of A||B, branch-free
+__device__ __forceinline__ uint4 funnel16_lane(const uint4 &A, const uint4 &B, uint32_t sh) {
+    const uint32_t q = sh >> 2, r = sh & 3u;
+    const uint32_t W[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+    uint32_t E[5];
+#pragma unroll
+    for (int d = 0; d < 5; ++d) {
+        const uint32_t w0 = W[d], w1 = d + 1 < 8 ? W[d + 1] : 0u, w2 = d + 2 < 8 ? W[d + 2] : 0u,
+                       w3 = d + 3 < 8 ? W[d + 3] : 0u;
+        E[d] = q == 0 ? w0 : q == 1 ? w1 : q == 2 ? w2 : w3;
+    }
+    uint4 o;
+    o.x = rsk::funnel(E[1], E[0], r);
+    o.y = rsk::funnel(E[2], E[1], r);
+    o.z = rsk::funnel(E[3], E[2], r);
+    o.w = rsk::funnel(E[4], E[3], r);
+    return o;
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int U, int NT>
+__device__ __forceinline__ void copy_flat(const EncArgs &a, const Lane1 &L, uint32_t lane, bool mine,
+                                          CopyRec *recs, uint32_t *cend) {
+    uint32_t cc = 0;
+    CopyRec r;
+    r.src_al = nullptr; r.dst = nullptr; r.cstart = 0; r.sh = 0; r.last_rel = 0; r.flen = 0;
+    if (mine) {
+        const uint8_t *src = a.payload + L.po;
+        uint8_t *dst = a.frame + L.fo;
+        st16<NT>(dst, make_uint4(L.H[0], L.H[1], L.H[2], L.H[3]));  // frame bytes [0, 32): always
+        st16<NT>(dst + 16, make_uint4(L.H[4], L.H[5], L.H[6], L.H[7]));  // whole (31 + P >= 32)
+        const uint32_t flen = (uint32_t)L.st;
+        cc = ((flen + 15u) >> 4) - 2u;
+        const uint32_t sh = (uint32_t)((reinterpret_cast<uintptr_t>(src) + 1u) & 15u);
+        r.src_al = src + 1 - sh;
+        r.dst = dst;
+        r.sh = sh;
+        r.last_rel = (int32_t)flen - RSK_HEAD_SIZE + (int32_t)sh - 2;
+        r.flen = flen;
+    }
+    uint32_t inc = cc;  // wave-inclusive scan -> tile chunk table
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t v = __shfl_up(inc, off);
+        if (lane >= (uint32_t)off) inc += v;
+    }
+    r.cstart = inc - cc;
+    recs[lane] = r;
+    cend[lane] = inc;
+    const uint32_t C = (uint32_t)__shfl((int)inc, 63);
+    wave_lds_sync();
+    for (uint32_t g0 = 0; g0 < C; g0 += 64u * U) {
+        uint4 A[U], B[U];
+        uint8_t *dsts[U];
+        uint32_t shs[U];
+        int32_t lims[U];
+        bool act[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t g = g0 + 64u * u + lane;
+            act[u] = g < C;
+            A[u] = make_uint4(0u, 0u, 0u, 0u);
+            B[u] = make_uint4(0u, 0u, 0u, 0u);
+            shs[u] = 0;
+            lims[u] = 0;
+            dsts[u] = nullptr;
+            if (act[u]) {
+                uint32_t lo = 0;
+#pragma unroll
+                for (uint32_t st = 32; st; st >>= 1)
+                    if (cend[lo + st - 1] <= g) lo += st;
+                const CopyRec rr = recs[lo];
+                const uint32_t ro = 16u * (g - rr.cstart);
+                A[u] = ld16<NT>(rr.src_al + ro);
+                if (rr.sh != 0u && (int32_t)(ro + 16u) <= rr.last_rel) B[u] = ld16<NT>(rr.src_al + ro + 16);
+                shs[u] = rr.sh;
+                dsts[u] = rr.dst + 32u + ro;
+                lims[u] = (int32_t)rr.flen - 32 - (int32_t)ro;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (act[u]) store_last16<NT>(dsts[u], funnel16_lane(A[u], B[u], shs[u]), lims[u], a.pad != 0u);
+    }
+    wave_lds_sync();  // LDS slice reusable by the caller afterwards
+}
+
+// ---- frames that are not 16-B aligned: byte path, one packet at a time -------------------------
+__device__ __forceinline__ void copy_bytes(const EncArgs &a, const Lane1 &L, uint32_t lane, uint64_t sm) {
+    while (sm) {
+        const uint32_t j = (uint32_t)__builtin_ctzll(sm);
+        sm &= sm - 1ull;
+        const uint32_t fl = rdl((uint32_t)L.st, j);
+        const uint8_t *src = a.payload + rdl64(L.po, j);
+        uint8_t *dst = a.frame + rdl64(L.fo, j);
+        uint32_t Hj[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) Hj[q] = rdl(L.H[q], j);
+        const uint32_t fend = a.pad ? fl + ((16u - ((reinterpret_cast<uintptr_t>(dst) + fl) & 15u)) & 15u) : fl;
+        for (uint32_t f = lane; f < fend; f += 64u) {
+            uint32_t byte;
+            if (f >= fl) {
+                byte = 0;
+            } else if (f < (uint32_t)RSK_HEAD_SIZE) {
+                uint32_t wv = Hj[0];
+#pragma unroll
+                for (int q = 1; q < 8; ++q)
+                    if ((f >> 2) == (uint32_t)q) wv = Hj[q];
+                byte = (wv >> (8u * (f & 3u))) & 0xffu;
+            } else {
+                byte = src[f - RSK_HEAD_SIZE];
+            }
+            dst[f] = (uint8_t)byte;
+        }
+    }
+}
+
+// Copy-path choice for the hybrid kernel: the per-packet loop wastes lanes on short frames (a
+// 95-B frame uses 6 of 64 lanes), the flat list costs a binary search + LDS table per chunk.
+// Measured crossover: flat wins below a tile-mean frame of ~256 B.
+constexpr uint32_t kFlatBelowMeanBytes = 256;
+
+// MODE: 0 per-packet, 1 flat, 2 hybrid (per-wave choice)
+template <int MODE, int PU, int U, int NT>
+__global__ __launch_bounds__(kBlock) void k_encode(EncArgs a, KeySched ks) {
+    __shared__ CopyRec recs[kWavesPerBlock][64];
+    __shared__ uint32_t cend[kWavesPerBlock][64];
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint64_t base = ((uint64_t)blockIdx.x * kWavesPerBlock + w) * 64u;
+    if (base >= a.n) return;  // wave-uniform; no block barriers below
+    const Lane1 L = encode_phase1(a, ks, base + lane);
+    const bool vec = L.st > 0 && !L.slow;
+    const uint64_t vm = __ballot(vec);
+    bool flat = MODE == 1;
+    if constexpr (MODE == 2) {
+        // tile mean frame length over framed packets (wave reduction)
+        uint32_t fl = vec ? (uint32_t)L.st : 0u;
+#pragma unroll
+        for (int off = 32; off; off >>= 1) fl += __shfl_xor(fl, off);
+        const uint32_t cnt = (uint32_t)__popcll(vm);
+        flat = fl < kFlatBelowMeanBytes * cnt;
+    }
+    if (flat) copy_flat<U, NT>(a, L, lane, vec, recs[w], cend[w]);
+    else copy_pkt<PU, NT>(a, L, lane, vm);
+    copy_bytes(a, L, lane, __ballot(L.st > 0 && L.slow));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -604,6 +811,7 @@ inline unsigned grid_for(uint64_t threads) { return (unsigned)((threads + kBlock
 
 struct rsk_ctx {
     int device = 0;
+    int enc_variant = 0;  // see rsk__set_encode_variant
     std::vector<uint8_t> key;
     KeySched ks;
     // compaction workspace
@@ -689,6 +897,19 @@ const char *rsk_last_error(void) { return g_last_error; }
 
 const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 
+// Internal tuning knob (not part of include/rsk_codec.h): selects the encode kernel variant for
+// in-process A/B measurements.  k_encode<MODE, PU, U, NT>: MODE 0 per-packet, 1 flat, 2 hybrid;
+// PU packets per per-packet iteration; U chunks per lane per flat iteration; NT bit0 nontemporal
+// loads, bit1 nontemporal stores.
+//   0 = hybrid<4,4> (default)   1 = pkt PU=1   2 = flat U=2    3 = flat U=4    4 = pkt PU=2
+//   5 = pkt PU=4                6 = hybrid nt-stores           7 = pkt PU=4 nt loads+stores
+//   8 = pkt PU=4 nt stores      9 = hybrid PU=2               10 = pkt PU=2 nt stores
+int rsk__set_encode_variant(rsk_ctx *c, int v) {
+    if (!c || v < 0 || v > 10) return RSK_EINVAL;
+    c->enc_variant = v;
+    return RSK_OK;
+}
+
 rsk_ctx *rsk_create(const uint8_t *key, uint32_t key_len, int device) {
     if (!key && key_len) { snprintf(g_last_error, sizeof g_last_error, "rsk_create: null key"); return nullptr; }
     int ndev = 0;
@@ -742,9 +963,24 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
     std::memcpy(&a.id_lo, in->id_uniform, 4);
     std::memcpy(&a.id_hi, in->id_uniform + 4, 4);
     a.n = n;
+    a.pad = (out->flags & RSK_ENC_ZERO_PAD16) ? 1u : 0u;
     const uint64_t waves = (n + 63ull) / 64ull;
     const unsigned grid = (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
-    hipLaunchKernelGGL(k_encode, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, a, c->ks);
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 gd(grid), bd(kBlock);
+    switch (c->enc_variant) {
+        case 1: hipLaunchKernelGGL((k_encode<0, 1, 4, 0>), gd, bd, 0, st, a, c->ks); break;
+        case 2: hipLaunchKernelGGL((k_encode<1, 4, 2, 0>), gd, bd, 0, st, a, c->ks); break;
+        case 3: hipLaunchKernelGGL((k_encode<1, 4, 4, 0>), gd, bd, 0, st, a, c->ks); break;
+        case 4: hipLaunchKernelGGL((k_encode<0, 2, 4, 0>), gd, bd, 0, st, a, c->ks); break;
+        case 5: hipLaunchKernelGGL((k_encode<0, 4, 4, 0>), gd, bd, 0, st, a, c->ks); break;
+        case 6: hipLaunchKernelGGL((k_encode<2, 4, 4, 2>), gd, bd, 0, st, a, c->ks); break;
+        case 7: hipLaunchKernelGGL((k_encode<0, 4, 4, 3>), gd, bd, 0, st, a, c->ks); break;
+        case 8: hipLaunchKernelGGL((k_encode<0, 4, 4, 2>), gd, bd, 0, st, a, c->ks); break;
+        case 9: hipLaunchKernelGGL((k_encode<2, 2, 4, 0>), gd, bd, 0, st, a, c->ks); break;
+        case 10: hipLaunchKernelGGL((k_encode<0, 2, 4, 2>), gd, bd, 0, st, a, c->ks); break;
+        default: hipLaunchKernelGGL((k_encode<2, 4, 4, 0>), gd, bd, 0, st, a, c->ks); break;
+    }
     return launch_check("k_encode");
 }
 

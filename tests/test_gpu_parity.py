@@ -26,7 +26,7 @@ def dev(a: np.ndarray, gpu, dt=None):
 
 
 def run_encode(codec, gpu, payload, pay_off, pay_len, cmd, conv, ckey, frame_off, frame_bytes,
-               idarr=None, id_uniform=workload.ID_UNIFORM, frame_init=None):
+               idarr=None, id_uniform=workload.ID_UNIFORM, frame_init=None, pad16=False):
     import torch
 
     n = len(pay_len)
@@ -37,7 +37,7 @@ def run_encode(codec, gpu, payload, pay_off, pay_len, cmd, conv, ckey, frame_off
                        dev(pay_len.astype(np.uint16), gpu, np.int16), dev(cmd.astype(np.uint8), gpu),
                        dev(conv.astype(np.uint32), gpu, np.int32), dev(ckey.astype(np.uint64), gpu, np.int64),
                        frame, dev(frame_off.astype(np.uint64), gpu, np.int64), status,
-                       id=None if idarr is None else dev(idarr, gpu), id_uniform=id_uniform)
+                       id=None if idarr is None else dev(idarr, gpu), id_uniform=id_uniform, pad16=pad16)
     torch.cuda.synchronize()
     return frame.cpu().numpy(), status.cpu().numpy()
 
@@ -72,7 +72,8 @@ def assert_dec_equal(got: dict, exp: dict):
 
 # ---- configs (reduced n) ----------------------------------------------------------------------
 @pytest.mark.parametrize("cfg,n", [("c2", 100_000), ("c3", 20_000), ("c4", 50_000)])
-def test_config_roundtrip_bitexact(codec, gpu, oracle, cfg, n):
+def test_config_roundtrip_bitexact(vcodec, gpu, oracle, cfg, n):
+    codec = vcodec
     d = workload.describe(cfg, 0, n, n=n)
     w = workload.DeviceWorkload(d, gpu)
     codec.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
@@ -103,8 +104,21 @@ def _rand_fields(rng, n):
             rng.integers(0, 2**63, n, dtype=np.uint64) * 2 + rng.integers(0, 2, n, dtype=np.uint64))
 
 
-@pytest.mark.parametrize("layout", ["slots16", "packed", "odd_frames", "odd_payloads"])
-def test_encode_edge_lengths_and_layouts(codec, gpu, oracle, layout):
+ENC_VARIANTS = list(range(11))
+
+
+@pytest.fixture(params=ENC_VARIANTS, ids=lambda v: f"encv{v}")
+def vcodec(request, codec):
+    codec.set_encode_variant(request.param)
+    yield codec
+    codec.set_encode_variant(0)
+
+
+@pytest.mark.parametrize("layout,pad16", [("slots16", False), ("packed", False), ("odd_frames", False),
+                                          ("odd_payloads", False), ("slots16", True), ("odd_frames", True),
+                                          ("odd_payloads", True)])
+def test_encode_edge_lengths_and_layouts(vcodec, gpu, oracle, layout, pad16):
+    codec = vcodec
     rng = np.random.default_rng(7)
     lens = [0, 1, 2, 3, 4, 7, 8, 15, 16, 17, 31, 32, 33, 47, 48, 63, 64, 65, 1000, 1023, 1024, 1025, 1400,
             1468, 1469, 1470, 1500, 4000, 65535]
@@ -139,13 +153,16 @@ def test_encode_edge_lengths_and_layouts(codec, gpu, oracle, layout):
     fill = rng.integers(0, 256, frame_bytes, dtype=np.uint8)  # pre-existing bytes must survive
     exp_frames = fill.copy()
     got_frames, got_status = run_encode(codec, gpu, payload, pay_off, pl16, cmd, conv, ckey, frame_off,
-                                        frame_bytes, frame_init=fill)
+                                        frame_bytes, frame_init=fill, pad16=pad16)
     ef, es = oracle.encode_batch(KEY, payload, d, workload.ID_UNIFORM, frame_bytes=frame_bytes)
     assert np.array_equal(got_status, es)
     for i in range(n):
         if es[i] > 0:
             o = int(frame_off[i])
             exp_frames[o:o + es[i]] = ef[o:o + es[i]]
+            if pad16:  # RSK_ENC_ZERO_PAD16: zeros up to the next 16-B boundary (arena is 256-B aligned)
+                e = o + int(es[i])
+                exp_frames[e:(e + 15) // 16 * 16] = 0
     bad = np.nonzero(got_frames != exp_frames)[0]
     assert bad.size == 0, f"{layout}: {bad.size} bytes differ, first at {bad[:8]}"
 

@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""In-process A/B of encode-kernel variants (interleaved rounds in ONE process, guide §5.4 rule 24).
+   python tools/ab_encode.py [--config c3] [--rounds 10] [--reps 10] [--variants 0,1,2,3]
+Prints per-variant median/min k_encode ms and algorithmic GB/s, and checks every variant's frame
+arena is byte-identical to variant 1's."""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--packets", type=int, default=0)
+    ap.add_argument("--rounds", type=int, default=10)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--variants", default="0,1,2,3")
+    ap.add_argument("--pads", default="0,1", help="RSK_ENC_ZERO_PAD16 off/on")
+    args = ap.parse_args()
+    import torch
+
+    from bench import enc_bytes_per_pkt
+    from rsock_amd import codec as rc
+    from rsock_amd import workload
+
+    dev = torch.device("cuda:0")
+    n = args.packets or workload.CONFIGS[args.config][1]
+    d = workload.describe(args.config, 0, n, n=n)
+    w = workload.DeviceWorkload(d, dev)
+    cx = rc.Codec(b"hello135", 0)
+    variants = [(int(v), int(p)) for v in args.variants.split(",") for p in args.pads.split(",")]
+    times = {v: [] for v in variants}
+    ref = None
+    s = torch.cuda.current_stream()
+
+    cur = {"pad": 0}
+
+    def enc():
+        cx.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
+                        w.status, id_uniform=workload.ID_UNIFORM, pad16=bool(cur["pad"]), stream=s)
+
+    for v in variants:  # correctness: identical frame arenas
+        cx.set_encode_variant(v[0])
+        cur["pad"] = v[1]
+        w.frame.zero_()
+        enc()
+        torch.cuda.synchronize()
+        h = w.frame.clone()
+        if ref is None:
+            ref = h
+        elif not torch.equal(ref, h):
+            raise SystemExit(f"variant {v} frame arena differs from variant {variants[0]}")
+    del ref
+    for _ in range(args.rounds):
+        for v in variants:
+            cx.set_encode_variant(v[0])
+            cur["pad"] = v[1]
+            enc()
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            ev[0].record(s)
+            for _ in range(args.reps):
+                enc()
+            ev[1].record(s)
+            torch.cuda.synchronize()
+            times[v].append(ev[0].elapsed_time(ev[1]) / args.reps)
+    p = int(d.pay_len.mean())
+    byts = d.n * enc_bytes_per_pkt(p)
+    out = {}
+    for v in variants:
+        t = np.array(times[v])
+        out[f"v{v[0]}pad{v[1]}"] = {"median_ms": round(float(np.median(t)), 4), "min_ms": round(float(t.min()), 4),
+                  "GBps_median": round(byts / (np.median(t) * 1e-3) / 1e9, 1)}
+    print(json.dumps({"config": args.config, "packets": d.n, "variants": out}))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,80 @@
+// hbm_probe.hip — calibration kernels for the encode roofline (tools only, not product code).
+// Measures what this chip sustains for the byte patterns k_encode uses:
+//   copy16      dst[i] = src[i], 16 B/lane, grid-stride                      (pure copy ceiling)
+//   read16      sum of src, 16 B/lane                                        (read-only)
+//   write16     dst[i] = const, 16 B/lane                                    (write-only)
+//   shift2ld    dst chunk k = src bytes [16k+1, 16k+17): two 16-B loads + v_alignbyte
+//   shiftdpp    same, second operand from lane+1 via DPP wave_shl:1 (one load per chunk)
+// Build: hipcc -O3 --offload-arch=gfx950 -shared -fPIC -o tools/libhbm_probe.so tools/hbm_probe.hip
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+__global__ __launch_bounds__(256) void k_copy16(const uint4 *__restrict__ s, uint4 *__restrict__ d, uint64_t n) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) d[i] = s[i];
+}
+
+__global__ __launch_bounds__(256) void k_read16(const uint4 *__restrict__ s, uint32_t *out, uint64_t n) {
+    uint32_t acc = 0;
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
+        const uint4 v = s[i];
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (acc == 0x12345678u) out[0] = acc;  // keeps the loads live
+}
+
+__global__ __launch_bounds__(256) void k_write16(uint4 *__restrict__ d, uint64_t n) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull)
+        d[i] = make_uint4((uint32_t)i, 1u, 2u, 3u);
+}
+
+__device__ __forceinline__ uint4 sh1(const uint4 &A, const uint4 &B) {
+    uint4 o;
+    o.x = __builtin_amdgcn_alignbyte(A.y, A.x, 1);
+    o.y = __builtin_amdgcn_alignbyte(A.z, A.y, 1);
+    o.z = __builtin_amdgcn_alignbyte(A.w, A.z, 1);
+    o.w = __builtin_amdgcn_alignbyte(B.x, A.w, 1);
+    return o;
+}
+
+__global__ __launch_bounds__(256) void k_shift2ld(const uint8_t *__restrict__ s, uint4 *__restrict__ d, uint64_t n) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
+        const uint4 A = reinterpret_cast<const uint4 *>(s)[i];
+        const uint4 B = reinterpret_cast<const uint4 *>(s)[i + 1];
+        d[i] = sh1(A, B);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_shiftdpp(const uint8_t *__restrict__ s, uint4 *__restrict__ d, uint64_t n) {
+    const uint32_t lane = threadIdx.x & 63u;
+    // n is a multiple of 64 chunks per wave-iteration here
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
+        const uint4 A = reinterpret_cast<const uint4 *>(s)[i];
+        // B.x = A.x of lane + 1 (DPP wave_shl:1 = 0x130); lane 63 loads its own
+        uint32_t bx = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)A.x, 0x130, 0xf, 0xf, false);
+        if (lane == 63u) bx = reinterpret_cast<const uint32_t *>(s)[4 * (i + 1)];
+        uint4 B;
+        B.x = bx; B.y = 0; B.z = 0; B.w = 0;
+        d[i] = sh1(A, B);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+// returns 0 on success; kind: 0 copy16, 1 read16, 2 write16, 3 shift2ld, 4 shiftdpp
+int probe_run(int kind, void *src, void *dst, uint64_t bytes, int grid, void *stream) {
+    const uint64_t n = bytes / 16u;
+    hipStream_t st = (hipStream_t)stream;
+    switch (kind) {
+        case 0: hipLaunchKernelGGL(k_copy16, dim3(grid), dim3(256), 0, st, (const uint4 *)src, (uint4 *)dst, n); break;
+        case 1: hipLaunchKernelGGL(k_read16, dim3(grid), dim3(256), 0, st, (const uint4 *)src, (uint32_t *)dst, n); break;
+        case 2: hipLaunchKernelGGL(k_write16, dim3(grid), dim3(256), 0, st, (uint4 *)dst, n); break;
+        case 3: hipLaunchKernelGGL(k_shift2ld, dim3(grid), dim3(256), 0, st, (const uint8_t *)src, (uint4 *)dst, n - 1); break;
+        case 4: hipLaunchKernelGGL(k_shiftdpp, dim3(grid), dim3(256), 0, st, (const uint8_t *)src, (uint4 *)dst, n - 64); break;
+        default: return -1;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+}
