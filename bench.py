@@ -146,7 +146,7 @@ def main() -> None:
         if ev is not None:
             ev[0].record(stream)
         cx.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
-                        w.status, id_uniform=workload.ID_UNIFORM, stream=stream)
+                        w.status, id_uniform=workload.ID_UNIFORM, pad16=True, stream=stream)
         if ev is not None:
             ev[1].record(stream)
         cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, w.dec, stream=stream)

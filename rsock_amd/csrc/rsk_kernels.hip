@@ -582,28 +582,44 @@ __global__ __launch_bounds__(kBlock) void k_parse_decode(ParseArgs a, DecOut d, 
 // ---------------------------------------------------------------------------------------------
 // Order-stable compaction of VALID indices
 // ---------------------------------------------------------------------------------------------
+// Exclusive scan of the per-block VALID counts -> offsets (one workgroup; 4 counts per thread per
+// pass, wave scans via DPP-backed shuffles, one LDS exchange per pass), plus the total.
 __global__ __launch_bounds__(1024) void k_scan(const uint32_t *counts, uint32_t *offsets, uint32_t nb,
                                                uint32_t *n_valid) {
-    __shared__ uint32_t s[1024];
-    const uint32_t t = threadIdx.x;
-    const uint32_t per = (nb + 1023u) / 1024u;
-    const uint32_t lo = min(t * per, nb), hi = min(lo + per, nb);
-    uint32_t sum = 0;
-    for (uint32_t k = lo; k < hi; ++k) sum += counts[k];
-    s[t] = sum;
-    __syncthreads();
-    for (uint32_t off = 1; off < 1024u; off <<= 1) {
-        const uint32_t v = t >= off ? s[t - off] : 0u;
+    __shared__ uint32_t wsum[16];
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < nb; base += 4096u) {
+        const uint32_t idx = base + 4u * t;
+        uint32_t c[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) c[k] = idx + k < nb ? counts[idx + k] : 0u;
+        const uint32_t tsum = c[0] + c[1] + c[2] + c[3];
+        uint32_t inc = tsum;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t v = __shfl_up(inc, off);
+            if (lane >= (uint32_t)off) inc += v;
+        }
+        if (lane == 63u) wsum[wv] = inc;
         __syncthreads();
-        s[t] += v;
-        __syncthreads();
+        uint32_t wpre = 0, total = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < 16; ++q) {
+            const uint32_t v = wsum[q];
+            wpre += q < wv ? v : 0u;
+            total += v;
+        }
+        uint32_t run = carry + wpre + inc - tsum;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (idx + k < nb) offsets[idx + k] = run;
+            run += c[k];
+        }
+        carry += total;
+        __syncthreads();  // wsum reused next pass
     }
-    uint32_t run = s[t] - sum;
-    for (uint32_t k = lo; k < hi; ++k) {
-        offsets[k] = run;
-        run += counts[k];
-    }
-    if (t == 1023u && n_valid) *n_valid = s[1023];
+    if (t == 0 && n_valid) *n_valid = carry;
 }
 
 __global__ __launch_bounds__(kBlock) void k_scatter(const uint64_t *masks, const uint32_t *offsets,

@@ -1,0 +1,118 @@
+"""Full BASELINE sizes (C2 1M x 64 B, C3 4M x 1400 B, C4 1M mixed) through size-independent
+properties checked on the device:
+  * encode -> decode round trip: every framed packet verifies, compaction is the identity list
+  * frame payload region == payload bytes; header bytes == the SoA fields (LE)
+  * tag bytes == the oracle's 256-entry tag table at payload[0] (the tag depends only on it)
+  * C4: exactly the corrupted frames drop, valid_idx is the order-stable list of the others
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from rsock_amd import workload
+
+pytestmark = pytest.mark.gpu
+KEY = b"hello135"
+
+
+def _tag_table(oracle, gpu):
+    import torch
+
+    t = np.frombuffer(b"".join(oracle.tag(KEY, b) for b in range(256)), np.uint8).reshape(256, 8)
+    return torch.from_numpy(t.copy()).to(gpu)
+
+
+def _le_bytes(x, nbytes):
+    import torch
+
+    x = x.to(torch.int64)
+    return torch.stack([(x >> (8 * k)) & 0xFF for k in range(nbytes)], dim=1).to(torch.uint8)
+
+
+@pytest.mark.parametrize("cfg", ["c3", "c2", "c4"])
+@pytest.mark.parametrize("pad16", [True, False])
+def test_fullsize_roundtrip(codec, gpu, oracle, cfg, pad16):
+    import torch
+
+    d = workload.describe(cfg)
+    w = workload.DeviceWorkload(d, gpu)
+    n = d.n
+    codec.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
+                       w.status, id_uniform=workload.ID_UNIFORM, pad16=pad16)
+    torch.cuda.synchronize()
+    plen = w.pay_len.to(torch.int64) & 0xFFFF
+    assert torch.equal(w.status.to(torch.int64), plen + 31)
+    frames = w.frame.view(n, d.frame_pitch)
+    pays = w.payload.view(n, d.pay_pitch)
+    tags = _tag_table(oracle, gpu)
+    assert torch.equal(frames[:, :8], tags[pays[:, 0].long()])
+    hdr = frames[:, 8:31]
+    assert bool((hdr[:, 0] == 23).all()) and torch.equal(hdr[:, 1], w.cmd)
+    idu = torch.frombuffer(bytearray(workload.ID_UNIFORM), dtype=torch.uint8).to(gpu)
+    assert bool((hdr[:, 2:10] == idu).all())
+    assert torch.equal(hdr[:, 10:14], _le_bytes(w.conv.to(torch.int64) & 0xFFFFFFFF, 4))
+    assert torch.equal(hdr[:, 14:22], _le_bytes(w.conn_key, 8))
+    assert bool((hdr[:, 22] == 0).all())
+    # payload region, per distinct payload length (C3/C2 uniform; C4 bucketed)
+    for p in torch.unique(plen).tolist():
+        sel = (plen == p).nonzero().squeeze(1)
+        for lo in range(0, sel.numel(), 1 << 18):
+            s = sel[lo: lo + (1 << 18)]
+            assert torch.equal(frames[s, 31:31 + p], pays[s, :p]), f"payload mismatch at P={p}"
+            if pad16:
+                end = 31 + p
+                pad_end = (end + 15) // 16 * 16
+                if pad_end > end:
+                    assert bool((frames[s, end:pad_end] == 0).all())
+    # decode: corrupt C4's marked frames first
+    w.corrupt_frames()
+    codec.onrecv_batch(w.frame, w.frame_off, w.frame_len, w.dec)
+    torch.cuda.synchronize()
+    keep = torch.from_numpy(~d.corrupt).to(gpu)
+    st = w.dec.status.to(torch.int64)
+    assert torch.equal(st == 1, keep)
+    nv = int(w.dec.n_valid.item())
+    exp_idx = keep.nonzero().squeeze(1).to(torch.int32)
+    assert nv == exp_idx.numel()
+    assert torch.equal(w.dec.valid_idx[:nv], exp_idx)
+    ok = keep
+    assert torch.equal((w.dec.pay_len.to(torch.int64) & 0xFFFF)[ok], plen[ok])
+    assert bool((w.dec.pay_off[ok] == 31).all()) and bool((w.dec.hlen[ok] == 23).all())
+    assert torch.equal(w.dec.conv[ok], w.conv[ok]) and torch.equal(w.dec.conn_key[ok], w.conn_key[ok])
+    assert torch.equal(w.dec.cmd[ok], w.cmd[ok])
+    assert bool((w.dec.id.view(n, 8)[ok] == idu).all())
+    # dropped frames expose zero fields
+    bad = ~keep
+    if bool(bad.any()):
+        assert bool((w.dec.conv[bad] == 0).all()) and bool((w.dec.hlen[bad] == 0).all())
+
+
+def test_compaction_large_random(codec, gpu, oracle):
+    """n > 4096 scan blocks x 256 (multi-pass k_scan): random validity pattern, order-stable."""
+    import torch
+
+    n = 5_000_003
+    g = torch.Generator(device=gpu)
+    g.manual_seed(1234)
+    # frames of 32 B in 32-B slots: tag of byte 0 or a wrong tag, chosen at random
+    valid = torch.rand(n, device=gpu, generator=g) < 0.37
+    tags = _tag_table(oracle, gpu)
+    body = torch.randint(0, 256, (n,), device=gpu, generator=g, dtype=torch.int64).to(torch.uint8)
+    frames = torch.zeros(n, 32, dtype=torch.uint8, device=gpu)
+    frames[:, :8] = tags[body.long()]
+    frames[~valid, 0] ^= 0x55
+    frames[:, 8] = 23
+    frames[:, 31] = body
+    off = torch.arange(n, device=gpu, dtype=torch.int64) * 32
+    flen = torch.full((n,), 32, dtype=torch.int16, device=gpu)
+    from rsock_amd.codec import DecodeBuffers
+
+    out = DecodeBuffers.alloc(n, gpu)
+    codec.onrecv_batch(frames.view(-1), off, flen, out)
+    torch.cuda.synchronize()
+    exp = valid.nonzero().squeeze(1).to(torch.int32)
+    nv = int(out.n_valid.item())
+    assert nv == exp.numel()
+    assert torch.equal(out.valid_idx[:nv], exp)
+    assert torch.equal(out.status == 1, valid)

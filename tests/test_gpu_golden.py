@@ -1,0 +1,91 @@
+"""GPU vs the REFERENCE's own outputs (tests/golden, produced by oracle/_ref from /root/reference
+sources): encode the golden inputs and decode the golden frames through the C-ABI; bytes and
+fields must equal the reference's, bit for bit."""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+
+from tests.test_gpu_parity import DEC_VIEWS, dev, run_decode, run_encode
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+KEY = b"hello135"
+
+
+def gold(name):
+    return np.load(os.path.join(GOLD, name), allow_pickle=False)
+
+
+@pytest.mark.parametrize("pad16", [False, True])
+def test_encode_matches_reference_frames(codec, gpu, pad16):
+    g = gold("frames.npz")
+    n = len(g["status"])
+    pitch = 1504
+    frame_off = (np.arange(n) * pitch).astype(np.uint64)
+    fr, st = run_encode(codec, gpu, g["payload"], g["pay_off"], np.minimum(g["pay_len"], 65535).astype(np.uint16),
+                        g["cmd"], g["conv"], g["conn_key"], frame_off, n * pitch, idarr=g["id"], pad16=pad16)
+    assert np.array_equal(st, g["status"])
+    for i in range(n):
+        if st[i] > 0:
+            o = int(g["frame_off"][i])
+            assert fr[i * pitch: i * pitch + st[i]].tobytes() == g["frames"][o: o + int(g["frame_len"][i])].tobytes(), i
+
+
+def test_decode_matches_reference_onrecv(codec, gpu):
+    g = gold("onrecv.npz")
+    got = run_decode(codec, gpu, g["frames"], g["frame_off"], g["frame_len"].astype(np.uint16), g["close"])
+    for k, dt in DEC_VIEWS.items():
+        assert np.array_equal(got[k].view(dt), g[k]), k
+    nv = int(got["n_valid"][0])
+    assert nv == int((g["status"] == 1).sum())
+    assert np.array_equal(got["valid_idx"][:nv].view(np.uint32), np.nonzero(g["status"] == 1)[0].astype(np.uint32))
+
+
+def test_tags_all_keys_match_reference(gpu):
+    from rsock_amd.codec import Codec
+
+    g = gold("tags.npz")
+    kb, ko, kl = g["key_bytes"], g["key_off"], g["key_len"]
+    for k in range(len(kl)):
+        key = kb[int(ko[k]): int(ko[k]) + int(kl[k])].tobytes()
+        cx = Codec(key, 0)
+        try:
+            payload = np.repeat(np.arange(256, dtype=np.uint8), 16)
+            z = np.zeros(256, np.uint8)
+            fr, st = run_encode(cx, gpu, payload, (np.arange(256) * 16).astype(np.uint64), np.full(256, 16, np.uint16),
+                                z, z.astype(np.uint32), z.astype(np.uint64), (np.arange(256) * 48).astype(np.uint64),
+                                256 * 48)
+            assert np.array_equal(fr.reshape(256, 48)[:, :8], g["tags"][k]), len(key)
+        finally:
+            cx.close()
+
+
+def test_tcpinfo_records_match_reference(codec, gpu):
+    import torch
+
+    g = gold("tcpinfo_keys.npz")
+    n = len(g["src"])
+    rec = torch.zeros(21 * n, dtype=torch.uint8, device=gpu)
+    codec.tcpinfo_encode_batch(dev(g["src"], gpu, np.int32), dev(g["dst"], gpu, np.int32), dev(g["sp"], gpu, np.int16),
+                               dev(g["dp"], gpu, np.int16), dev(g["seq"], gpu, np.int32), dev(g["ack"], gpu, np.int32),
+                               dev(g["flag"], gpu), rec)
+    assert np.array_equal(rec.cpu().numpy(), g["records"])
+
+
+def test_enchead_shims_match_reference(codec):
+    g = gold("enchead.npz")
+    for i in range(len(g["enc_buf_len"])):
+        h = codec.enc2buf(int(g["enc_cmd"][i]), g["enc_id"][8 * i: 8 * i + 8].tobytes(), int(g["enc_conv"][i]),
+                          int(g["enc_key"][i]), buf_len=int(g["enc_buf_len"][i]))
+        assert (h is not None) == bool(g["enc_ok"][i])
+        if h is not None:
+            assert h == g["enc_out"][23 * i: 23 * i + 23].tobytes()
+    for i in range(0, len(g["dec_buf_len"]), 3):
+        r = codec.decodebuf(g["dec_in"][23 * i: 23 * i + 23].tobytes(), int(g["dec_buf_len"][i]))
+        assert (r is not None) == bool(g["dec_ok"][i]), i
+        if r is not None:
+            assert r[1:] == (int(g["dec_cmd"][i]), g["dec_id"][8 * i: 8 * i + 8].tobytes(), int(g["dec_conv"][i]),
+                             int(g["dec_key"][i]))

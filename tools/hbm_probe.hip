@@ -60,9 +60,40 @@ __global__ __launch_bounds__(256) void k_shiftdpp(const uint8_t *__restrict__ s,
     }
 }
 
+// each wave copies its own contiguous tile of `tile16` 16-B chunks, 64 chunks per iteration
+// (the access shape of k_encode's per-wave packet tiles) — U iterations' loads in flight
+template <int U>
+__global__ __launch_bounds__(256) void k_tilecopy(const uint4 *__restrict__ s, uint4 *__restrict__ d, uint64_t n,
+                                                  uint32_t tile16) {
+    const uint64_t wave = blockIdx.x * 4ull + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t b0 = wave * tile16;
+    if (b0 >= n) return;
+    const uint64_t e = b0 + tile16 < n ? b0 + tile16 : n;
+    for (uint64_t b = b0 + lane; b < e; b += 64u * U) {
+        uint4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) if (b + 64u * u < e) v[u] = s[b + 64u * u];
+#pragma unroll
+        for (int u = 0; u < U; ++u) if (b + 64u * u < e) d[b + 64u * u] = v[u];
+    }
+}
+
 }  // namespace
 
 extern "C" {
+// each wave copies a contiguous tile of tile_bytes (multiple of 16)
+int probe_tile(int unroll, void *src, void *dst, uint64_t bytes, uint32_t tile_bytes, void *stream) {
+    const uint64_t n = bytes / 16u;
+    const uint32_t t16 = tile_bytes / 16u;
+    const uint64_t waves = (n + t16 - 1) / t16;
+    const unsigned grid = (unsigned)((waves + 3) / 4);
+    hipStream_t st = (hipStream_t)stream;
+    if (unroll == 4) hipLaunchKernelGGL(k_tilecopy<4>, dim3(grid), dim3(256), 0, st, (const uint4 *)src, (uint4 *)dst, n, t16);
+    else hipLaunchKernelGGL(k_tilecopy<1>, dim3(grid), dim3(256), 0, st, (const uint4 *)src, (uint4 *)dst, n, t16);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 // returns 0 on success; kind: 0 copy16, 1 read16, 2 write16, 3 shift2ld, 4 shiftdpp
 int probe_run(int kind, void *src, void *dst, uint64_t bytes, int grid, void *stream) {
     const uint64_t n = bytes / 16u;

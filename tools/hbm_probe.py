@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--gib", type=float, default=6.0)
     ap.add_argument("--grids", default="2048,8192,65536")
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--tiles", default="1024,16384,92160,1048576")
     args = ap.parse_args()
     L = ctypes.CDLL(os.path.join(HERE, "libhbm_probe.so"))
     L.probe_run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
@@ -37,6 +38,19 @@ def main():
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / args.reps
             res[f"{nm}@{g}"] = round(moved[k] * nbytes / (ms * 1e-3) / 1e9, 1)
+    L.probe_tile.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                             ctypes.c_void_p]
+    for unroll in (1, 4):
+        for tile in [int(x) for x in args.tiles.split(",")]:
+            L.probe_tile(unroll, src.data_ptr(), dst.data_ptr(), nbytes, tile, s.cuda_stream)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for _ in range(args.reps):
+                L.probe_tile(unroll, src.data_ptr(), dst.data_ptr(), nbytes, tile, s.cuda_stream)
+            e1.record(s)
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / args.reps
+            res[f"tilecopy_u{unroll}@{tile}"] = round(2 * nbytes / (ms * 1e-3) / 1e9, 1)
     # check shiftdpp == shift2ld output on a prefix
     L.probe_run(3, src.data_ptr(), dst.data_ptr(), 1 << 20, 256, s.cuda_stream)
     a = dst[: (1 << 20) - 64 * 16].clone()
