@@ -136,6 +136,9 @@ typedef struct rsk_encode_out {
  * no byte stores and no partially written cache lines, which the memory side otherwise services
  * with read-modify-write. */
 #define RSK_ENC_ZERO_PAD16 0x1u
+/* RSK_ENC_ZERO_PAD128: as RSK_ENC_ZERO_PAD16 but up to the next 128-byte (cache-line) boundary;
+ * takes precedence over RSK_ENC_ZERO_PAD16. */
+#define RSK_ENC_ZERO_PAD128 0x2u
 
 /* frame_i = tag(8) | EncHead(23) | payload(P), written to frame_arena + frame_off[i].
  * Frames must not overlap each other or the payload arena. */

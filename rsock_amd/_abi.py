@@ -53,6 +53,7 @@ class EncodeOut(ctypes.Structure):
 
 
 ENC_ZERO_PAD16 = 0x1
+ENC_ZERO_PAD128 = 0x2
 
 
 class DecodeOut(ctypes.Structure):
@@ -111,7 +112,20 @@ SIGNATURES = [
     ("rsk_key_for_tcp", ctypes.c_uint64, [ctypes.c_uint16, ctypes.c_uint16]),
     ("rsk_key_for_udp", ctypes.c_uint64, [ctypes.c_uint16, ctypes.c_uint16]),
     ("rsk_fill_splitmix", ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint64, _vp]),
+    # include/rsk_rconn.h (RConn-shaped batching adapter)
+    ("rsk_rconn_create", _vp, [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_uint32]),
+    ("rsk_rconn_destroy", None, [_vp]),
+    ("rsk_rconn_set_callbacks", None, [_vp, _vp, _vp, _vp, _vp]),
+    ("rsk_rconn_output", ctypes.c_int,
+     [_vp, ctypes.c_int64, ctypes.c_char_p, ctypes.c_uint8, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint64, _vp]),
+    ("rsk_rconn_onrecv", ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_char_p, ctypes.c_int, _vp]),
+    ("rsk_rconn_flush", ctypes.c_int, [_vp]),
 ]
+
+SEND_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p)
+RESET_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p)
+RECV_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_int, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_void_p, ctypes.c_uint32,
+                           ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p)
 
 
 def load(path: str = LIB_PATH) -> ctypes.CDLL:
@@ -127,12 +141,16 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     return lib
 
 
-def header_symbols(header_path: str | None = None) -> list[str]:
-    """Names of every function declared in include/rsk_codec.h (used by the ABI test)."""
+def header_symbols(header_paths: list[str] | None = None) -> list[str]:
+    """Names of every function declared in include/rsk_codec.h and include/rsk_rconn.h."""
     import re
 
-    if header_path is None:
-        header_path = os.path.join(os.path.dirname(_HERE), "include", "rsk_codec.h")
-    text = open(header_path).read()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(rsk_[a-z0-9_]+)\s*\(", text)))
+    if header_paths is None:
+        inc = os.path.join(os.path.dirname(_HERE), "include")
+        header_paths = [os.path.join(inc, "rsk_codec.h"), os.path.join(inc, "rsk_rconn.h")]
+    names = set()
+    for hp in header_paths:
+        text = re.sub(r"/\*.*?\*/", "", open(hp).read(), flags=re.S)
+        text = re.sub(r"typedef[^;]*;", "", text)  # callback typedefs are not exported symbols
+        names |= set(re.findall(r"\b(rsk_[a-z0-9_]+)\s*\(", text))
+    return sorted(names)

@@ -161,14 +161,16 @@ class Codec:
 
     # ---- batch paths ---------------------------------------------------------------------
     def output_batch(self, payload, pay_off, pay_len, cmd, conv, conn_key, frame, frame_off, status,
-                     id=None, id_uniform: bytes = b"\0" * 8, pad16: bool = False, stream=None) -> None:
-        """RConn::Output framing for n packets (rsk_encode_batch).  pad16 sets RSK_ENC_ZERO_PAD16."""
+                     id=None, id_uniform: bytes = b"\0" * 8, pad16: bool = False, pad128: bool = False,
+                     stream=None) -> None:
+        """RConn::Output framing for n packets (rsk_encode_batch).  pad16 / pad128 set
+        RSK_ENC_ZERO_PAD16 / RSK_ENC_ZERO_PAD128."""
         n = pay_len.numel()
         ein = _abi.EncodeIn(_ptr(payload), _ptr(pay_off), _ptr(pay_len), _ptr(cmd), _ptr(conv),
                             _ptr(conn_key), _ptr(id),
                             (ctypes.c_uint8 * 8)(*bytes(id_uniform)[:8].ljust(8, b"\0")))
         eout = _abi.EncodeOut(_ptr(frame), _ptr(frame_off), _ptr(status),
-                              _abi.ENC_ZERO_PAD16 if pad16 else 0)
+                              (_abi.ENC_ZERO_PAD16 if pad16 else 0) | (_abi.ENC_ZERO_PAD128 if pad128 else 0))
         _check(lib().rsk_encode_batch(self._ctx, n, ctypes.byref(ein), ctypes.byref(eout),
                                       _stream(stream)), "rsk_encode_batch")
 

@@ -52,7 +52,7 @@ struct EncArgs {
     int32_t *status;
     uint32_t id_lo, id_hi;
     uint32_t n;
-    uint32_t pad;  // RSK_ENC_ZERO_PAD16
+    uint32_t pad;  // log2 of the zero-pad granularity (4: RSK_ENC_ZERO_PAD16, 7: RSK_ENC_ZERO_PAD128), 0 = none
 };
 
 __device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t j) {
@@ -134,11 +134,20 @@ __device__ __forceinline__ void st16(uint8_t *p, const uint4 &v) {
         *reinterpret_cast<uint4 *>(p) = v;
     }
 }
+// Store chunk data v whose first `lim` bytes belong to the frame: whole chunk when lim >= 16;
+// with padding, the tail (or the whole chunk, lim <= 0) is zeroed; without, only [0, lim).
 template <int NT>
 __device__ __forceinline__ void store_last16(uint8_t *d, const uint4 &v, int lim, bool pad) {
     if (lim >= 16) st16<NT>(d, v);
-    else if (pad) st16<NT>(d, rsk::keep_bytes16(v, lim));
+    else if (pad) st16<NT>(d, lim > 0 ? rsk::keep_bytes16(v, lim) : make_uint4(0u, 0u, 0u, 0u));
     else rsk::store_partial16(d, v, lim);
+}
+
+// Bytes written for a frame of flen bytes at d: flen, or up to the next 2^pad boundary.
+__device__ __forceinline__ uint32_t padded_len(const uint8_t *d, uint32_t flen, uint32_t pad) {
+    if (!pad) return flen;
+    const uint32_t m = (1u << pad) - 1u;
+    return flen + ((m + 1u - ((uint32_t)(reinterpret_cast<uintptr_t>(d) + flen) & m)) & m);
 }
 
 // ---- per-packet copy: the wave streams the frames of the packets in `vm` (16-B aligned), PU
@@ -168,7 +177,7 @@ __device__ __forceinline__ void copy_pkt(const EncArgs &a, const Lane1 &L, uint3
             sh[p] = (uint32_t)((reinterpret_cast<uintptr_t>(src) + 1u) & 15u);
             srcp[p] = src + 1 - sh[p];  // chunk k >= 2 = payload bytes [16k-31, 16k-15)
             last_rel[p] = (int32_t)flen[p] - RSK_HEAD_SIZE + (int32_t)sh[p] - 2;
-            const uint32_t nch = (flen[p] + 15u) >> 4;
+            const uint32_t nch = (flen[p] + 15u) >> 4;  // chunks holding frame bytes (loads)
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
                 const uint32_t k = lane + 64u * q;
@@ -184,7 +193,7 @@ __device__ __forceinline__ void copy_pkt(const EncArgs &a, const Lane1 &L, uint3
 #pragma unroll
         for (int p = 0; p < PU; ++p) {
             if (!on[p]) continue;
-            const uint32_t nch = (flen[p] + 15u) >> 4;
+            const uint32_t nch = (padded_len(dstp[p], flen[p], a.pad) + 15u) >> 4;  // chunks stored
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
                 const uint32_t k = lane + 64u * q;
@@ -255,7 +264,7 @@ __device__ __forceinline__ void copy_flat(const EncArgs &a, const Lane1 &L, uint
         st16<NT>(dst, make_uint4(L.H[0], L.H[1], L.H[2], L.H[3]));  // frame bytes [0, 32): always
         st16<NT>(dst + 16, make_uint4(L.H[4], L.H[5], L.H[6], L.H[7]));  // whole (31 + P >= 32)
         const uint32_t flen = (uint32_t)L.st;
-        cc = ((flen + 15u) >> 4) - 2u;
+        cc = ((padded_len(dst, flen, a.pad) + 15u) >> 4) - 2u;
         const uint32_t sh = (uint32_t)((reinterpret_cast<uintptr_t>(src) + 1u) & 15u);
         r.src_al = src + 1 - sh;
         r.dst = dst;
@@ -296,8 +305,10 @@ __device__ __forceinline__ void copy_flat(const EncArgs &a, const Lane1 &L, uint
                     if (cend[lo + st - 1] <= g) lo += st;
                 const CopyRec rr = recs[lo];
                 const uint32_t ro = 16u * (g - rr.cstart);
-                A[u] = ld16<NT>(rr.src_al + ro);
-                if (rr.sh != 0u && (int32_t)(ro + 16u) <= rr.last_rel) B[u] = ld16<NT>(rr.src_al + ro + 16);
+                if ((int32_t)ro + 32 < (int32_t)rr.flen) {  // chunk holds frame bytes (else pure pad)
+                    A[u] = ld16<NT>(rr.src_al + ro);
+                    if (rr.sh != 0u && (int32_t)(ro + 16u) <= rr.last_rel) B[u] = ld16<NT>(rr.src_al + ro + 16);
+                }
                 shs[u] = rr.sh;
                 dsts[u] = rr.dst + 32u + ro;
                 lims[u] = (int32_t)rr.flen - 32 - (int32_t)ro;
@@ -321,7 +332,7 @@ __device__ __forceinline__ void copy_bytes(const EncArgs &a, const Lane1 &L, uin
         uint32_t Hj[8];
 #pragma unroll
         for (int q = 0; q < 8; ++q) Hj[q] = rdl(L.H[q], j);
-        const uint32_t fend = a.pad ? fl + ((16u - ((reinterpret_cast<uintptr_t>(dst) + fl) & 15u)) & 15u) : fl;
+        const uint32_t fend = padded_len(dst, fl, a.pad);
         for (uint32_t f = lane; f < fend; f += 64u) {
             uint32_t byte;
             if (f >= fl) {
@@ -345,7 +356,30 @@ __device__ __forceinline__ void copy_bytes(const EncArgs &a, const Lane1 &L, uin
 // Measured crossover: flat wins below a tile-mean frame of ~256 B.
 constexpr uint32_t kFlatBelowMeanBytes = 256;
 
-// MODE: 0 per-packet, 1 flat, 2 hybrid (per-wave choice)
+// One 64-packet set per wave: phase 1, then the chosen copy path.
+template <int MODE, int PU, int U, int NT>
+__device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks, uint64_t i, uint32_t lane,
+                                           CopyRec *recs, uint32_t *cend) {
+    const Lane1 L = encode_phase1(a, ks, i);
+    const bool vec = L.st > 0 && !L.slow;
+    const uint64_t vm = __ballot(vec);
+    bool flat = MODE == 1;
+    if constexpr (MODE == 2) {
+        // set mean frame length over framed packets (wave reduction)
+        uint32_t fl = vec ? (uint32_t)L.st : 0u;
+#pragma unroll
+        for (int off = 32; off; off >>= 1) fl += __shfl_xor(fl, off);
+        const uint32_t cnt = (uint32_t)__popcll(vm);
+        flat = fl < kFlatBelowMeanBytes * cnt;
+    }
+    if (flat) copy_flat<U, NT>(a, L, lane, vec, recs, cend);
+    else copy_pkt<PU, NT>(a, L, lane, vm);
+    copy_bytes(a, L, lane, __ballot(L.st > 0 && L.slow));
+}
+
+// MODE: 0 per-packet, 1 flat, 2 hybrid (per-wave choice).
+// Tiled mapping: wave t takes packets [64t, 64t + 64) (coalesced descriptor loads, but the 5000+
+// co-resident waves each stream their own ~92 KB region).
 template <int MODE, int PU, int U, int NT>
 __global__ __launch_bounds__(kBlock) void k_encode(EncArgs a, KeySched ks) {
     __shared__ CopyRec recs[kWavesPerBlock][64];
@@ -353,22 +387,9 @@ __global__ __launch_bounds__(kBlock) void k_encode(EncArgs a, KeySched ks) {
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     const uint64_t base = ((uint64_t)blockIdx.x * kWavesPerBlock + w) * 64u;
     if (base >= a.n) return;  // wave-uniform; no block barriers below
-    const Lane1 L = encode_phase1(a, ks, base + lane);
-    const bool vec = L.st > 0 && !L.slow;
-    const uint64_t vm = __ballot(vec);
-    bool flat = MODE == 1;
-    if constexpr (MODE == 2) {
-        // tile mean frame length over framed packets (wave reduction)
-        uint32_t fl = vec ? (uint32_t)L.st : 0u;
-#pragma unroll
-        for (int off = 32; off; off >>= 1) fl += __shfl_xor(fl, off);
-        const uint32_t cnt = (uint32_t)__popcll(vm);
-        flat = fl < kFlatBelowMeanBytes * cnt;
-    }
-    if (flat) copy_flat<U, NT>(a, L, lane, vec, recs[w], cend[w]);
-    else copy_pkt<PU, NT>(a, L, lane, vm);
-    copy_bytes(a, L, lane, __ballot(L.st > 0 && L.slow));
+    encode_set<MODE, PU, U, NT>(a, ks, base + lane, lane, recs[w], cend[w]);
 }
+
 
 // ---------------------------------------------------------------------------------------------
 // Decode (shared by k_decode and k_parse_decode)
@@ -979,7 +1000,7 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
     std::memcpy(&a.id_lo, in->id_uniform, 4);
     std::memcpy(&a.id_hi, in->id_uniform + 4, 4);
     a.n = n;
-    a.pad = (out->flags & RSK_ENC_ZERO_PAD16) ? 1u : 0u;
+    a.pad = (out->flags & RSK_ENC_ZERO_PAD128) ? 7u : (out->flags & RSK_ENC_ZERO_PAD16) ? 4u : 0u;
     const uint64_t waves = (n + 63ull) / 64ull;
     const unsigned grid = (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
     hipStream_t st = (hipStream_t)stream;

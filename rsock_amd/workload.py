@@ -76,8 +76,10 @@ class Descriptors:
     first: int  # global index of packet 0 of this shard
 
 
-def describe(name: str, lo: int = 0, hi: int | None = None, n: int | None = None) -> Descriptors:
-    """Descriptors of packets [lo, hi) of config `name` (n overrides the config's packet count)."""
+def describe(name: str, lo: int = 0, hi: int | None = None, n: int | None = None,
+             frame_pitch: int | None = None) -> Descriptors:
+    """Descriptors of packets [lo, hi) of config `name` (n overrides the config's packet count;
+    frame_pitch overrides the frame slot pitch, a multiple of 16 >= 31 + P_max)."""
     idx, n_cfg, pmin, pmax, ports, mixed, corrupt_every = CONFIGS[name]
     n_total = n_cfg if n is None else n
     if hi is None:
@@ -103,7 +105,8 @@ def describe(name: str, lo: int = 0, hi: int | None = None, n: int | None = None
     # control bodies: conv reset carries a 4-byte conv, the others an 8-byte key
     plen = np.where(cmd == 1, np.uint16(4), np.where(cmd >= 2, np.uint16(8), plen)).astype(np.uint16)
     pay_pitch = round16(pmax)
-    frame_pitch = round16(HEAD + pmax)
+    frame_pitch = round16(HEAD + pmax) if frame_pitch is None else int(frame_pitch)
+    assert frame_pitch % 16 == 0 and frame_pitch >= HEAD + pmax
     local = np.arange(cnt, dtype=np.uint64)
     corrupt = (gi % np.uint64(corrupt_every) == np.uint64(7)) if corrupt_every else np.zeros(cnt, bool)
     return Descriptors(

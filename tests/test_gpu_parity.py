@@ -26,7 +26,7 @@ def dev(a: np.ndarray, gpu, dt=None):
 
 
 def run_encode(codec, gpu, payload, pay_off, pay_len, cmd, conv, ckey, frame_off, frame_bytes,
-               idarr=None, id_uniform=workload.ID_UNIFORM, frame_init=None, pad16=False):
+               idarr=None, id_uniform=workload.ID_UNIFORM, frame_init=None, pad16=False, pad128=False):
     import torch
 
     n = len(pay_len)
@@ -37,7 +37,8 @@ def run_encode(codec, gpu, payload, pay_off, pay_len, cmd, conv, ckey, frame_off
                        dev(pay_len.astype(np.uint16), gpu, np.int16), dev(cmd.astype(np.uint8), gpu),
                        dev(conv.astype(np.uint32), gpu, np.int32), dev(ckey.astype(np.uint64), gpu, np.int64),
                        frame, dev(frame_off.astype(np.uint64), gpu, np.int64), status,
-                       id=None if idarr is None else dev(idarr, gpu), id_uniform=id_uniform, pad16=pad16)
+                       id=None if idarr is None else dev(idarr, gpu), id_uniform=id_uniform, pad16=pad16,
+                       pad128=pad128)
     torch.cuda.synchronize()
     return frame.cpu().numpy(), status.cpu().numpy()
 
@@ -114,10 +115,10 @@ def vcodec(request, codec):
     codec.set_encode_variant(0)
 
 
-@pytest.mark.parametrize("layout,pad16", [("slots16", False), ("packed", False), ("odd_frames", False),
-                                          ("odd_payloads", False), ("slots16", True), ("odd_frames", True),
-                                          ("odd_payloads", True)])
-def test_encode_edge_lengths_and_layouts(vcodec, gpu, oracle, layout, pad16):
+@pytest.mark.parametrize("layout,pad", [("slots16", 0), ("packed", 0), ("odd_frames", 0), ("odd_payloads", 0),
+                                        ("slots16", 16), ("odd_frames", 16), ("odd_payloads", 16),
+                                        ("slots16", 128), ("odd_frames", 128)])
+def test_encode_edge_lengths_and_layouts(vcodec, gpu, oracle, layout, pad):
     codec = vcodec
     rng = np.random.default_rng(7)
     lens = [0, 1, 2, 3, 4, 7, 8, 15, 16, 17, 31, 32, 33, 47, 48, 63, 64, 65, 1000, 1023, 1024, 1025, 1400,
@@ -137,9 +138,11 @@ def test_encode_edge_lengths_and_layouts(vcodec, gpu, oracle, layout, pad16):
     if layout == "packed":
         frame_off = np.concatenate([[0], np.cumsum(flen)[:-1]]).astype(np.uint64)
     elif layout == "odd_frames":
-        frame_off = (np.arange(n) * 1509 + 5).astype(np.uint64)
+        # pad16's contract: bytes up to the 16-B boundary after a frame belong to no other frame,
+        # so padded runs need a gap >= 15 B after the longest (1500-B) frame
+        frame_off = (np.arange(n) * {0: 1509, 16: 1521, 128: 1664}[pad] + 5).astype(np.uint64)
     else:
-        frame_off = (np.arange(n) * 1504).astype(np.uint64)
+        frame_off = (np.arange(n) * (1664 if pad == 128 else 1504)).astype(np.uint64)
     frame_bytes = int(frame_off[-1]) + 1600
     cmd, conv, ckey = _rand_fields(rng, n)
     # pay_len is u16 in the ABI: 65535 stays representable, oversize statuses must come back -1
@@ -153,16 +156,16 @@ def test_encode_edge_lengths_and_layouts(vcodec, gpu, oracle, layout, pad16):
     fill = rng.integers(0, 256, frame_bytes, dtype=np.uint8)  # pre-existing bytes must survive
     exp_frames = fill.copy()
     got_frames, got_status = run_encode(codec, gpu, payload, pay_off, pl16, cmd, conv, ckey, frame_off,
-                                        frame_bytes, frame_init=fill, pad16=pad16)
+                                        frame_bytes, frame_init=fill, pad16=pad == 16, pad128=pad == 128)
     ef, es = oracle.encode_batch(KEY, payload, d, workload.ID_UNIFORM, frame_bytes=frame_bytes)
     assert np.array_equal(got_status, es)
     for i in range(n):
         if es[i] > 0:
             o = int(frame_off[i])
             exp_frames[o:o + es[i]] = ef[o:o + es[i]]
-            if pad16:  # RSK_ENC_ZERO_PAD16: zeros up to the next 16-B boundary (arena is 256-B aligned)
+            if pad:  # RSK_ENC_ZERO_PAD16/128: zeros up to the next pad boundary (arena is 256-B aligned)
                 e = o + int(es[i])
-                exp_frames[e:(e + 15) // 16 * 16] = 0
+                exp_frames[e:(e + pad - 1) // pad * pad] = 0
     bad = np.nonzero(got_frames != exp_frames)[0]
     assert bad.size == 0, f"{layout}: {bad.size} bytes differ, first at {bad[:8]}"
 

@@ -20,7 +20,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--variants", default="0,1,2,3")
-    ap.add_argument("--pads", default="0,1", help="RSK_ENC_ZERO_PAD16 off/on")
+    ap.add_argument("--pads", default="0,16", help="zero-pad modes: 0, 16, 128")
+    ap.add_argument("--frame-pitch", type=int, default=0)
     args = ap.parse_args()
     import torch
 
@@ -30,7 +31,7 @@ def main():
 
     dev = torch.device("cuda:0")
     n = args.packets or workload.CONFIGS[args.config][1]
-    d = workload.describe(args.config, 0, n, n=n)
+    d = workload.describe(args.config, 0, n, n=n, frame_pitch=args.frame_pitch or None)
     w = workload.DeviceWorkload(d, dev)
     cx = rc.Codec(b"hello135", 0)
     variants = [(int(v), int(p)) for v in args.variants.split(",") for p in args.pads.split(",")]
@@ -42,7 +43,8 @@ def main():
 
     def enc():
         cx.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
-                        w.status, id_uniform=workload.ID_UNIFORM, pad16=bool(cur["pad"]), stream=s)
+                        w.status, id_uniform=workload.ID_UNIFORM, pad16=cur["pad"] == 16,
+                        pad128=cur["pad"] == 128, stream=s)
 
     for v in variants:  # correctness: identical frame arenas
         cx.set_encode_variant(v[0])
@@ -75,7 +77,7 @@ def main():
         t = np.array(times[v])
         out[f"v{v[0]}pad{v[1]}"] = {"median_ms": round(float(np.median(t)), 4), "min_ms": round(float(t.min()), 4),
                   "GBps_median": round(byts / (np.median(t) * 1e-3) / 1e9, 1)}
-    print(json.dumps({"config": args.config, "packets": d.n, "variants": out}))
+    print(json.dumps({"config": args.config, "packets": d.n, "frame_pitch": d.frame_pitch, "variants": out}))
 
 
 if __name__ == "__main__":
