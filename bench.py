@@ -115,6 +115,9 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1 << 20)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal only: every rank uses GPU 0 (N ranks on a 1-GPU box)")
     args = ap.parse_args()
 
     import torch
@@ -128,17 +131,21 @@ def main() -> None:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    gpu = 0 if args.same_device else local
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
 
     cfg = args.config
     n = args.packets or workload.CONFIGS[cfg][1]
     # weak scaling: rank r owns packets [r*n, (r+1)*n) of the config's global stream
     d = workload.describe(cfg, rank * n, (rank + 1) * n, n=world * n)
     w = workload.DeviceWorkload(d, dev)
-    cx = rc.Codec(b"hello135", local)
+    cx = rc.Codec(b"hello135", gpu)
     cx.reserve(d.n)
     stream = torch.cuda.current_stream()
 
@@ -173,7 +180,7 @@ def main() -> None:
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed_max = float(t.item())

@@ -5,6 +5,19 @@
 
 namespace rsk {
 
+// Global (address space 1) views of generic pointers.  Pointers that pass through LDS records,
+// readlane'd offsets or selects lose their address space and would otherwise be accessed with
+// flat_* instructions, which count against both vmcnt and lgkmcnt and force conservative waits.
+#define RSK_GLOBAL __attribute__((address_space(1)))
+template <typename T>
+__device__ __forceinline__ RSK_GLOBAL T *gptr(T *p) {
+    return (RSK_GLOBAL T *)p;
+}
+template <typename T>
+__device__ __forceinline__ const RSK_GLOBAL T *gptr(const T *p) {
+    return (const RSK_GLOBAL T *)p;
+}
+
 // bytes [r, r+4) of the 8-byte little-endian pair {hi:lo}  (v_alignbyte_b32)
 __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t r) {
     return __builtin_amdgcn_alignbyte(hi, lo, r);
@@ -40,15 +53,16 @@ __device__ __forceinline__ uint4 funnel16(const uint4 &A, const uint4 &B, uint32
 // dwords, byte stores for the tail.  Neighbouring frames may own the rest of the 16-B chunk.
 __device__ __forceinline__ void store_partial16(uint8_t *p, const uint4 &v, int lim) {
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    RSK_GLOBAL uint8_t *g = gptr(p);
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
         const int lo = 4 * d;
         if (lo + 4 <= lim) {
-            *reinterpret_cast<uint32_t *>(p + lo) = w[d];
+            *reinterpret_cast<RSK_GLOBAL uint32_t *>(g + lo) = w[d];
         } else if (lo < lim) {
 #pragma unroll
             for (int b = 0; b < 3; ++b)
-                if (lo + b < lim) p[lo + b] = (uint8_t)(w[d] >> (8 * b));
+                if (lo + b < lim) g[lo + b] = (uint8_t)(w[d] >> (8 * b));
         }
     }
 }
@@ -64,9 +78,14 @@ __device__ __forceinline__ uint4 keep_bytes16(const uint4 &v, int lim) {
 
 // Store the last chunk of a frame: bytes [0, lim) of v at p (16-B aligned).  With pad, the whole
 // chunk is written with the tail zeroed (RSK_ENC_ZERO_PAD16); without, only [0, lim).
+typedef uint32_t gu32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void store16(uint8_t *p, const uint4 &v) {
+    const gu32x4 w = {v.x, v.y, v.z, v.w};
+    *reinterpret_cast<RSK_GLOBAL gu32x4 *>(gptr(p)) = w;
+}
 __device__ __forceinline__ void store_tail16(uint8_t *p, const uint4 &v, int lim, bool pad) {
-    if (lim >= 16) *reinterpret_cast<uint4 *>(p) = v;
-    else if (pad) *reinterpret_cast<uint4 *>(p) = keep_bytes16(v, lim);
+    if (lim >= 16) store16(p, v);
+    else if (pad) store16(p, keep_bytes16(v, lim));
     else store_partial16(p, v, lim);
 }
 
@@ -76,7 +95,7 @@ __device__ __forceinline__ void store_tail16(uint8_t *p, const uint4 &v, int lim
 template <int NW>
 __device__ __forceinline__ void load_window(const uint8_t *p, const uint8_t *last, uint32_t (&w)[NW]) {
     const uint32_t r = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3u);
-    const uint32_t *q = reinterpret_cast<const uint32_t *>(p - r);  // keeps the global AS
+    const RSK_GLOBAL uint32_t *q = reinterpret_cast<const RSK_GLOBAL uint32_t *>(gptr(p - r));
     const intptr_t lim = last - (p - r);                             // last valid byte, rel. to q
     uint32_t raw[NW + 1];
 #pragma unroll

@@ -118,21 +118,18 @@ __device__ __forceinline__ Lane1 encode_phase1(const EncArgs &a, const KeySched 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 template <int NT>
 __device__ __forceinline__ uint4 ld16(const uint8_t *p) {
-    if constexpr (NT & 1) {
-        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
-        return make_uint4(v.x, v.y, v.z, v.w);
-    } else {
-        return *reinterpret_cast<const uint4 *>(p);
-    }
+    const RSK_GLOBAL u32x4 *g = reinterpret_cast<const RSK_GLOBAL u32x4 *>(rsk::gptr(p));
+    u32x4 v;
+    if constexpr (NT & 1) v = __builtin_nontemporal_load(g);
+    else v = *g;
+    return make_uint4(v.x, v.y, v.z, v.w);
 }
 template <int NT>
 __device__ __forceinline__ void st16(uint8_t *p, const uint4 &v) {
-    if constexpr (NT & 2) {
-        const u32x4 w = {v.x, v.y, v.z, v.w};
-        __builtin_nontemporal_store(w, reinterpret_cast<u32x4 *>(p));
-    } else {
-        *reinterpret_cast<uint4 *>(p) = v;
-    }
+    RSK_GLOBAL u32x4 *g = reinterpret_cast<RSK_GLOBAL u32x4 *>(rsk::gptr(p));
+    const u32x4 w = {v.x, v.y, v.z, v.w};
+    if constexpr (NT & 2) __builtin_nontemporal_store(w, g);
+    else *g = w;
 }
 // Store chunk data v whose first `lim` bytes belong to the frame: whole chunk when lim >= 16;
 // with padding, the tail (or the whole chunk, lim <= 0) is zeroed; without, only [0, lim).
@@ -344,9 +341,9 @@ __device__ __forceinline__ void copy_bytes(const EncArgs &a, const Lane1 &L, uin
                     if ((f >> 2) == (uint32_t)q) wv = Hj[q];
                 byte = (wv >> (8u * (f & 3u))) & 0xffu;
             } else {
-                byte = src[f - RSK_HEAD_SIZE];
+                byte = rsk::gptr(src)[f - RSK_HEAD_SIZE];
             }
-            dst[f] = (uint8_t)byte;
+            rsk::gptr(dst)[f] = (uint8_t)byte;
         }
     }
 }
