@@ -17,6 +17,7 @@
  *   rsk_parse_decode_batch<- int RawTcp::RawInput(u_char*, const pcap_pkthdr*, const u_char*) conn/RawTcp.h:38, conn/RawTcp.cpp:138-237
  *                            + RawTcp::cap2uv size check (RawTcp.cpp:239-244) fused with RConn::OnRecv
  *   rsk_tcpinfo_encode_batch <- char* TcpInfo::Encode(char*, int) (21-B hand-off record)      bean/TcpInfo.cpp:20-32, bean/ConnInfo.cpp:12-20
+ *   rsk_encode_wire_batch <- RConn::Output + RawTcp::SendRawTcp -> libnet_build_tcp/ipv4     conn/RawTcp.cpp:280-341
  *   rsk_key_for_tcp/udp   <- KeyGenerator::KeyForTcp / KeyForUdp                              src/util/KeyGenerator.cpp:16-36
  */
 #ifndef RSK_CODEC_H
@@ -144,6 +145,27 @@ typedef struct rsk_encode_out {
  * Frames must not overlap each other or the payload arena. */
 int rsk_encode_batch(rsk_ctx *ctx, uint32_t n, const rsk_encode_in *in, const rsk_encode_out *out,
                      void *stream);
+
+/* ---- batch encode straight to wire packets (RConn::Output + RawTcp::SendRawTcp) ---
+ * RawTcp::SendRawTcp (conn/RawTcp.cpp:280-341) hands each frame to libnet 1.1.6:
+ * libnet_build_tcp(sp, dp, seq, ack, flag, win 65535, sum auto, urg 0) and
+ * libnet_build_ipv4(40 + frame, tos 0, id = mIpId++, IP_DF, TTL 64, IPPROTO_TCP, sum auto, src, dst).
+ * This entry point frames AND builds the packet in one pass: out->frame_arena + frame_off[i] receives
+ * [eth 14 if with_eth] | IPv4 20 | TCP 20 | tag 8 | EncHead 23 | payload, with the IPv4 header checksum
+ * and the TCP checksum (RFC 793 pseudo-header, RFC 1071 sum over header + frame) filled in.
+ * status[i] = wire length (14? + 40 + 31 + P), RSK_SEND_OVERSIZE or RSK_SEND_RESET as for
+ * rsk_encode_batch; out->flags as there (padding counts from the end of the wire packet). */
+typedef struct rsk_wire_in {
+    const uint32_t *src, *dst; /* [n] TcpInfo::src / dst: IPv4 addresses as stored (network order) */
+    const uint16_t *sp, *dp;   /* [n] ports, host order                                           */
+    const uint32_t *seq, *ack; /* [n] host order (TcpInfo seq / ack at send time)                 */
+    const uint8_t *flag;       /* [n] TCP flags (TcpInfo::flag)                                   */
+    const uint16_t *ip_id;     /* [n] IPv4 identification (RawTcp::mIpId++, host order)           */
+    uint8_t eth[14];           /* link header written before the IPv4 header when with_eth       */
+    uint8_t with_eth;          /* 0: LIBNET_RAW4 layout (IPv4 first); 1: Ethernet frame           */
+} rsk_wire_in;
+int rsk_encode_wire_batch(rsk_ctx *ctx, uint32_t n, const rsk_encode_in *in, const rsk_wire_in *wire,
+                          const rsk_encode_out *out, void *stream);
 
 /* ---- batch decode + verify (RConn::OnRecv) --------------------------------------------------- */
 typedef struct rsk_decode_out {

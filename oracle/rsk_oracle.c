@@ -310,6 +310,65 @@ int orc_tcpinfo_decode(const uint8_t *rec, int len, orc_tcpinfo *t) {
     return 21;
 }
 
+/* ------------------------------------------------------------------------------------------------
+ * Send-side wire build: RawTcp::SendRawTcp (conn/RawTcp.cpp:280-341) = libnet_build_tcp(sp, dp,
+ * seq, ack, flag, win 65535, sum 0 = auto, urg 0, len = 20 + frame) + libnet_build_ipv4(
+ * 40 + frame, tos 0, id = mIpId++, IP_DF, TTL_OUT 64, IPPROTO_TCP, sum 0 = auto, src, dst).
+ * Checksums per RFC 791 / RFC 793 (pseudo-header) with the RFC 1071 one's-complement sum.  libnet
+ * 1.1.6 is present only as the reference's prebuilt .a, so this restatement is pinned to the RFCs
+ * (and an independent Python restatement in tests), not to libnet output.
+ * --------------------------------------------------------------------------------------------- */
+uint16_t orc_inet_csum(const uint8_t *p, size_t n, uint32_t init) {
+    uint64_t s = init;
+    size_t i = 0;
+    for (; i + 1 < n; i += 2) s += ((uint32_t)p[i] << 8) | p[i + 1];
+    if (i < n) s += (uint32_t)p[i] << 8;
+    while (s >> 16) s = (s & 0xffff) + (s >> 16);
+    return (uint16_t)~s;
+}
+
+int orc_build_wire(const uint8_t *frame, int frame_len, uint32_t src, uint32_t dst, uint16_t sp,
+                   uint16_t dp, uint32_t seq, uint32_t ack, uint8_t flag, uint16_t ip_id,
+                   const uint8_t *eth, uint8_t *wire) {
+    int o = 0;
+    if (eth) {
+        memcpy(wire, eth, 14);
+        o = 14;
+    }
+    uint8_t *ip = wire + o, *tcp = ip + 20;
+    const int tot = 40 + frame_len;
+    ip[0] = 0x45; ip[1] = 0;
+    ip[2] = (uint8_t)(tot >> 8); ip[3] = (uint8_t)tot;
+    ip[4] = (uint8_t)(ip_id >> 8); ip[5] = (uint8_t)ip_id;
+    ip[6] = 0x40; ip[7] = 0x00; /* IP_DF */
+    ip[8] = 64; ip[9] = 6;
+    ip[10] = ip[11] = 0;
+    put_le(ip + 12, src, 4); /* stored network-order word, copied as is */
+    put_le(ip + 16, dst, 4);
+    const uint16_t ic = orc_inet_csum(ip, 20, 0);
+    ip[10] = (uint8_t)(ic >> 8); ip[11] = (uint8_t)ic;
+    tcp[0] = (uint8_t)(sp >> 8); tcp[1] = (uint8_t)sp;
+    tcp[2] = (uint8_t)(dp >> 8); tcp[3] = (uint8_t)dp;
+    for (int k = 0; k < 4; k++) tcp[4 + k] = (uint8_t)(seq >> (24 - 8 * k));
+    for (int k = 0; k < 4; k++) tcp[8 + k] = (uint8_t)(ack >> (24 - 8 * k));
+    tcp[12] = 0x50; tcp[13] = flag;
+    tcp[14] = 0xff; tcp[15] = 0xff;
+    tcp[16] = tcp[17] = 0;
+    tcp[18] = tcp[19] = 0;
+    memcpy(tcp + 20, frame, (size_t)frame_len);
+    /* pseudo-header: src, dst, zero, proto, TCP length */
+    uint8_t ph[12];
+    memcpy(ph, ip + 12, 8);
+    ph[8] = 0; ph[9] = 6;
+    ph[10] = (uint8_t)((20 + frame_len) >> 8); ph[11] = (uint8_t)(20 + frame_len);
+    uint64_t s = 0;
+    for (int i = 0; i < 12; i += 2) s += ((uint32_t)ph[i] << 8) | ph[i + 1];
+    while (s >> 16) s = (s & 0xffff) + (s >> 16);
+    const uint16_t tc = orc_inet_csum(tcp, (size_t)(20 + frame_len), (uint32_t)s);
+    tcp[16] = (uint8_t)(tc >> 8); tcp[17] = (uint8_t)tc;
+    return o + tot;
+}
+
 /* KeyGenerator.cpp:16-36 and KeyGenerator.h:21-23,51: INIT_KEY 0 | TYPE | (dp << 16) | sp. */
 uint64_t orc_key_for_tcp(uint16_t sp, uint16_t dp) {
     return 0x10000000ull | ((uint64_t)dp << 16) | (uint64_t)sp;

@@ -75,6 +75,18 @@ int orc_rawinput(const uint8_t *pkt, uint32_t wire_len, uint32_t cap_len, int da
 int orc_tcpinfo_encode(const orc_tcpinfo *t, uint8_t rec[21]);
 int orc_tcpinfo_decode(const uint8_t *rec, int len, orc_tcpinfo *t);
 
+/* RawTcp::SendRawTcp (conn/RawTcp.cpp:280-341) through libnet 1.1.6: the wire packet for one frame.
+ * [eth 14 if eth != NULL] | IPv4 20 (v4, IHL 5, tos 0, tot_len, id, DF, ttl 64, proto 6, checksum,
+ * src, dst) | TCP 20 (sp, dp, seq, ack, doff 5, flags, win 65535, checksum, urg 0) | frame.
+ * src/dst are the stored network-byte-order words (TcpInfo::src/dst); sp, dp, seq, ack host order.
+ * Returns the wire length. */
+int orc_build_wire(const uint8_t *frame, int frame_len, uint32_t src, uint32_t dst, uint16_t sp,
+                   uint16_t dp, uint32_t seq, uint32_t ack, uint8_t flag, uint16_t ip_id,
+                   const uint8_t *eth, uint8_t *wire);
+/* RFC 1071 Internet checksum of bytes (as stored on the wire), returned in network byte order
+ * value (i.e. the 16-bit value whose big-endian bytes go into the header). */
+uint16_t orc_inet_csum(const uint8_t *p, size_t n, uint32_t init);
+
 /* KeyGenerator::KeyForTcp / KeyForUdp (src/util/KeyGenerator.cpp:16-36) */
 uint64_t orc_key_for_tcp(uint16_t sp, uint16_t dp);
 uint64_t orc_key_for_udp(uint16_t sp, uint16_t dp);

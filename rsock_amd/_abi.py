@@ -56,6 +56,13 @@ ENC_ZERO_PAD16 = 0x1
 ENC_ZERO_PAD128 = 0x2
 
 
+class WireIn(ctypes.Structure):
+    _fields_ = [
+        ("src", _vp), ("dst", _vp), ("sp", _vp), ("dp", _vp), ("seq", _vp), ("ack", _vp), ("flag", _vp),
+        ("ip_id", _vp), ("eth", ctypes.c_uint8 * 14), ("with_eth", ctypes.c_uint8),
+    ]
+
+
 class DecodeOut(ctypes.Structure):
     _fields_ = [
         ("hlen", _vp),
@@ -95,6 +102,8 @@ SIGNATURES = [
     ("rsk_version", ctypes.c_char_p, []),
     ("rsk_encode_batch", ctypes.c_int,
      [_vp, ctypes.c_uint32, ctypes.POINTER(EncodeIn), ctypes.POINTER(EncodeOut), _vp]),
+    ("rsk_encode_wire_batch", ctypes.c_int,
+     [_vp, ctypes.c_uint32, ctypes.POINTER(EncodeIn), ctypes.POINTER(WireIn), ctypes.POINTER(EncodeOut), _vp]),
     ("rsk_decode_batch", ctypes.c_int,
      [_vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, ctypes.POINTER(DecodeOut), _vp]),
     ("rsk_parse_decode_batch", ctypes.c_int,

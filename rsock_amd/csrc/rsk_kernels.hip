@@ -389,6 +389,233 @@ __global__ __launch_bounds__(kBlock) void k_encode(EncArgs a, KeySched ks) {
 
 
 // ---------------------------------------------------------------------------------------------
+// Encode straight to wire packets (RConn::Output + RawTcp::SendRawTcp / libnet)
+// ---------------------------------------------------------------------------------------------
+struct WireArgs {
+    const uint32_t *src, *dst;
+    const uint16_t *sp, *dp;
+    const uint32_t *seq, *ack;
+    const uint8_t *flag;
+    const uint16_t *ip_id;
+    uint32_t eth[4];  // 14 link-header bytes, LE words
+};
+
+// one's-complement sum of the little-endian 16-bit halves of w (RFC 1071 is byte-order agnostic:
+// summing LE halfwords and storing ~sum little-endian gives the big-endian checksum bytes)
+__device__ __forceinline__ uint32_t hsum(uint32_t w) { return (w & 0xffffu) + (w >> 16); }
+__device__ __forceinline__ uint32_t fold16(uint32_t s) {
+    s = (s & 0xffffu) + (s >> 16);
+    s = (s & 0xffffu) + (s >> 16);
+    return s;
+}
+// OR `nb` bytes of v (LE) into the byte image PW at byte offset off (all compile-time after inlining)
+template <int N>
+__device__ __forceinline__ void put_bytes(uint32_t (&PW)[N], int off, uint32_t v, int nb) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+        if (b < nb) PW[(off + b) >> 2] |= ((v >> (8 * b)) & 0xffu) << (8 * ((off + b) & 3));
+}
+
+template <int E>  // E = link header bytes before IPv4: 0 (RAW4) or 14 (Ethernet)
+struct WireGeom {
+    static constexpr int HL = E + 40;                // bytes before the frame
+    static constexpr int HB = HL + RSK_HEAD_SIZE;     // bytes before the payload
+    static constexpr int NPRE = HB / 16 + 1;          // chunks built from the prefix image
+    static constexpr int NPW = 4 * NPRE;              // prefix words (covers HB + 16 payload bytes at least... up to 16*NPRE)
+    static constexpr int D0 = 16 * NPRE - HB;         // payload offset of chunk NPRE's first byte
+    static constexpr int CK = E + 36;                 // TCP checksum byte offset
+    static constexpr int IPC = E + 10;                // IPv4 checksum byte offset
+};
+
+template <int E, int PU>
+__global__ __launch_bounds__(kBlock) void k_encode_wire(EncArgs a, WireArgs wa, KeySched ks) {
+    using G = WireGeom<E>;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t base = ((uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * 64u;
+    if (base >= a.n) return;
+    const uint64_t i = base + lane;
+    // ---- phase 1: frame words (encode_phase1 writes the frame status; patch it to the wire length)
+    Lane1 L = encode_phase1(a, ks, i);
+    uint32_t PW[G::NPW];
+#pragma unroll
+    for (int q = 0; q < G::NPW; ++q) PW[q] = 0;
+    uint32_t sum_pre = 0;  // TCP checksum contribution of the prefix chunks (+ pseudo-header)
+    int32_t wst = L.st;
+    if (L.st > 0) {
+        const uint32_t flen = (uint32_t)L.st, P = flen - RSK_HEAD_SIZE;
+        const uint32_t wlen = G::HL + flen;
+        wst = (int32_t)wlen;
+        a.status[i] = wst;
+        const uint32_t src = wa.src[i], dst = wa.dst[i], sp = wa.sp[i], dp = wa.dp[i];
+        const uint32_t seq = wa.seq[i], ack = wa.ack[i], fl = wa.flag[i], id = wa.ip_id[i];
+        if constexpr (E > 0) {
+#pragma unroll
+            for (int b = 0; b < E; b += 4) put_bytes(PW, b, wa.eth[b >> 2], E - b < 4 ? E - b : 4);
+        }
+        // IPv4 header (libnet_build_ipv4): 45 00 | len | id | 40 00 | 40 06 | csum | src | dst
+        const uint32_t tot = 40u + flen;
+        put_bytes(PW, E + 0, 0x45u | (rsk::bswap16(tot) << 16), 4);
+        put_bytes(PW, E + 4, rsk::bswap16(id) | (0x0040u << 16), 4);
+        put_bytes(PW, E + 8, 64u | (6u << 8), 2);
+        put_bytes(PW, E + 12, src, 4);
+        put_bytes(PW, E + 16, dst, 4);
+        const uint32_t ips = hsum(0x45u | (rsk::bswap16(tot) << 16)) + hsum(rsk::bswap16(id) | (0x0040u << 16)) +
+                             hsum(64u | (6u << 8)) + hsum(src) + hsum(dst);
+        put_bytes(PW, G::IPC, ~fold16(ips) & 0xffffu, 2);
+        // TCP header (libnet_build_tcp): sp dp seq ack | 50 flags | ffff | csum | 0000
+        const uint32_t t0 = rsk::bswap16(sp) | (rsk::bswap16(dp) << 16), t1 = rsk::bswap32(seq),
+                       t2 = rsk::bswap32(ack), t3 = 0x50u | (fl << 8) | (0xffffu << 16);
+        put_bytes(PW, E + 20, t0, 4);
+        put_bytes(PW, E + 24, t1, 4);
+        put_bytes(PW, E + 28, t2, 4);
+        put_bytes(PW, E + 32, t3, 4);
+        // frame bytes [0, 31) = tag + EncHead (H[7]'s top byte is payload[0], written below)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) put_bytes(PW, G::HL + 4 * q, L.H[q], q == 7 ? 3 : 4);
+        // payload bytes [0, 16) (bounded by P; bytes past P stay zero)
+        const uint8_t *pay = a.payload + L.po;
+        uint32_t pw[4];
+        rsk::load_window<4>(pay, pay + P - 1, pw);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int k = (int)P - 4 * q;
+            pw[q] &= k >= 4 ? 0xffffffffu : (k <= 0 ? 0u : ((1u << (8 * k)) - 1u));
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int off = G::HB + 4 * q;
+            const int nb = (off + 4 <= 4 * G::NPW) ? 4 : 4 * G::NPW - off;
+            if (nb > 0) put_bytes(PW, off, pw[q], nb);
+        }
+        // pseudo-header (src, dst, 0, 6, tcp_len) + TCP header + prefix frame/payload bytes, from the
+        // TCP header start (even offset E + 20) to the end of the prefix chunks
+        uint32_t s = hsum(src) + hsum(dst) + (6u << 8) + rsk::bswap16(20u + flen);
+#pragma unroll
+        for (int q = (E + 20) / 4; q < G::NPW; ++q) s += ((E + 20) % 4 && q == (E + 20) / 4) ? (PW[q] >> 16) : hsum(PW[q]);
+        sum_pre = s;
+    }
+    // ---- copy: per packet, prefix chunks from the lane's image, payload chunks funnel-shifted
+    const bool vec = L.st > 0 && !L.slow;
+    uint64_t vm = __ballot(vec);
+    while (vm) {
+        uint32_t js[PU];
+        bool on[PU];
+#pragma unroll
+        for (int p = 0; p < PU; ++p) {
+            on[p] = vm != 0ull;
+            js[p] = on[p] ? (uint32_t)__builtin_ctzll(vm) : 0u;
+            if (on[p]) vm &= vm - 1ull;
+        }
+        uint4 v[PU][2];
+        uint32_t part[PU];
+        uint32_t wlen[PU];
+        uint8_t *dstp[PU];
+#pragma unroll
+        for (int p = 0; p < PU; ++p) {
+            wlen[p] = on[p] ? (uint32_t)rdl((uint32_t)wst, js[p]) : 0u;
+            const uint32_t P = wlen[p] - G::HB;
+            const uint8_t *pay = a.payload + rdl64(L.po, js[p]);
+            dstp[p] = a.frame + rdl64(L.fo, js[p]);
+            const uint32_t sh = (uint32_t)((reinterpret_cast<uintptr_t>(pay) + G::D0) & 15u);
+            const uint8_t *src_al = pay + G::D0 - sh;
+            const int32_t last_rel = (int32_t)P - 1 - G::D0 + (int32_t)sh;
+            const uint32_t nch = (wlen[p] + 15u) >> 4;
+            part[p] = 0;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const uint32_t k = lane + 64u * q;
+                uint4 A = make_uint4(0u, 0u, 0u, 0u), B = make_uint4(0u, 0u, 0u, 0u);
+                if (k >= (uint32_t)G::NPRE && k < nch) {
+                    const uint32_t ro = 16u * (k - G::NPRE);
+                    A = ld16<0>(src_al + ro);
+                    if (sh != 0u && (int32_t)(ro + 16u) <= last_rel) B = ld16<0>(src_al + ro + 16u);
+                }
+                v[p][q] = rsk::funnel16(A, B, sh);
+                const int lim = (int)wlen[p] - 16 * (int)k;
+                if (k >= (uint32_t)G::NPRE && k < nch) {
+                    if (lim < 16) v[p][q] = rsk::keep_bytes16(v[p][q], lim);
+                    part[p] += hsum(v[p][q].x) + hsum(v[p][q].y) + hsum(v[p][q].z) + hsum(v[p][q].w);
+                }
+            }
+        }
+        // per-packet wave reduction of the payload-chunk sums -> TCP checksum
+#pragma unroll
+        for (int p = 0; p < PU; ++p) {
+            uint32_t t = fold16(part[p]);
+#pragma unroll
+            for (int off = 32; off; off >>= 1) t += __shfl_xor(t, off);
+            t += rdl(sum_pre, js[p]);
+            part[p] = ~fold16(t) & 0xffffu;  // now the checksum, uniform
+        }
+#pragma unroll
+        for (int p = 0; p < PU; ++p) {
+            if (!on[p]) continue;
+            const uint32_t nst = (padded_len(dstp[p], wlen[p], a.pad) + 15u) >> 4;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const uint32_t k = lane + 64u * q;
+                if (k >= nst) continue;
+                uint4 val = v[p][q];
+                if (k < (uint32_t)G::NPRE) {
+                    uint32_t Wj[G::NPW];
+#pragma unroll
+                    for (int t = 0; t < G::NPW; ++t) Wj[t] = rdl(PW[t], js[p]);
+                    uint32_t w4[4] = {0, 0, 0, 0};
+#pragma unroll
+                    for (int c = 0; c < G::NPRE; ++c)
+                        if (k == (uint32_t)c) {
+                            w4[0] = Wj[4 * c]; w4[1] = Wj[4 * c + 1]; w4[2] = Wj[4 * c + 2]; w4[3] = Wj[4 * c + 3];
+                        }
+                    if (k == (uint32_t)(G::CK / 16)) w4[(G::CK & 15) >> 2] |= part[p] << (8 * (G::CK & 3));
+                    val = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+                }
+                store_last16<0>(dstp[p] + 16u * k, val, (int)wlen[p] - 16 * (int)k, a.pad != 0u);
+            }
+        }
+    }
+    // wire packets that are not 16-B aligned: byte path (prefix bytes from the lane image)
+    uint64_t sm = __ballot(L.st > 0 && L.slow);
+    while (sm) {
+        const uint32_t j = (uint32_t)__builtin_ctzll(sm);
+        sm &= sm - 1ull;
+        const uint32_t wl = rdl((uint32_t)wst, j);
+        const uint8_t *pay = a.payload + rdl64(L.po, j);
+        uint8_t *dst = a.frame + rdl64(L.fo, j);
+        uint32_t Wj[G::NPW];
+#pragma unroll
+        for (int t = 0; t < G::NPW; ++t) Wj[t] = rdl(PW[t], j);
+        // checksum: prefix part from the packet lane, payload bytes past the prefix summed here
+        uint32_t s = 0;
+        for (uint32_t f = 16u * G::NPRE + lane; f < wl; f += 64u) {
+            const uint32_t byte = rsk::gptr(pay)[f - G::HB];
+            s += byte << (8u * ((f - (E + 20)) & 1u));
+        }
+        s = fold16(s);
+#pragma unroll
+        for (int off = 32; off; off >>= 1) s += __shfl_xor(s, off);
+        const uint32_t ck = ~fold16(s + rdl(sum_pre, j)) & 0xffffu;
+        const uint32_t fend = padded_len(dst, wl, a.pad);
+        for (uint32_t f = lane; f < fend; f += 64u) {
+            uint32_t byte = 0;
+            if (f >= wl) {
+                byte = 0;
+            } else if (f < 16u * G::NPRE) {
+                uint32_t wv = 0;
+#pragma unroll
+                for (int q = 0; q < G::NPW; ++q)
+                    if ((f >> 2) == (uint32_t)q) wv = Wj[q];
+                byte = (wv >> (8u * (f & 3u))) & 0xffu;
+                if (f == (uint32_t)G::CK) byte = ck & 0xffu;
+                if (f == (uint32_t)G::CK + 1u) byte = ck >> 8;
+            } else {
+                byte = rsk::gptr(pay)[f - G::HB];
+            }
+            rsk::gptr(dst)[f] = (uint8_t)byte;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Decode (shared by k_decode and k_parse_decode)
 // ---------------------------------------------------------------------------------------------
 struct Dec {
@@ -1016,6 +1243,40 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         default: hipLaunchKernelGGL((k_encode<2, 4, 4, 0>), gd, bd, 0, st, a, c->ks); break;
     }
     return launch_check("k_encode");
+}
+
+int rsk_encode_wire_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_wire_in *wire,
+                          const rsk_encode_out *out, void *stream) {
+    if (!c || !in || !wire || !out) return RSK_EINVAL;
+    if (n == 0) return RSK_OK;
+    if (!in->payload_arena || !in->pay_off || !in->pay_len || !in->cmd || !in->conv || !in->conn_key ||
+        !out->frame_arena || !out->frame_off || !out->status || !wire->src || !wire->dst || !wire->sp ||
+        !wire->dp || !wire->seq || !wire->ack || !wire->flag || !wire->ip_id)
+        return RSK_EINVAL;
+    if (in->id && (reinterpret_cast<uintptr_t>(in->id) & 7u)) return RSK_EINVAL;
+    DeviceGuard g(c->device);
+    if (!g.ok) return RSK_EDEVICE;
+    EncArgs a;
+    a.payload = in->payload_arena; a.pay_off = in->pay_off; a.pay_len = in->pay_len; a.cmd = in->cmd;
+    a.conv = in->conv; a.conn_key = in->conn_key; a.id = in->id;
+    a.frame = out->frame_arena; a.frame_off = out->frame_off; a.status = out->status;
+    std::memcpy(&a.id_lo, in->id_uniform, 4);
+    std::memcpy(&a.id_hi, in->id_uniform + 4, 4);
+    a.n = n;
+    a.pad = (out->flags & RSK_ENC_ZERO_PAD128) ? 7u : (out->flags & RSK_ENC_ZERO_PAD16) ? 4u : 0u;
+    WireArgs w;
+    w.src = wire->src; w.dst = wire->dst; w.sp = wire->sp; w.dp = wire->dp; w.seq = wire->seq;
+    w.ack = wire->ack; w.flag = wire->flag; w.ip_id = wire->ip_id;
+    uint8_t eth[16] = {0};
+    std::memcpy(eth, wire->eth, 14);
+    std::memcpy(w.eth, eth, 16);
+    const uint64_t waves = (n + 63ull) / 64ull;
+    const unsigned grid = (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
+    if (wire->with_eth)
+        hipLaunchKernelGGL((k_encode_wire<14, 2>), dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, a, w, c->ks);
+    else
+        hipLaunchKernelGGL((k_encode_wire<0, 2>), dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, a, w, c->ks);
+    return launch_check("k_encode_wire");
 }
 
 int rsk_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *frame_arena, const uint64_t *frame_off,

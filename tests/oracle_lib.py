@@ -55,6 +55,11 @@ class Oracle:
                                    ctypes.c_int, ctypes.POINTER(OrcTcpInfo)]
         L.orc_tcpinfo_encode.argtypes = [ctypes.POINTER(OrcTcpInfo), ctypes.c_char_p]
         L.orc_tcpinfo_decode.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(OrcTcpInfo)]
+        L.orc_build_wire.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint16,
+                                     ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint8,
+                                     ctypes.c_uint16, ctypes.c_char_p, ctypes.c_char_p]
+        L.orc_inet_csum.restype = ctypes.c_uint16
+        L.orc_inet_csum.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32]
         L.orc_key_for_tcp.restype = ctypes.c_uint64
         L.orc_key_for_tcp.argtypes = [ctypes.c_uint16, ctypes.c_uint16]
         L.orc_key_for_udp.restype = ctypes.c_uint64
@@ -123,6 +128,11 @@ class Oracle:
 
     def key_for_udp(self, sp: int, dp: int) -> int:
         return self.L.orc_key_for_udp(sp, dp)
+
+    def build_wire(self, frame: bytes, src, dst, sp, dp, seq, ack, flag, ip_id, eth: bytes | None = None) -> bytes:
+        out = ctypes.create_string_buffer(len(frame) + 64)
+        n = self.L.orc_build_wire(frame, len(frame), src, dst, sp, dp, seq, ack, flag, ip_id, eth, out)
+        return out.raw[:n]
 
     def splitmix_bytes(self, seed: int, n: int) -> np.ndarray:
         out = np.empty(n, np.uint8)

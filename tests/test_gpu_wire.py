@@ -1,0 +1,118 @@
+"""GPU: rsk_encode_wire_batch (RConn::Output + RawTcp::SendRawTcp / libnet build)
+against the oracle, byte for byte, for both link layouts, odd payload offsets, unaligned packet
+offsets (byte path) and the zero-pad modes; every packet's IPv4 and TCP checksums re-verified."""
+from __future__ import annotations
+
+import struct
+
+import numpy as np
+import pytest
+
+from rsock_amd import workload
+from tests.test_gpu_parity import dev
+from tests.test_wire_oracle import py_csum
+
+pytestmark = pytest.mark.gpu
+KEY = b"hello135"
+
+
+@pytest.mark.parametrize("eth", [False, True])
+@pytest.mark.parametrize("layout", ["aligned", "odd_payload", "odd_wire"])
+@pytest.mark.parametrize("pad16", [False, True])
+def test_wire_batch(codec, gpu, oracle, eth, layout, pad16):
+    import torch
+
+    rng = np.random.default_rng(hash((eth, layout, pad16)) & 0xFFFF)
+    lens = [0, 1, 2, 8, 9, 10, 11, 12, 15, 16, 17, 31, 32, 33, 100, 1000, 1400, 1468, 1469, 1470] + \
+        list(rng.integers(1, 1470, 400))
+    n = len(lens)
+    plen = np.array(lens, np.uint16)
+    pitch_p = 1504
+    pay_off = (np.arange(n) * pitch_p + (np.arange(n) % 13 if layout == "odd_payload" else 0)).astype(np.uint64)
+    payload = rng.integers(0, 256, n * pitch_p + 64, dtype=np.uint8)
+    pitch_w = 1600
+    wire_off = (np.arange(n) * pitch_w + (5 if layout == "odd_wire" else 0)).astype(np.uint64)
+    cmd = rng.integers(0, 5, n).astype(np.uint8)
+    conv = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    ckey = rng.integers(0, 2**63, n, dtype=np.uint64)
+    src = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    dst = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    sp = rng.integers(1, 65536, n).astype(np.uint16)
+    dp = rng.integers(1, 65536, n).astype(np.uint16)
+    seq = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    ack = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    flag = rng.integers(0, 256, n).astype(np.uint8)
+    ipid = rng.integers(0, 65536, n).astype(np.uint16)
+    ethb = bytes(rng.integers(0, 256, 14, dtype=np.uint8)) if eth else None
+    fill = rng.integers(0, 256, n * pitch_w + 64, dtype=np.uint8)
+    wire = dev(fill, gpu)
+    status = torch.empty(n, dtype=torch.int32, device=gpu)
+    codec.output_wire_batch(dev(payload, gpu), dev(pay_off, gpu, np.int64), dev(plen, gpu, np.int16), dev(cmd, gpu),
+                            dev(conv, gpu, np.int32), dev(ckey, gpu, np.int64), dev(src, gpu, np.int32),
+                            dev(dst, gpu, np.int32), dev(sp, gpu, np.int16), dev(dp, gpu, np.int16),
+                            dev(seq, gpu, np.int32), dev(ack, gpu, np.int32), dev(flag, gpu), dev(ipid, gpu, np.int16),
+                            wire, dev(wire_off, gpu, np.int64), status, eth=ethb, id_uniform=workload.ID_UNIFORM,
+                            pad16=pad16)
+    torch.cuda.synchronize()
+    got, st = wire.cpu().numpy(), status.cpu().numpy()
+    exp = fill.copy()
+    L = 14 if eth else 0
+    for i in range(n):
+        p = payload[int(pay_off[i]): int(pay_off[i]) + int(plen[i])].tobytes()
+        fst, frame = oracle.rconn_output(KEY, p, int(cmd[i]), workload.ID_UNIFORM, int(conv[i]), int(ckey[i]))
+        if fst <= 0:
+            assert st[i] == fst
+            continue
+        w = oracle.build_wire(frame, int(src[i]), int(dst[i]), int(sp[i]), int(dp[i]), int(seq[i]), int(ack[i]),
+                              int(flag[i]), int(ipid[i]), eth=ethb)
+        assert st[i] == len(w), i
+        o = int(wire_off[i])
+        exp[o: o + len(w)] = np.frombuffer(w, np.uint8)
+        if pad16:
+            e = o + len(w)
+            exp[e: (e + 15) // 16 * 16] = 0
+        g = got[o: o + len(w)].tobytes()
+        assert py_csum(g[L: L + 20]) == 0, i                      # IPv4 header checksum verifies
+        pseudo = g[L + 12: L + 20] + struct.pack("!BBH", 0, 6, len(w) - L - 20)
+        assert py_csum(pseudo + g[L + 20:]) == 0, i               # TCP checksum verifies
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, f"{bad.size} bytes differ, first at {bad[:8]}"
+
+
+def test_wire_to_parse_loop(codec, gpu):
+    """Send path -> receive path on the device: Ethernet wire packets built by rsk_encode_wire_batch
+    are exactly what pcap captures, so rsk_parse_decode_batch must DELIVER and verify every one and
+    hand back the TcpInfo (reversed "self" view) and the EncHead fields."""
+    import torch
+
+    from rsock_amd.codec import DecodeBuffers, TcpInfoBuffers
+
+    d = workload.describe("c4", 0, 20000, n=20000)
+    w = workload.DeviceWorkload(d, gpu)
+    n = d.n
+    g = torch.Generator(device=gpu)
+    g.manual_seed(5)
+    ri = lambda hi, dt: torch.randint(0, hi, (n,), device=gpu, generator=g, dtype=torch.int64).to(dt)  # noqa: E731
+    src, dst = ri(2**31, torch.int32), ri(2**31, torch.int32)
+    sp, dp = ri(2**15, torch.int16) + 1, ri(2**15, torch.int16) + 1
+    seq, ack, ipid = ri(2**31, torch.int32), ri(2**31, torch.int32), ri(2**15, torch.int16)
+    flag = torch.full((n,), 0x18, dtype=torch.uint8, device=gpu)
+    pitch = 1488
+    wire = torch.zeros(n * pitch, dtype=torch.uint8, device=gpu)
+    woff = torch.arange(n, device=gpu, dtype=torch.int64) * pitch
+    st = torch.empty(n, dtype=torch.int32, device=gpu)
+    eth = bytes([2, 0, 0, 0, 0, 1, 2, 0, 0, 0, 0, 2, 8, 0])
+    codec.output_wire_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, src, dst, sp, dp, seq, ack,
+                            flag, ipid, wire, woff, st, eth=eth, id_uniform=workload.ID_UNIFORM)
+    tcp, out = TcpInfoBuffers.alloc(n, gpu), DecodeBuffers.alloc(n, gpu)
+    codec.rawinput_batch(wire, woff, st, st, 1, 0, tcp, out)
+    torch.cuda.synchronize()
+    assert bool((tcp.parse_status == 1).all()) and bool((out.status == 1).all())
+    assert int(out.n_valid.item()) == n
+    assert torch.equal(tcp.src, dst) and torch.equal(tcp.dst, src)          # reversed view (RawTcp.cpp:213-216)
+    assert torch.equal(tcp.sp, dp) and torch.equal(tcp.dp, sp)
+    plen = (w.pay_len.to(torch.int64) & 0xFFFF) + 31
+    assert torch.equal((tcp.seq.to(torch.int64) & 0xFFFFFFFF), ((seq.to(torch.int64) & 0xFFFFFFFF) + plen) & 0xFFFFFFFF)
+    assert torch.equal(tcp.cap_pay_off.to(torch.int64), torch.full_like(plen, 54))
+    assert torch.equal(out.conv, w.conv) and torch.equal(out.conn_key, w.conn_key) and torch.equal(out.cmd, w.cmd)
+    assert torch.equal(out.pay_len.to(torch.int64) & 0xFFFF, plen - 31)

@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""Per-path kernel timings on one config (device-resident, HIP events, interleaved rounds in one
+process): encode (framing), encode_wire RAW4 / Ethernet (framing + IPv4/TCP build + checksums),
+decode (verify + compaction), parse_decode (pcap parse of the Ethernet wire packets + verify).
+    python tools/bench_paths.py [--config c3] [--rounds 5] [--reps 10]"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--packets", type=int, default=0)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=10)
+    args = ap.parse_args()
+    import torch
+
+    from rsock_amd import codec as rc
+    from rsock_amd import workload
+
+    dev = torch.device("cuda:0")
+    n = args.packets or workload.CONFIGS[args.config][1]
+    d = workload.describe(args.config, 0, n, n=n)
+    w = workload.DeviceWorkload(d, dev)
+    cx = rc.Codec(b"hello135", 0)
+    cx.reserve(n)
+    s = torch.cuda.current_stream()
+    g = torch.Generator(device=dev)
+    g.manual_seed(1)
+    ri = lambda hi, dt: torch.randint(0, hi, (n,), device=dev, generator=g, dtype=torch.int64).to(dt)  # noqa: E731
+    src, dst, seq, ack = ri(2**31, torch.int32), ri(2**31, torch.int32), ri(2**31, torch.int32), ri(2**31, torch.int32)
+    sp, dp, ipid = ri(2**15, torch.int16) + 1, ri(2**15, torch.int16) + 1, ri(2**15, torch.int16)
+    flag = torch.full((n,), 0x18, dtype=torch.uint8, device=dev)
+    pmax = workload.CONFIGS[args.config][3]
+    p4, pe = workload.round16(40 + 31 + pmax), workload.round16(54 + 31 + pmax)
+    wire4 = torch.empty(n * p4, dtype=torch.uint8, device=dev)
+    wiree = torch.empty(n * pe, dtype=torch.uint8, device=dev)
+    off4 = torch.arange(n, device=dev, dtype=torch.int64) * p4
+    offe = torch.arange(n, device=dev, dtype=torch.int64) * pe
+    st4 = torch.empty(n, dtype=torch.int32, device=dev)
+    ste = torch.empty(n, dtype=torch.int32, device=dev)
+    eth = bytes([2, 0, 0, 0, 0, 1, 2, 0, 0, 0, 0, 2, 8, 0])
+    tcp = rc.TcpInfoBuffers.alloc(n, dev)
+    pdec = rc.DecodeBuffers.alloc(n, dev)
+    common = (w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key)
+    ops = {
+        "encode": lambda: cx.output_batch(*common, w.frame, w.frame_off, w.status, id_uniform=workload.ID_UNIFORM,
+                                          pad16=True, stream=s),
+        "encode_wire_raw4": lambda: cx.output_wire_batch(*common, src, dst, sp, dp, seq, ack, flag, ipid, wire4, off4,
+                                                         st4, id_uniform=workload.ID_UNIFORM, pad16=True, stream=s),
+        "encode_wire_eth": lambda: cx.output_wire_batch(*common, src, dst, sp, dp, seq, ack, flag, ipid, wiree, offe,
+                                                        ste, eth=eth, id_uniform=workload.ID_UNIFORM, pad16=True,
+                                                        stream=s),
+        "decode": lambda: cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, w.dec, stream=s),
+        "parse_decode": lambda: cx.rawinput_batch(wiree, offe, ste, ste, 1, 0, tcp, pdec, stream=s),
+    }
+    for f in ops.values():
+        f()
+    torch.cuda.synchronize()
+    assert bool((pdec.status == 1).all()) and int(pdec.n_valid.item()) == n
+    times = {k: [] for k in ops}
+    for _ in range(args.rounds):
+        for k, f in ops.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for _ in range(args.reps):
+                f()
+            e1.record(s)
+            torch.cuda.synchronize()
+            times[k].append(e0.elapsed_time(e1) / args.reps)
+    p = float(d.pay_len.astype(np.float64).mean())
+    alg = {  # algorithmic bytes per packet
+        "encode": 2 * p + 66,
+        "encode_wire_raw4": 2 * p + 66 + 40 + 23,
+        "encode_wire_eth": 2 * p + 66 + 54 + 23,
+        "decode": 73,
+        "parse_decode": 54 + 32 + 16 + 21 + 4 + 73 - 42,
+    }
+    out = {}
+    for k, t in times.items():
+        m = float(np.median(t))
+        out[k] = {"ms": round(m, 4), "Mpkt_s": round(n / m / 1e3, 1), "GBps_alg": round(n * alg[k] / m / 1e6, 1)}
+    print(json.dumps({"config": args.config, "packets": n, "paths": out}))
+
+
+if __name__ == "__main__":
+    main()
