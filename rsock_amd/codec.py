@@ -150,11 +150,19 @@ class Codec:
             pass
 
     def set_encode_variant(self, v: int) -> None:
-        """Internal tuning knob (not in the public header): 0 flat<4> (default), 1 per-packet,
-        2 flat<2>, 3 flat<8>.  Every variant is parity-tested; used for in-process A/B."""
+        """Internal tuning knob (not in the public header) selecting k_encode's copy path: 0 hybrid
+        (default), 1/4/5 per-packet PU=1/2/4, 2/3 flat U=2/4, 6-10 non-temporal and PU=2 variants
+        (list in rsk_kernels.hip).  Every variant is parity-tested; used for in-process A/B."""
         fn = lib().rsk__set_encode_variant
         fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
         _check(fn(self._ctx, v), "rsk__set_encode_variant")
+
+    def set_wire_variant(self, v: int) -> None:
+        """Internal tuning knob for k_encode_wire: 0 two-launch hybrid (default), 1 per-packet, 2 flat,
+        3 one-launch hybrid."""
+        fn = lib().rsk__set_wire_variant
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        _check(fn(self._ctx, v), "rsk__set_wire_variant")
 
     def reserve(self, n_max: int) -> None:
         _check(lib().rsk_reserve(self._ctx, n_max), "rsk_reserve")

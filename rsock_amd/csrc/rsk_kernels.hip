@@ -427,76 +427,90 @@ struct WireGeom {
     static constexpr int IPC = E + 10;                // IPv4 checksum byte offset
 };
 
-template <int E, int PU>
-__global__ __launch_bounds__(kBlock) void k_encode_wire(EncArgs a, WireArgs wa, KeySched ks) {
+// ---- phase 1 (one lane per packet): the wire prefix image PW = link header, IPv4 header (with its
+// checksum), TCP header (checksum 0), frame bytes [0, 31) and payload bytes [0, D0) (masked to P);
+// sum_pre = TCP checksum contribution of the pseudo-header and PW from the TCP header on; the
+// packet status becomes the wire length.
+template <int E>
+__device__ __forceinline__ void wire_phase1(const EncArgs &a, const WireArgs &wa, const Lane1 &L, uint64_t i,
+                                            uint32_t (&PW)[WireGeom<E>::NPW], uint32_t &sum_pre, int32_t &wst) {
     using G = WireGeom<E>;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t base = ((uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * 64u;
-    if (base >= a.n) return;
-    const uint64_t i = base + lane;
-    // ---- phase 1: frame words (encode_phase1 writes the frame status; patch it to the wire length)
-    Lane1 L = encode_phase1(a, ks, i);
-    uint32_t PW[G::NPW];
 #pragma unroll
     for (int q = 0; q < G::NPW; ++q) PW[q] = 0;
-    uint32_t sum_pre = 0;  // TCP checksum contribution of the prefix chunks (+ pseudo-header)
-    int32_t wst = L.st;
-    if (L.st > 0) {
-        const uint32_t flen = (uint32_t)L.st, P = flen - RSK_HEAD_SIZE;
-        const uint32_t wlen = G::HL + flen;
-        wst = (int32_t)wlen;
-        a.status[i] = wst;
-        const uint32_t src = wa.src[i], dst = wa.dst[i], sp = wa.sp[i], dp = wa.dp[i];
-        const uint32_t seq = wa.seq[i], ack = wa.ack[i], fl = wa.flag[i], id = wa.ip_id[i];
-        if constexpr (E > 0) {
+    sum_pre = 0;
+    wst = L.st;
+    if (L.st <= 0) return;
+    const uint32_t flen = (uint32_t)L.st, P = flen - RSK_HEAD_SIZE;
+    const uint32_t wlen = G::HL + flen;
+    wst = (int32_t)wlen;
+    a.status[i] = wst;
+    const uint32_t src = wa.src[i], dst = wa.dst[i], sp = wa.sp[i], dp = wa.dp[i];
+    const uint32_t seq = wa.seq[i], ack = wa.ack[i], fl = wa.flag[i], id = wa.ip_id[i];
+    if constexpr (E > 0) {
 #pragma unroll
-            for (int b = 0; b < E; b += 4) put_bytes(PW, b, wa.eth[b >> 2], E - b < 4 ? E - b : 4);
-        }
-        // IPv4 header (libnet_build_ipv4): 45 00 | len | id | 40 00 | 40 06 | csum | src | dst
-        const uint32_t tot = 40u + flen;
-        put_bytes(PW, E + 0, 0x45u | (rsk::bswap16(tot) << 16), 4);
-        put_bytes(PW, E + 4, rsk::bswap16(id) | (0x0040u << 16), 4);
-        put_bytes(PW, E + 8, 64u | (6u << 8), 2);
-        put_bytes(PW, E + 12, src, 4);
-        put_bytes(PW, E + 16, dst, 4);
-        const uint32_t ips = hsum(0x45u | (rsk::bswap16(tot) << 16)) + hsum(rsk::bswap16(id) | (0x0040u << 16)) +
-                             hsum(64u | (6u << 8)) + hsum(src) + hsum(dst);
-        put_bytes(PW, G::IPC, ~fold16(ips) & 0xffffu, 2);
-        // TCP header (libnet_build_tcp): sp dp seq ack | 50 flags | ffff | csum | 0000
-        const uint32_t t0 = rsk::bswap16(sp) | (rsk::bswap16(dp) << 16), t1 = rsk::bswap32(seq),
-                       t2 = rsk::bswap32(ack), t3 = 0x50u | (fl << 8) | (0xffffu << 16);
-        put_bytes(PW, E + 20, t0, 4);
-        put_bytes(PW, E + 24, t1, 4);
-        put_bytes(PW, E + 28, t2, 4);
-        put_bytes(PW, E + 32, t3, 4);
-        // frame bytes [0, 31) = tag + EncHead (H[7]'s top byte is payload[0], written below)
-#pragma unroll
-        for (int q = 0; q < 8; ++q) put_bytes(PW, G::HL + 4 * q, L.H[q], q == 7 ? 3 : 4);
-        // payload bytes [0, 16) (bounded by P; bytes past P stay zero)
-        const uint8_t *pay = a.payload + L.po;
-        uint32_t pw[4];
-        rsk::load_window<4>(pay, pay + P - 1, pw);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int k = (int)P - 4 * q;
-            pw[q] &= k >= 4 ? 0xffffffffu : (k <= 0 ? 0u : ((1u << (8 * k)) - 1u));
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int off = G::HB + 4 * q;
-            const int nb = (off + 4 <= 4 * G::NPW) ? 4 : 4 * G::NPW - off;
-            if (nb > 0) put_bytes(PW, off, pw[q], nb);
-        }
-        // pseudo-header (src, dst, 0, 6, tcp_len) + TCP header + prefix frame/payload bytes, from the
-        // TCP header start (even offset E + 20) to the end of the prefix chunks
-        uint32_t s = hsum(src) + hsum(dst) + (6u << 8) + rsk::bswap16(20u + flen);
-#pragma unroll
-        for (int q = (E + 20) / 4; q < G::NPW; ++q) s += ((E + 20) % 4 && q == (E + 20) / 4) ? (PW[q] >> 16) : hsum(PW[q]);
-        sum_pre = s;
+        for (int b = 0; b < E; b += 4) put_bytes(PW, b, wa.eth[b >> 2], E - b < 4 ? E - b : 4);
     }
-    // ---- copy: per packet, prefix chunks from the lane's image, payload chunks funnel-shifted
-    const bool vec = L.st > 0 && !L.slow;
-    uint64_t vm = __ballot(vec);
+    // IPv4 header (libnet_build_ipv4): 45 00 | len | id | 40 00 | 40 06 | csum | src | dst
+    const uint32_t tot = 40u + flen;
+    put_bytes(PW, E + 0, 0x45u | (rsk::bswap16(tot) << 16), 4);
+    put_bytes(PW, E + 4, rsk::bswap16(id) | (0x0040u << 16), 4);
+    put_bytes(PW, E + 8, 64u | (6u << 8), 2);
+    put_bytes(PW, E + 12, src, 4);
+    put_bytes(PW, E + 16, dst, 4);
+    const uint32_t ips = hsum(0x45u | (rsk::bswap16(tot) << 16)) + hsum(rsk::bswap16(id) | (0x0040u << 16)) +
+                         hsum(64u | (6u << 8)) + hsum(src) + hsum(dst);
+    put_bytes(PW, G::IPC, ~fold16(ips) & 0xffffu, 2);
+    // TCP header (libnet_build_tcp): sp dp seq ack | 50 flags | ffff | csum | 0000
+    const uint32_t t0 = rsk::bswap16(sp) | (rsk::bswap16(dp) << 16), t1 = rsk::bswap32(seq),
+                   t2 = rsk::bswap32(ack), t3 = 0x50u | (fl << 8) | (0xffffu << 16);
+    put_bytes(PW, E + 20, t0, 4);
+    put_bytes(PW, E + 24, t1, 4);
+    put_bytes(PW, E + 28, t2, 4);
+    put_bytes(PW, E + 32, t3, 4);
+    // frame bytes [0, 31) = tag + EncHead (H[7]'s top byte is payload[0], written below)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) put_bytes(PW, G::HL + 4 * q, L.H[q], q == 7 ? 3 : 4);
+    // payload bytes [0, 16) (bounded by P; bytes past P stay zero)
+    const uint8_t *pay = a.payload + L.po;
+    uint32_t pw[4];
+    rsk::load_window<4>(pay, pay + P - 1, pw);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int k = (int)P - 4 * q;
+        pw[q] &= k >= 4 ? 0xffffffffu : (k <= 0 ? 0u : ((1u << (8 * k)) - 1u));
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int off = G::HB + 4 * q;
+        const int nb = (off + 4 <= 4 * G::NPW) ? 4 : 4 * G::NPW - off;
+        if (nb > 0) put_bytes(PW, off, pw[q], nb);
+    }
+    // pseudo-header (src, dst, 0, 6, tcp_len) + TCP header + prefix frame/payload bytes, from the
+    // TCP header start (even offset E + 20) to the end of the prefix chunks
+    uint32_t s = hsum(src) + hsum(dst) + (6u << 8) + rsk::bswap16(20u + flen);
+#pragma unroll
+    for (int q = (E + 20) / 4; q < G::NPW; ++q) s += ((E + 20) % 4 && q == (E + 20) / 4) ? (PW[q] >> 16) : hsum(PW[q]);
+    sum_pre = s;
+}
+
+// Wave-wide sum of v (each lane's value < 2^26): DPP row_shr 1/2/4/8 inclusive scans within each
+// 16-lane row (bound_ctrl: lanes shifted in from outside the row read 0), then the four row totals.
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);
+    return rdl(v, 15) + rdl(v, 31) + rdl(v, 47) + rdl(v, 63);
+}
+
+// ---- per-packet copy, PU packets per iteration: lane l takes payload chunks NPRE + l and
+// NPRE + 64 + l (a packet has at most 88 past the prefix); the halfword sums of those chunks are
+// reduced over the wave into the TCP checksum, which lane CK/16 patches into its prefix chunk (read
+// from the wave's LDS stage of the 64 lanes' prefix images) before the stores.
+template <int E, int PU>
+__device__ __forceinline__ void copy_wire_pkt(const EncArgs &a, const Lane1 &L, const uint32_t *stage,
+                                              uint32_t sum_pre, int32_t wst, uint32_t lane, uint64_t vm) {
+    using G = WireGeom<E>;
     while (vm) {
         uint32_t js[PU];
         bool on[PU];
@@ -507,8 +521,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_wire(EncArgs a, WireArgs wa, 
             if (on[p]) vm &= vm - 1ull;
         }
         uint4 v[PU][2];
-        uint32_t part[PU];
-        uint32_t wlen[PU];
+        uint32_t ck[PU], wlen[PU];
         uint8_t *dstp[PU];
 #pragma unroll
         for (int p = 0; p < PU; ++p) {
@@ -520,61 +533,153 @@ __global__ __launch_bounds__(kBlock) void k_encode_wire(EncArgs a, WireArgs wa, 
             const uint8_t *src_al = pay + G::D0 - sh;
             const int32_t last_rel = (int32_t)P - 1 - G::D0 + (int32_t)sh;
             const uint32_t nch = (wlen[p] + 15u) >> 4;
-            part[p] = 0;
+            uint32_t part = 0;
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
-                const uint32_t k = lane + 64u * q;
+                const uint32_t k = G::NPRE + lane + 64u * q;
                 uint4 A = make_uint4(0u, 0u, 0u, 0u), B = make_uint4(0u, 0u, 0u, 0u);
-                if (k >= (uint32_t)G::NPRE && k < nch) {
+                if (k < nch) {
                     const uint32_t ro = 16u * (k - G::NPRE);
                     A = ld16<0>(src_al + ro);
                     if (sh != 0u && (int32_t)(ro + 16u) <= last_rel) B = ld16<0>(src_al + ro + 16u);
                 }
                 v[p][q] = rsk::funnel16(A, B, sh);
                 const int lim = (int)wlen[p] - 16 * (int)k;
-                if (k >= (uint32_t)G::NPRE && k < nch) {
+                if (k < nch) {
                     if (lim < 16) v[p][q] = rsk::keep_bytes16(v[p][q], lim);
-                    part[p] += hsum(v[p][q].x) + hsum(v[p][q].y) + hsum(v[p][q].z) + hsum(v[p][q].w);
+                    part += hsum(v[p][q].x) + hsum(v[p][q].y) + hsum(v[p][q].z) + hsum(v[p][q].w);
                 }
             }
+            ck[p] = part;
         }
-        // per-packet wave reduction of the payload-chunk sums -> TCP checksum
 #pragma unroll
-        for (int p = 0; p < PU; ++p) {
-            uint32_t t = fold16(part[p]);
-#pragma unroll
-            for (int off = 32; off; off >>= 1) t += __shfl_xor(t, off);
-            t += rdl(sum_pre, js[p]);
-            part[p] = ~fold16(t) & 0xffffu;  // now the checksum, uniform
-        }
+        for (int p = 0; p < PU; ++p) ck[p] = ~fold16(wave_sum(ck[p]) + rdl(sum_pre, js[p])) & 0xffffu;
 #pragma unroll
         for (int p = 0; p < PU; ++p) {
             if (!on[p]) continue;
             const uint32_t nst = (padded_len(dstp[p], wlen[p], a.pad) + 15u) >> 4;
+            if (lane < (uint32_t)G::NPRE && lane < nst) {
+                const uint4 sv = *reinterpret_cast<const uint4 *>(stage + js[p] * G::NPW + 4u * lane);
+                uint32_t w4[4] = {sv.x, sv.y, sv.z, sv.w};
+                if (lane == (uint32_t)(G::CK / 16)) w4[(G::CK & 15) >> 2] |= ck[p] << (8 * (G::CK & 3));
+                store_last16<0>(dstp[p] + 16u * lane, make_uint4(w4[0], w4[1], w4[2], w4[3]),
+                                (int)wlen[p] - 16 * (int)lane, a.pad != 0u);
+            }
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
-                const uint32_t k = lane + 64u * q;
-                if (k >= nst) continue;
-                uint4 val = v[p][q];
-                if (k < (uint32_t)G::NPRE) {
-                    uint32_t Wj[G::NPW];
-#pragma unroll
-                    for (int t = 0; t < G::NPW; ++t) Wj[t] = rdl(PW[t], js[p]);
-                    uint32_t w4[4] = {0, 0, 0, 0};
-#pragma unroll
-                    for (int c = 0; c < G::NPRE; ++c)
-                        if (k == (uint32_t)c) {
-                            w4[0] = Wj[4 * c]; w4[1] = Wj[4 * c + 1]; w4[2] = Wj[4 * c + 2]; w4[3] = Wj[4 * c + 3];
-                        }
-                    if (k == (uint32_t)(G::CK / 16)) w4[(G::CK & 15) >> 2] |= part[p] << (8 * (G::CK & 3));
-                    val = make_uint4(w4[0], w4[1], w4[2], w4[3]);
-                }
-                store_last16<0>(dstp[p] + 16u * k, val, (int)wlen[p] - 16 * (int)k, a.pad != 0u);
+                const uint32_t k = G::NPRE + lane + 64u * q;
+                if (k < nst) store_last16<0>(dstp[p] + 16u * k, v[p][q], (int)wlen[p] - 16 * (int)k, a.pad != 0u);
             }
         }
     }
-    // wire packets that are not 16-B aligned: byte path (prefix bytes from the lane image)
-    uint64_t sm = __ballot(L.st > 0 && L.slow);
+}
+
+// ---- flat copy for short packets, two passes over the set: (1) the payload chunks of all packets as
+// one flat chunk list (as copy_flat), each lane adding its chunk's halfword sum into the packet's
+// LDS slot; (2) the NPRE prefix chunks of every packet as a dense (packet, chunk) grid read from the
+// LDS stage, the TCP checksum patched into chunk CK/16 — both passes store coalesced runs.
+template <int E, int U>
+__device__ __forceinline__ void copy_wire_flat(const EncArgs &a, const Lane1 &L, const uint32_t *stage,
+                                               uint32_t sum_pre, int32_t wst, uint32_t lane, bool mine,
+                                               CopyRec *recs, uint32_t *cend, uint32_t *psum) {
+    using G = WireGeom<E>;
+    uint32_t cc = 0;
+    CopyRec r;
+    r.src_al = nullptr; r.dst = nullptr; r.cstart = 0; r.sh = 0; r.last_rel = 0; r.flen = 0;
+    if (mine) {
+        uint8_t *dst = a.frame + L.fo;
+        const uint32_t wlen = (uint32_t)wst;
+        const uint32_t nst = (padded_len(dst, wlen, a.pad) + 15u) >> 4;
+        cc = nst > (uint32_t)G::NPRE ? nst - G::NPRE : 0u;
+        const uint8_t *pay = a.payload + L.po;
+        const uint32_t sh = (uint32_t)((reinterpret_cast<uintptr_t>(pay) + G::D0) & 15u);
+        r.src_al = pay + G::D0 - sh;
+        r.dst = dst;
+        r.sh = sh;
+        r.last_rel = (int32_t)(wlen - G::HB) - 1 - G::D0 + (int32_t)sh;
+        r.flen = wlen;
+    }
+    uint32_t inc = cc;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t v = __shfl_up(inc, off);
+        if (lane >= (uint32_t)off) inc += v;
+    }
+    r.cstart = inc - cc;
+    recs[lane] = r;
+    cend[lane] = inc;
+    psum[lane] = sum_pre;
+    const uint32_t C = (uint32_t)__shfl((int)inc, 63);
+    wave_lds_sync();
+    for (uint32_t g0 = 0; g0 < C; g0 += 64u * U) {
+        uint4 A[U], B[U];
+        uint8_t *dsts[U];
+        uint32_t shs[U], pk[U];
+        int32_t lims[U];
+        bool act[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t g = g0 + 64u * u + lane;
+            act[u] = g < C;
+            A[u] = make_uint4(0u, 0u, 0u, 0u);
+            B[u] = make_uint4(0u, 0u, 0u, 0u);
+            shs[u] = 0;
+            lims[u] = 0;
+            dsts[u] = nullptr;
+            pk[u] = 0;
+            if (act[u]) {
+                uint32_t lo = 0;
+#pragma unroll
+                for (uint32_t st = 32; st; st >>= 1)
+                    if (cend[lo + st - 1] <= g) lo += st;
+                const CopyRec rr = recs[lo];
+                const uint32_t ro = 16u * (g - rr.cstart);
+                lims[u] = (int32_t)rr.flen - 16 * G::NPRE - (int32_t)ro;
+                if (lims[u] > 0) {  // chunk holds packet bytes (else pure pad)
+                    A[u] = ld16<0>(rr.src_al + ro);
+                    if (rr.sh != 0u && (int32_t)(ro + 16u) <= rr.last_rel) B[u] = ld16<0>(rr.src_al + ro + 16);
+                }
+                shs[u] = rr.sh;
+                dsts[u] = rr.dst + 16 * G::NPRE + ro;
+                pk[u] = lo;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!act[u]) continue;
+            uint4 v = funnel16_lane(A[u], B[u], shs[u]);
+            if (lims[u] < 16) v = lims[u] > 0 ? rsk::keep_bytes16(v, lims[u]) : make_uint4(0u, 0u, 0u, 0u);
+            const uint32_t s = hsum(v.x) + hsum(v.y) + hsum(v.z) + hsum(v.w);
+            if (s) atomicAdd(&psum[pk[u]], s);
+            store_last16<0>(dsts[u], v, lims[u], a.pad != 0u);
+        }
+    }
+    wave_lds_sync();
+    // pass 2: prefix chunk (j, c) for g = NPRE * j + c
+#pragma unroll
+    for (int t = 0; t < G::NPRE; ++t) {
+        const uint32_t g = 64u * t + lane;
+        const uint32_t j = g / G::NPRE, c = g - j * G::NPRE;
+        const CopyRec rr = recs[j];
+        if (rr.dst == nullptr) continue;  // not a vector-path packet
+        const uint32_t nstj = (padded_len(rr.dst, rr.flen, a.pad) + 15u) >> 4;
+        if (c >= nstj) continue;
+        const uint4 sv = *reinterpret_cast<const uint4 *>(stage + j * G::NPW + 4u * c);
+        uint32_t w4[4] = {sv.x, sv.y, sv.z, sv.w};
+        if (c == (uint32_t)(G::CK / 16)) {
+            const uint32_t ck = ~fold16(psum[j]) & 0xffffu;
+            w4[(G::CK & 15) >> 2] |= ck << (8 * (G::CK & 3));
+        }
+        store_last16<0>(rr.dst + 16u * c, make_uint4(w4[0], w4[1], w4[2], w4[3]), (int)rr.flen - 16 * (int)c,
+                        a.pad != 0u);
+    }
+}
+
+// ---- wire packets that are not 16-B aligned: byte path (prefix bytes from the lane image)
+template <int E>
+__device__ __forceinline__ void copy_wire_bytes(const EncArgs &a, const Lane1 &L, const uint32_t *stage,
+                                                uint32_t sum_pre, int32_t wst, uint32_t lane, uint64_t sm) {
+    using G = WireGeom<E>;
     while (sm) {
         const uint32_t j = (uint32_t)__builtin_ctzll(sm);
         sm &= sm - 1ull;
@@ -583,7 +688,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_wire(EncArgs a, WireArgs wa, 
         uint8_t *dst = a.frame + rdl64(L.fo, j);
         uint32_t Wj[G::NPW];
 #pragma unroll
-        for (int t = 0; t < G::NPW; ++t) Wj[t] = rdl(PW[t], j);
+        for (int t = 0; t < G::NPW; ++t) Wj[t] = stage[j * G::NPW + t];  // uniform LDS reads
         // checksum: prefix part from the packet lane, payload bytes past the prefix summed here
         uint32_t s = 0;
         for (uint32_t f = 16u * G::NPRE + lane; f < wl; f += 64u) {
@@ -612,6 +717,80 @@ __global__ __launch_bounds__(kBlock) void k_encode_wire(EncArgs a, WireArgs wa, 
             }
             rsk::gptr(dst)[f] = (uint8_t)byte;
         }
+    }
+}
+
+// MODE: 0 per-packet, 1 flat, 2 hybrid (per-wave choice on the set's mean wire length, one launch),
+// 3 / 4 = the per-packet / flat halves of the two-launch hybrid: each wave re-derives the same
+// choice from pay_len and frame_off alone and returns unless it is its launch's path, so every set
+// is handled exactly once and each launch sizes LDS (hence occupancy) for its own path only.
+template <int E, int MODE>
+struct WireLds {
+    static constexpr int kStage = 64 * WireGeom<E>::NPW * 4;  // prefix images (both paths)
+    static constexpr bool kFlat = MODE == 1 || MODE == 2 || MODE == 4;
+    static constexpr int kBytes = kStage + (kFlat ? 64 * (int)sizeof(CopyRec) + 2 * 64 * 4 : 0);
+};
+
+// Per-wave copy-path choice (identical in both launches of the split hybrid).
+template <int E>
+__device__ __forceinline__ bool wire_flat_choice(bool vec, uint32_t wlen) {
+    uint32_t fl = vec ? wlen : 0u;
+#pragma unroll
+    for (int off = 32; off; off >>= 1) fl += __shfl_xor(fl, off);
+    return fl < kFlatBelowMeanBytes * (uint32_t)__popcll(__ballot(vec));
+}
+
+template <int E, int MODE, int PU, int U>
+__global__ __launch_bounds__(kBlock) void k_encode_wire(EncArgs a, WireArgs wa, KeySched ks) {
+    using G = WireGeom<E>;
+    __shared__ uint4 lds[kWavesPerBlock][WireLds<E, MODE>::kBytes / 16];
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint64_t base = ((uint64_t)blockIdx.x * kWavesPerBlock + w) * 64u;
+    if (base >= a.n) return;  // wave-uniform; no block barriers below
+    const uint64_t i = base + lane;
+    if constexpr (MODE >= 3) {  // split hybrid: is this set ours?
+        bool v0 = false;
+        uint32_t wl = 0;
+        if (i < a.n) {
+            const uint32_t P = a.pay_len[i];
+            v0 = P != 0u && P <= (uint32_t)RSK_MAX_PAYLOAD &&
+                 ((reinterpret_cast<uintptr_t>(a.frame + a.frame_off[i]) & 15u) == 0);
+            wl = G::HL + RSK_HEAD_SIZE + P;
+        }
+        if (wire_flat_choice<E>(v0, wl) != (MODE == 4)) return;
+    }
+    const Lane1 L = encode_phase1(a, ks, i);
+    uint32_t PW[G::NPW];
+    uint32_t sum_pre;
+    int32_t wst;
+    wire_phase1<E>(a, wa, L, i, PW, sum_pre, wst);
+    const bool vec = L.st > 0 && !L.slow;
+    const uint64_t vm = __ballot(vec);
+    bool flat = MODE == 1 || MODE == 4;
+    if constexpr (MODE == 2) flat = wire_flat_choice<E>(vec, (uint32_t)wst);
+    uint8_t *slice = reinterpret_cast<uint8_t *>(lds[w]);
+    uint32_t *stage = reinterpret_cast<uint32_t *>(slice);
+    if (L.st > 0) {  // every framed packet's prefix image (vector and byte paths read it from here)
+#pragma unroll
+        for (int c = 0; c < G::NPRE; ++c)
+            *reinterpret_cast<uint4 *>(stage + lane * G::NPW + 4 * c) =
+                make_uint4(PW[4 * c], PW[4 * c + 1], PW[4 * c + 2], PW[4 * c + 3]);
+    }
+    if constexpr (WireLds<E, MODE>::kFlat) {
+        if (flat) {
+            CopyRec *recs = reinterpret_cast<CopyRec *>(slice + WireLds<E, MODE>::kStage);
+            uint32_t *cend = reinterpret_cast<uint32_t *>(slice + WireLds<E, MODE>::kStage + 64 * sizeof(CopyRec));
+            copy_wire_flat<E, U>(a, L, stage, sum_pre, wst, lane, vec, recs, cend, cend + 64);
+        }
+    }
+    if (!flat) {
+        wave_lds_sync();
+        copy_wire_pkt<E, PU>(a, L, stage, sum_pre, wst, lane, vm);
+    }
+    const uint64_t sm = __ballot(L.st > 0 && L.slow);
+    if (sm) {
+        wave_lds_sync();
+        copy_wire_bytes<E>(a, L, stage, sum_pre, wst, lane, sm);
     }
 }
 
@@ -1073,6 +1252,7 @@ inline unsigned grid_for(uint64_t threads) { return (unsigned)((threads + kBlock
 struct rsk_ctx {
     int device = 0;
     int enc_variant = 0;  // see rsk__set_encode_variant
+    int wire_variant = 0;  // see rsk__set_wire_variant
     std::vector<uint8_t> key;
     KeySched ks;
     // compaction workspace
@@ -1168,6 +1348,14 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
     if (!c || v < 0 || v > 10) return RSK_EINVAL;
     c->enc_variant = v;
+    return RSK_OK;
+}
+
+// Internal (A/B and tests): wire-build copy path.  0 = two-launch hybrid (default), 1 = per-packet,
+// 2 = flat, 3 = one-launch hybrid.
+int rsk__set_wire_variant(rsk_ctx *c, int v) {
+    if (!c || v < 0 || v > 3) return RSK_EINVAL;
+    c->wire_variant = v;
     return RSK_OK;
 }
 
@@ -1272,10 +1460,21 @@ int rsk_encode_wire_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const
     std::memcpy(w.eth, eth, 16);
     const uint64_t waves = (n + 63ull) / 64ull;
     const unsigned grid = (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
-    if (wire->with_eth)
-        hipLaunchKernelGGL((k_encode_wire<14, 2>), dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, a, w, c->ks);
-    else
-        hipLaunchKernelGGL((k_encode_wire<0, 2>), dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, a, w, c->ks);
+    const hipStream_t st = (hipStream_t)stream;
+#define RSK_WIRE(E, M, PU, U) hipLaunchKernelGGL((k_encode_wire<E, M, PU, U>), dim3(grid), dim3(kBlock), 0, st, a, w, c->ks)
+    const int v = c->wire_variant;
+    if (wire->with_eth) {
+        if (v == 1) RSK_WIRE(14, 0, 2, 4);
+        else if (v == 2) RSK_WIRE(14, 1, 2, 2);
+        else if (v == 3) RSK_WIRE(14, 2, 2, 2);
+        else { RSK_WIRE(14, 3, 2, 2); RSK_WIRE(14, 4, 2, 2); }
+    } else {
+        if (v == 1) RSK_WIRE(0, 0, 2, 4);
+        else if (v == 2) RSK_WIRE(0, 1, 2, 2);
+        else if (v == 3) RSK_WIRE(0, 2, 2, 2);
+        else { RSK_WIRE(0, 3, 2, 2); RSK_WIRE(0, 4, 2, 2); }
+    }
+#undef RSK_WIRE
     return launch_check("k_encode_wire");
 }
 

@@ -19,12 +19,16 @@ KEY = b"hello135"
 @pytest.mark.parametrize("eth", [False, True])
 @pytest.mark.parametrize("layout", ["aligned", "odd_payload", "odd_wire"])
 @pytest.mark.parametrize("pad16", [False, True])
-def test_wire_batch(codec, gpu, oracle, eth, layout, pad16):
+@pytest.mark.parametrize("mix", ["mixed", "short", "bimodal"])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])  # split hybrid / per-packet / flat / 1-launch hybrid
+def test_wire_batch(codec, gpu, oracle, eth, layout, pad16, mix, variant):
     import torch
 
-    rng = np.random.default_rng(hash((eth, layout, pad16)) & 0xFFFF)
+    rng = np.random.default_rng(hash((eth, layout, pad16, mix)) & 0xFFFF)
     lens = [0, 1, 2, 8, 9, 10, 11, 12, 15, 16, 17, 31, 32, 33, 100, 1000, 1400, 1468, 1469, 1470] + \
-        list(rng.integers(1, 1470, 400))
+        list(rng.integers(1, 1470 if mix == "mixed" else 160, 400))
+    if mix == "bimodal":  # short sets then long sets: both launches of the split hybrid in one batch
+        lens = lens[:20] + list(rng.integers(1, 160, 236)) + list(rng.integers(1000, 1470, 200))
     n = len(lens)
     plen = np.array(lens, np.uint16)
     pitch_p = 1504
@@ -47,12 +51,14 @@ def test_wire_batch(codec, gpu, oracle, eth, layout, pad16):
     fill = rng.integers(0, 256, n * pitch_w + 64, dtype=np.uint8)
     wire = dev(fill, gpu)
     status = torch.empty(n, dtype=torch.int32, device=gpu)
+    codec.set_wire_variant(variant)
     codec.output_wire_batch(dev(payload, gpu), dev(pay_off, gpu, np.int64), dev(plen, gpu, np.int16), dev(cmd, gpu),
                             dev(conv, gpu, np.int32), dev(ckey, gpu, np.int64), dev(src, gpu, np.int32),
                             dev(dst, gpu, np.int32), dev(sp, gpu, np.int16), dev(dp, gpu, np.int16),
                             dev(seq, gpu, np.int32), dev(ack, gpu, np.int32), dev(flag, gpu), dev(ipid, gpu, np.int16),
                             wire, dev(wire_off, gpu, np.int64), status, eth=ethb, id_uniform=workload.ID_UNIFORM,
                             pad16=pad16)
+    codec.set_wire_variant(0)
     torch.cuda.synchronize()
     got, st = wire.cpu().numpy(), status.cpu().numpy()
     exp = fill.copy()

@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--packets", type=int, default=0)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--wire-align", type=int, default=16, help="wire packet pitch alignment (bytes)")
     args = ap.parse_args()
     import torch
 
@@ -39,7 +40,8 @@ def main():
     sp, dp, ipid = ri(2**15, torch.int16) + 1, ri(2**15, torch.int16) + 1, ri(2**15, torch.int16)
     flag = torch.full((n,), 0x18, dtype=torch.uint8, device=dev)
     pmax = workload.CONFIGS[args.config][3]
-    p4, pe = workload.round16(40 + 31 + pmax), workload.round16(54 + 31 + pmax)
+    al = args.wire_align
+    p4, pe = (40 + 31 + pmax + al - 1) // al * al, (54 + 31 + pmax + al - 1) // al * al
     wire4 = torch.empty(n * p4, dtype=torch.uint8, device=dev)
     wiree = torch.empty(n * pe, dtype=torch.uint8, device=dev)
     off4 = torch.arange(n, device=dev, dtype=torch.int64) * p4
@@ -58,6 +60,15 @@ def main():
         "encode_wire_eth": lambda: cx.output_wire_batch(*common, src, dst, sp, dp, seq, ack, flag, ipid, wiree, offe,
                                                         ste, eth=eth, id_uniform=workload.ID_UNIFORM, pad16=True,
                                                         stream=s),
+        "encode_wire_raw4_pkt": lambda: (cx.set_wire_variant(1), cx.output_wire_batch(
+            *common, src, dst, sp, dp, seq, ack, flag, ipid, wire4, off4, st4, id_uniform=workload.ID_UNIFORM,
+            pad16=True, stream=s), cx.set_wire_variant(0)),
+        "encode_wire_raw4_flat": lambda: (cx.set_wire_variant(2), cx.output_wire_batch(
+            *common, src, dst, sp, dp, seq, ack, flag, ipid, wire4, off4, st4, id_uniform=workload.ID_UNIFORM,
+            pad16=True, stream=s), cx.set_wire_variant(0)),
+        "encode_wire_raw4_hyb1": lambda: (cx.set_wire_variant(3), cx.output_wire_batch(
+            *common, src, dst, sp, dp, seq, ack, flag, ipid, wire4, off4, st4, id_uniform=workload.ID_UNIFORM,
+            pad16=True, stream=s), cx.set_wire_variant(0)),
         "decode": lambda: cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, w.dec, stream=s),
         "parse_decode": lambda: cx.rawinput_batch(wiree, offe, ste, ste, 1, 0, tcp, pdec, stream=s),
     }
@@ -80,6 +91,9 @@ def main():
         "encode": 2 * p + 66,
         "encode_wire_raw4": 2 * p + 66 + 40 + 23,
         "encode_wire_eth": 2 * p + 66 + 54 + 23,
+        "encode_wire_raw4_pkt": 2 * p + 66 + 40 + 23,
+        "encode_wire_raw4_flat": 2 * p + 66 + 40 + 23,
+        "encode_wire_raw4_hyb1": 2 * p + 66 + 40 + 23,
         "decode": 73,
         "parse_decode": 54 + 32 + 16 + 21 + 4 + 73 - 42,
     }
@@ -87,7 +101,7 @@ def main():
     for k, t in times.items():
         m = float(np.median(t))
         out[k] = {"ms": round(m, 4), "Mpkt_s": round(n / m / 1e3, 1), "GBps_alg": round(n * alg[k] / m / 1e6, 1)}
-    print(json.dumps({"config": args.config, "packets": n, "paths": out}))
+    print(json.dumps({"config": args.config, "packets": n, "wire_pitch": [p4, pe], "paths": out}))
 
 
 if __name__ == "__main__":
