@@ -19,6 +19,11 @@
  *   rsk_tcpinfo_encode_batch <- char* TcpInfo::Encode(char*, int) (21-B hand-off record)      bean/TcpInfo.cpp:20-32, bean/ConnInfo.cpp:12-20
  *   rsk_encode_wire_batch <- RConn::Output + RawTcp::SendRawTcp -> libnet_build_tcp/ipv4     conn/RawTcp.cpp:280-341
  *   rsk_key_for_tcp/udp   <- KeyGenerator::KeyForTcp / KeyForUdp                              src/util/KeyGenerator.cpp:16-36
+ *   rsk_demux_batch       <- the per-packet conn lookups of the receive path, batched:
+ *                            INetGroup::Input by connKey (conn/INetGroup.cpp:57-83), IAppGroup::Input
+ *                            by cmd (conn/IAppGroup.cpp:76-96), ServerGroup::OnRecv by IdBuf
+ *                            (server/ServerGroup.cpp:44-60), SubGroup::OnRecv by (dst, conv)
+ *                            (server/SubGroup.cpp:31-50), ClientGroup::OnRecv by conv (client/ClientGroup.cpp:66-80)
  */
 #ifndef RSK_CODEC_H
 #define RSK_CODEC_H
@@ -215,6 +220,40 @@ int rsk_parse_decode_batch(rsk_ctx *ctx, uint32_t n, const uint8_t *cap_arena, c
 int rsk_tcpinfo_encode_batch(rsk_ctx *ctx, uint32_t n, const uint32_t *src, const uint32_t *dst,
                              const uint16_t *sp, const uint16_t *dp, const uint32_t *seq,
                              const uint32_t *ack, const uint8_t *flag, uint8_t *rec, void *stream);
+
+/* ---- receive demux: stable group-by of the VALID packets on decoded fields --- */
+/* The reference routes every VALID packet on its own: a map lookup per packet on the fields below,
+ * packets delivered in arrival order.  rsk_demux_batch groups a decoded batch so the host does one
+ * lookup per segment and hands each conn its packets as one run:
+ *   - the key is the tuple of the fields selected in `fields` (unselected fields are ignored);
+ *   - with RSK_DEMUX_CMD_BARRIER, a packet whose cmd != RSK_CMD_DATA (RST / keepalive, handled by
+ *     IAppGroup outside the conn maps) is a segment of its own and an ordering barrier: DATA
+ *     packets on either side of it never share a segment;
+ *   - segments are ordered by their first packet, packets inside a segment by arrival.
+ * Delivering segment by segment therefore hands every conn the same packet sequence as the
+ * reference's per-packet loop, and creates new conns in the same order (first occurrence). */
+#define RSK_DEMUX_ID          0x01u /* EncHead IdBuf (8 B)                                        */
+#define RSK_DEMUX_CONN_KEY    0x02u /* EncHead connKey                                            */
+#define RSK_DEMUX_CONV        0x04u /* EncHead conv                                               */
+#define RSK_DEMUX_DST         0x08u /* TcpInfo dst (SubGroup keys on BuildConvKey(dst, conv))     */
+#define RSK_DEMUX_CMD_BARRIER 0x10u
+typedef struct rsk_demux_in {
+    const int8_t *status;      /* [n] packet i takes part iff status[i] == RSK_RECV_VALID       */
+    const uint8_t *cmd;        /* [n]                                                           */
+    const uint8_t *id;         /* [n*8] (8-B aligned); may be NULL unless RSK_DEMUX_ID           */
+    const uint32_t *conv;      /* [n]; may be NULL unless RSK_DEMUX_CONV                         */
+    const uint64_t *conn_key;  /* [n]; may be NULL unless RSK_DEMUX_CONN_KEY                     */
+    const uint32_t *dst;       /* [n]; may be NULL unless RSK_DEMUX_DST                          */
+} rsk_demux_in;
+typedef struct rsk_demux_out {
+    uint32_t *perm;      /* [n] packet indices, segment by segment (first n_valid entries used)   */
+    uint32_t *seg_off;   /* [n+1] segment s = perm[seg_off[s] .. seg_off[s+1]) (first n_seg+1)   */
+    uint32_t *seg_first; /* [n] first packet of segment s (its key representative), increasing    */
+    uint32_t *n_seg;     /* [1]                                                                   */
+    uint32_t *n_valid;   /* [1]                                                                   */
+} rsk_demux_out;
+int rsk_demux_batch(rsk_ctx *ctx, uint32_t n, const rsk_demux_in *in, uint32_t fields,
+                    const rsk_demux_out *out, void *stream);
 
 /* ---- single-packet shims with the reference signatures (host pointers) ----------------------- */
 /* These run the same HIP kernels on a batch of one (device round trip, synchronous), so a caller

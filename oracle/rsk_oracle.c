@@ -555,3 +555,84 @@ void orc_parse_decode_batch(const uint8_t *key, size_t key_len, uint32_t n, cons
     }
     if (n_valid) *n_valid = nv;
 }
+
+/* ---- receive demux ------------------------------------------------------------ */
+typedef struct orc_dkey {
+    uint32_t epoch, conv, dst, used;
+    uint64_t id, key;
+    uint32_t seg;
+} orc_dkey;
+
+static uint64_t orc_dkey_hash(const orc_dkey *k) {
+    uint64_t h = k->epoch * 0x9E3779B97F4A7C15ull ^ k->id * 0xC2B2AE3D27D4EB4Full ^
+                 k->key * 0x165667B19E3779F9ull ^ ((uint64_t)k->conv | (uint64_t)k->dst << 32) * 0xD6E8FEB86659FD93ull;
+    h ^= h >> 31;
+    h *= 0xBF58476D1CE4E5B9ull;
+    h ^= h >> 29;
+    return h;
+}
+
+int orc_demux_batch(uint32_t n, const int8_t *status, const uint8_t *cmd, const uint8_t *id,
+                    const uint32_t *conv, const uint64_t *conn_key, const uint32_t *dst,
+                    uint32_t fields, uint32_t *perm, uint32_t *seg_off, uint32_t *seg_first,
+                    uint32_t *n_seg, uint32_t *n_valid) {
+    uint64_t cap = 2;
+    while (cap < 2ull * n) cap <<= 1;
+    orc_dkey *tab = (orc_dkey *)calloc(cap, sizeof(orc_dkey));
+    uint32_t *seg_of = (uint32_t *)malloc((n ? n : 1) * sizeof(uint32_t));
+    uint32_t *cnt = (uint32_t *)calloc(n + 1, sizeof(uint32_t));
+    if (!tab || !seg_of || !cnt) {
+        free(tab); free(seg_of); free(cnt);
+        return -12;
+    }
+    const int barrier = (fields & RSK_DEMUX_CMD_BARRIER) != 0;
+    uint32_t epoch = 0, S = 0, nv = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        if (status[i] != RSK_RECV_VALID) continue;
+        nv++;
+        if (barrier && cmd[i] != RSK_CMD_DATA) {  /* singleton segment, then a new epoch */
+            seg_first[S] = i;
+            seg_of[i] = S++;
+            epoch++;
+            continue;
+        }
+        orc_dkey k;
+        memset(&k, 0, sizeof k);
+        k.epoch = epoch;
+        if (fields & RSK_DEMUX_ID) memcpy(&k.id, id + 8ull * i, 8);
+        if (fields & RSK_DEMUX_CONN_KEY) k.key = conn_key[i];
+        if (fields & RSK_DEMUX_CONV) k.conv = conv[i];
+        if (fields & RSK_DEMUX_DST) k.dst = dst[i];
+        uint64_t h = orc_dkey_hash(&k) & (cap - 1);
+        for (;;) {
+            orc_dkey *t = &tab[h];
+            if (!t->used) {  /* first occurrence: the reference would create the conn here */
+                *t = k;
+                t->used = 1;
+                t->seg = S;
+                seg_first[S] = i;
+                S++;
+                break;
+            }
+            if (t->epoch == k.epoch && t->id == k.id && t->key == k.key && t->conv == k.conv && t->dst == k.dst)
+                break;
+            h = (h + 1) & (cap - 1);
+        }
+        seg_of[i] = tab[h].seg;
+    }
+    for (uint32_t i = 0; i < n; i++)
+        if (status[i] == RSK_RECV_VALID) cnt[seg_of[i]]++;
+    uint32_t run = 0;
+    for (uint32_t s = 0; s < S; s++) {
+        seg_off[s] = run;
+        run += cnt[s];
+        cnt[s] = seg_off[s];
+    }
+    seg_off[S] = run;
+    for (uint32_t i = 0; i < n; i++)
+        if (status[i] == RSK_RECV_VALID) perm[cnt[seg_of[i]]++] = i;
+    *n_seg = S;
+    *n_valid = nv;
+    free(tab); free(seg_of); free(cnt);
+    return 0;
+}

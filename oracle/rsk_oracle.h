@@ -87,6 +87,17 @@ int orc_build_wire(const uint8_t *frame, int frame_len, uint32_t src, uint32_t d
  * value (i.e. the 16-bit value whose big-endian bytes go into the header). */
 uint16_t orc_inet_csum(const uint8_t *p, size_t n, uint32_t init);
 
+/* Receive demux (semantics in include/rsk_codec.h rsk_demux_batch): the reference's
+ * per-packet conn lookups (INetGroup.cpp:57-83 by connKey, IAppGroup.cpp:76-96 by cmd,
+ * ServerGroup.cpp:44-60 by IdBuf, SubGroup.cpp:31-50 by (dst, conv), ClientGroup.cpp:66-80 by conv)
+ * restated as a sequential walk: each VALID packet looks its key up in a map (new key -> next
+ * segment id), control packets (cmd != 0) under RSK_DEMUX_CMD_BARRIER open a new epoch.  Pointers
+ * for unselected fields may be NULL.  Returns 0, or -12 on allocation failure. */
+int orc_demux_batch(uint32_t n, const int8_t *status, const uint8_t *cmd, const uint8_t *id,
+                    const uint32_t *conv, const uint64_t *conn_key, const uint32_t *dst,
+                    uint32_t fields, uint32_t *perm, uint32_t *seg_off, uint32_t *seg_first,
+                    uint32_t *n_seg, uint32_t *n_valid);
+
 /* KeyGenerator::KeyForTcp / KeyForUdp (src/util/KeyGenerator.cpp:16-36) */
 uint64_t orc_key_for_tcp(uint16_t sp, uint16_t dp);
 uint64_t orc_key_for_udp(uint16_t sp, uint16_t dp);

@@ -30,6 +30,7 @@ SEND_OVERSIZE, SEND_RESET = -1, 0
 RECV_VALID, RECV_CLOSE, RECV_DROP = 1, 0, -1
 PARSE_DROP, PARSE_DELIVER, PARSE_SYN, PARSE_MALFORMED = 0, 1, 2, 3
 PARSE_HAS_ACK_POOL, PARSE_IS_SERVER = 0x1, 0x2
+DEMUX_ID, DEMUX_CONN_KEY, DEMUX_CONV, DEMUX_DST, DEMUX_CMD_BARRIER = 0x01, 0x02, 0x04, 0x08, 0x10
 
 _vp = ctypes.c_void_p
 _u8p = ctypes.c_void_p  # all arrays passed as raw addresses
@@ -93,6 +94,14 @@ class TcpInfoOut(ctypes.Structure):
     ]
 
 
+class DemuxIn(ctypes.Structure):
+    _fields_ = [("status", _vp), ("cmd", _vp), ("id", _vp), ("conv", _vp), ("conn_key", _vp), ("dst", _vp)]
+
+
+class DemuxOut(ctypes.Structure):
+    _fields_ = [("perm", _vp), ("seg_off", _vp), ("seg_first", _vp), ("n_seg", _vp), ("n_valid", _vp)]
+
+
 # (name, restype, argtypes) for every symbol the header declares
 SIGNATURES = [
     ("rsk_create", _vp, [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_int]),
@@ -111,6 +120,8 @@ SIGNATURES = [
       ctypes.POINTER(TcpInfoOut), ctypes.POINTER(DecodeOut), _vp]),
     ("rsk_tcpinfo_encode_batch", ctypes.c_int,
      [_vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("rsk_demux_batch", ctypes.c_int,
+     [_vp, ctypes.c_uint32, ctypes.POINTER(DemuxIn), ctypes.c_uint32, ctypes.POINTER(DemuxOut), _vp]),
     ("rsk_compute_hash", _vp, [_vp, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]),
     ("rsk_hash_equal", ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]),
     ("rsk_enchead_enc2buf", _vp,

@@ -98,6 +98,33 @@ class DecodeBuffers:
 
 
 @dataclass
+class DemuxBuffers:
+    """Outputs of rsk_demux_batch for a batch of n packets (rsk_demux_out)."""
+
+    perm: torch.Tensor
+    seg_off: torch.Tensor
+    seg_first: torch.Tensor
+    n_seg: torch.Tensor
+    n_valid: torch.Tensor
+
+    @classmethod
+    def alloc(cls, n: int, device) -> "DemuxBuffers":
+        e = lambda k: torch.empty(k, dtype=torch.int32, device=device)  # noqa: E731
+        return cls(perm=e(max(n, 1)), seg_off=e(n + 1), seg_first=e(max(n, 1)), n_seg=e(1), n_valid=e(1))
+
+    def abi(self) -> _abi.DemuxOut:
+        return _abi.DemuxOut(*[_ptr(getattr(self, f.name)) for f in fields(self)])
+
+    def segments(self):
+        """Host view: list of (first packet, [packet indices]) in segment order."""
+        ns, nv = int(self.n_seg.item()), int(self.n_valid.item())
+        perm = self.perm[:nv].cpu().numpy().astype("uint32")
+        off = self.seg_off[: ns + 1].cpu().numpy().astype("uint32")
+        first = self.seg_first[:ns].cpu().numpy().astype("uint32")
+        return [(int(first[s]), perm[off[s]:off[s + 1]].tolist()) for s in range(ns)]
+
+
+@dataclass
 class TcpInfoBuffers:
     """SoA TcpInfo outputs of RawTcp::RawInput for n captured packets (rsk_tcpinfo_out)."""
 
@@ -223,6 +250,15 @@ class Codec:
         _check(lib().rsk_tcpinfo_encode_batch(self._ctx, n, _ptr(src), _ptr(dst), _ptr(sp), _ptr(dp),
                                               _ptr(seq), _ptr(ack), _ptr(flag), _ptr(rec),
                                               _stream(stream)), "rsk_tcpinfo_encode_batch")
+
+    def demux_batch(self, status, cmd, fields: int, out: "DemuxBuffers", id=None, conv=None, conn_key=None,
+                    dst=None, stream=None) -> None:
+        """Stable group-by of the VALID packets on `fields` (rsk_demux_batch):
+        segment s = out.perm[out.seg_off[s]:out.seg_off[s + 1]], keyed by packet out.seg_first[s]."""
+        n = status.numel()
+        din = _abi.DemuxIn(_ptr(status), _ptr(cmd), _ptr(id), _ptr(conv), _ptr(conn_key), _ptr(dst))
+        _check(lib().rsk_demux_batch(self._ctx, n, ctypes.byref(din), fields, ctypes.byref(out.abi()),
+                                     _stream(stream)), "rsk_demux_batch")
 
     # ---- reference single-call signatures (GPU round trip each) -----------------------------
     def compute_hash(self, data: bytes) -> bytes | None:

@@ -1,0 +1,536 @@
+// rsk_demux.hip — receive demux for MI355X (gfx950): stable group-by of a decoded batch's VALID
+// packets on selected EncHead / TcpInfo fields (semantics: include/rsk_codec.h).
+//
+// The reference routes each VALID packet with its own map lookup — INetGroup::Input by connKey
+// (conn/INetGroup.cpp:57-83), IAppGroup::Input by cmd (conn/IAppGroup.cpp:76-96), ServerGroup::
+// OnRecv by IdBuf (server/ServerGroup.cpp:44-60), SubGroup::OnRecv by (dst, conv)
+// (server/SubGroup.cpp:31-50), ClientGroup::OnRecv by conv (client/ClientGroup.cpp:66-80).  Here a
+// batch becomes segments (one per key and epoch, ordered by first packet, arrival order inside), so
+// the host does one lookup per segment.
+//
+// Pipeline (all stream-ordered, no host sync; n_valid and the segment count stay on the device):
+//   k_dm_flags   per-wave ballots of VALID and VALID-control packets + per-block counts
+//   scan x2      block offsets (compacted index, epoch = number of earlier control packets)
+//   k_dm_prep    cidx[j] = packet of compacted slot j, cep[j] = its epoch (CTRL for singletons)
+//   k_dm_insert  open-addressing table keyed by packet index: a slot holds the compacted index of
+//                one packet of its key, so key comparison reads the immutable input arrays (no
+//                lane ever waits on another lane's write); lanes of a wave with equal keys insert
+//                once; atomicMin leaves each key's first packet in tab_min
+//   k_dm_leader  leader of j = tab_min[slot] (or j for a control packet); ballots of leaders
+//   scan         leader ranks = dense segment ids in first-occurrence order
+//   k_dm_rank    rank_at[leader], seg_first[rank]
+//   k_dm_segof   radix keys = segment id of each compacted packet, values = j
+//   radix        stable LSD sort by segment id, 8-bit digits, as many passes as the segment count
+//                needs (passes beyond that return at once; the device-side count decides)
+//   k_dm_final   perm = cidx[sorted values], seg_off from the key boundaries, n_seg / n_valid
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+
+#include "../../include/rsk_codec.h"
+#include "rsk_ctx.h"
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;
+constexpr uint32_t kItems = 16;                 // radix: items per thread per tile
+constexpr uint32_t kTile = kBlock * kItems;     // 4096 packets per radix tile
+constexpr uint32_t kNone = 0xffffffffu;
+constexpr uint32_t kCtrl = 0xffffffffu;         // cep[] marker: control packet (singleton segment)
+constexpr uint32_t kScanChunk = 4096;           // elements per block in the multi-block scan
+
+__device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t j) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)j);
+}
+__device__ __forceinline__ uint64_t lanemask_lt(uint32_t lane) { return (1ull << lane) - 1ull; }
+
+// ---- scans ----------------------------------------------------------------------------------
+// exclusive scan of 4096 u32 per pass by one 1024-thread block; carry across passes
+__device__ __forceinline__ void block_scan_4096(const uint32_t *in, uint32_t *out, uint32_t base, uint32_t cnt,
+                                                uint32_t &carry, uint32_t *wsum) {
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+    const uint32_t idx = base + 4u * t;
+    uint32_t c[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) c[k] = idx + k < cnt ? in[idx + k] : 0u;
+    const uint32_t tsum = c[0] + c[1] + c[2] + c[3];
+    uint32_t inc = tsum;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t v = __shfl_up(inc, off);
+        if (lane >= (uint32_t)off) inc += v;
+    }
+    if (lane == 63u) wsum[wv] = inc;
+    __syncthreads();
+    uint32_t wpre = 0, total = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 16; ++q) {
+        const uint32_t v = wsum[q];
+        wpre += q < wv ? v : 0u;
+        total += v;
+    }
+    uint32_t run = carry + wpre + inc - tsum;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (idx + k < cnt) out[idx + k] = run;
+        run += c[k];
+    }
+    carry += total;
+    __syncthreads();
+}
+
+// one block: exclusive scan of cnt elements (any cnt), total to *total if non-null
+__global__ __launch_bounds__(1024) void k_dm_scan1(const uint32_t *in, uint32_t *out, uint32_t cnt, uint32_t *total) {
+    __shared__ uint32_t wsum[16];
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < cnt; base += 4096u) block_scan_4096(in, out, base, cnt, carry, wsum);
+    if (threadIdx.x == 0 && total) *total = carry;
+}
+// multi-block: chunk sums, then (k_dm_scan1 over the sums), then per-chunk scan with its offset
+__global__ __launch_bounds__(1024) void k_dm_chunk_sum(const uint32_t *in, uint32_t cnt, uint32_t *sums) {
+    __shared__ uint32_t wsum[16];
+    const uint32_t base = blockIdx.x * kScanChunk, t = threadIdx.x, lane = t & 63u;
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s += base + 4u * t + k < cnt ? in[base + 4u * t + k] : 0u;
+#pragma unroll
+    for (int off = 32; off; off >>= 1) s += __shfl_xor(s, off);
+    if (lane == 0) wsum[t >> 6] = s;
+    __syncthreads();
+    if (t == 0) {
+        uint32_t a = 0;
+        for (int q = 0; q < 16; ++q) a += wsum[q];
+        sums[blockIdx.x] = a;
+    }
+}
+__global__ __launch_bounds__(1024) void k_dm_chunk_apply(const uint32_t *in, uint32_t *out, uint32_t cnt,
+                                                         const uint32_t *sum_off) {
+    __shared__ uint32_t wsum[16];
+    uint32_t carry = sum_off[blockIdx.x];
+    block_scan_4096(in, out, blockIdx.x * kScanChunk, cnt, carry, wsum);
+}
+
+struct ScanWs {
+    uint32_t *sums, *sum_off;  // >= ceil(max cnt / kScanChunk) each
+};
+
+int scan_u32(const uint32_t *in, uint32_t *out, uint32_t cnt, uint32_t *total, const ScanWs &w, hipStream_t s) {
+    if (cnt <= 4u * kScanChunk) {
+        hipLaunchKernelGGL(k_dm_scan1, dim3(1), dim3(1024), 0, s, in, out, cnt, total);
+        return rsk::launch_check("k_dm_scan1");
+    }
+    const uint32_t nc = (cnt + kScanChunk - 1) / kScanChunk;
+    hipLaunchKernelGGL(k_dm_chunk_sum, dim3(nc), dim3(1024), 0, s, in, cnt, w.sums);
+    hipLaunchKernelGGL(k_dm_scan1, dim3(1), dim3(1024), 0, s, w.sums, w.sum_off, nc, total);
+    hipLaunchKernelGGL(k_dm_chunk_apply, dim3(nc), dim3(1024), 0, s, in, out, cnt, w.sum_off);
+    return rsk::launch_check("scan_u32");
+}
+
+// ---- demux kernels --------------------------------------------------------------------------
+struct DmIn {
+    const int8_t *status;
+    const uint8_t *cmd;
+    const uint64_t *id;  // IdBuf as one u64 (8-B aligned)
+    const uint32_t *conv;
+    const uint64_t *key;
+    const uint32_t *dst;
+    uint32_t n, fields;
+};
+
+// ballots of a block's 4 waves + the block's popcount
+__device__ __forceinline__ void block_ballot(bool p, uint64_t *masks, uint32_t *counts, uint32_t *wc) {
+    const uint64_t m = __ballot(p);
+    const uint32_t w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63u) == 0) {
+        masks[(uint64_t)blockIdx.x * kWaves + w] = m;
+        wc[w] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) counts[blockIdx.x] = wc[0] + wc[1] + wc[2] + wc[3];
+}
+// exclusive rank of this lane's set bit among the block's ballots, plus the block's scanned offset
+__device__ __forceinline__ uint32_t block_rank(const uint64_t *masks, const uint32_t *offsets) {
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint64_t *mb = masks + (uint64_t)blockIdx.x * kWaves;
+    uint32_t pos = offsets[blockIdx.x];
+    for (uint32_t q = 0; q < w; ++q) pos += (uint32_t)__popcll(mb[q]);
+    return pos + (uint32_t)__popcll(mb[w] & lanemask_lt(lane));
+}
+
+__global__ __launch_bounds__(kBlock) void k_dm_flags(DmIn a, uint64_t *mv, uint32_t *cv, uint64_t *mc, uint32_t *cc) {
+    __shared__ uint32_t wc[2][kWaves];
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const bool valid = i < a.n && a.status[i] == RSK_RECV_VALID;
+    const bool ctrl = valid && (a.fields & RSK_DEMUX_CMD_BARRIER) && a.cmd[i] != RSK_CMD_DATA;
+    block_ballot(valid, mv, cv, wc[0]);
+    block_ballot(ctrl, mc, cc, wc[1]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_dm_prep(DmIn a, const uint64_t *mv, const uint32_t *ov,
+                                                    const uint64_t *mc, const uint32_t *oc, uint32_t *cidx,
+                                                    uint32_t *cep) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    if (!((mv[(uint64_t)blockIdx.x * kWaves + w] >> lane) & 1ull)) return;
+    const uint32_t j = block_rank(mv, ov);
+    const bool ctrl = (mc[(uint64_t)blockIdx.x * kWaves + w] >> lane) & 1ull;
+    cidx[j] = i;
+    cep[j] = ctrl ? kCtrl : block_rank(mc, oc);  // epoch = control packets before this one
+}
+
+struct Key {
+    uint32_t ep, conv, dst;
+    uint64_t id, ck;
+};
+
+__device__ __forceinline__ Key load_key(const DmIn &a, uint32_t i, uint32_t ep) {
+    Key k;
+    k.ep = ep;
+    k.id = (a.fields & RSK_DEMUX_ID) ? a.id[i] : 0ull;
+    k.ck = (a.fields & RSK_DEMUX_CONN_KEY) ? a.key[i] : 0ull;
+    k.conv = (a.fields & RSK_DEMUX_CONV) ? a.conv[i] : 0u;
+    k.dst = (a.fields & RSK_DEMUX_DST) ? a.dst[i] : 0u;
+    return k;
+}
+__device__ __forceinline__ bool key_eq(const Key &x, const Key &y) {
+    return x.ep == y.ep && x.id == y.id && x.ck == y.ck && x.conv == y.conv && x.dst == y.dst;
+}
+__device__ __forceinline__ uint32_t key_hash(const Key &k, uint32_t mask) {
+    uint64_t h = (uint64_t)k.ep * 0x9E3779B97F4A7C15ull ^ k.id * 0xC2B2AE3D27D4EB4Full ^
+                 k.ck * 0x165667B19E3779F9ull ^ ((uint64_t)k.conv | (uint64_t)k.dst << 32) * 0xD6E8FEB86659FD93ull;
+    h ^= h >> 31;
+    h *= 0xBF58476D1CE4E5B9ull;
+    h ^= h >> 29;
+    return (uint32_t)h & mask;
+}
+
+__global__ __launch_bounds__(kBlock) void k_dm_insert(DmIn a, const uint32_t *nvp, const uint32_t *cidx,
+                                                      const uint32_t *cep, uint32_t *owner, uint32_t *tmin,
+                                                      uint32_t mask, uint32_t *hslot) {
+    const uint32_t nv = *nvp;
+    const uint32_t j0 = (blockIdx.x * kBlock + threadIdx.x) & ~63u;
+    if (j0 >= nv) return;  // wave-uniform
+    const uint32_t lane = threadIdx.x & 63u, j = j0 + lane;
+    const bool active = j < nv;
+    const uint32_t ep = active ? cep[j] : kCtrl;
+    const bool need = active && ep != kCtrl;
+    Key k = {0, 0, 0, 0, 0};
+    if (need) k = load_key(a, cidx[j], ep);
+    uint32_t slot = kNone;
+    uint64_t pend = __ballot(need);
+    while (pend) {  // one insert per distinct key in the wave, by its lowest lane
+        const uint32_t L = (uint32_t)__builtin_ctzll(pend);
+        Key r;
+        r.ep = rdl(k.ep, L);
+        r.conv = rdl(k.conv, L);
+        r.dst = rdl(k.dst, L);
+        r.id = (uint64_t)rdl((uint32_t)k.id, L) | ((uint64_t)rdl((uint32_t)(k.id >> 32), L) << 32);
+        r.ck = (uint64_t)rdl((uint32_t)k.ck, L) | ((uint64_t)rdl((uint32_t)(k.ck >> 32), L) << 32);
+        const uint64_t same = __ballot(need && key_eq(k, r)) & pend;
+        uint32_t h = 0;
+        if (lane == L) {
+            h = key_hash(r, mask);
+            for (;;) {
+                uint32_t o = __hip_atomic_load(owner + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (o == kNone) {
+                    o = atomicCAS(owner + h, kNone, j);
+                    if (o == kNone) break;
+                }
+                if (key_eq(load_key(a, cidx[o], cep[o]), r)) break;
+                h = (h + 1u) & mask;
+            }
+            if (__hip_atomic_load(tmin + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > j) atomicMin(tmin + h, j);
+        }
+        h = rdl(h, L);
+        if ((same >> lane) & 1ull) slot = h;
+        pend &= ~same;
+    }
+    if (active) hslot[j] = slot;
+}
+
+__global__ __launch_bounds__(kBlock) void k_dm_leader(const uint32_t *nvp, const uint32_t *hslot, const uint32_t *tmin,
+                                                      uint32_t *lead_of, uint64_t *ml, uint32_t *cl) {
+    __shared__ uint32_t wc[kWaves];
+    const uint32_t nv = *nvp;
+    const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
+    bool isl = false;
+    if (j < nv) {
+        const uint32_t h = hslot[j];
+        const uint32_t lead = h == kNone ? j : tmin[h];
+        lead_of[j] = lead;
+        isl = lead == j;
+    }
+    block_ballot(isl, ml, cl, wc);
+}
+
+__global__ __launch_bounds__(kBlock) void k_dm_rank(const uint32_t *nvp, const uint64_t *ml, const uint32_t *ol,
+                                                    const uint32_t *cidx, uint32_t *rank_at, uint32_t *seg_first) {
+    const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    if (j >= *nvp || !((ml[(uint64_t)blockIdx.x * kWaves + w] >> lane) & 1ull)) return;
+    const uint32_t r = block_rank(ml, ol);
+    rank_at[j] = r;
+    seg_first[r] = cidx[j];
+}
+
+__global__ __launch_bounds__(kBlock) void k_dm_segof(const uint32_t *nvp, const uint32_t *lead_of,
+                                                     const uint32_t *rank_at, uint32_t *keys, uint32_t *vals) {
+    const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
+    if (j >= *nvp) return;
+    keys[j] = rank_at[lead_of[j]];
+    vals[j] = j;
+}
+
+// ---- stable LSD radix sort by segment id ------------------------------------------------------
+__device__ __forceinline__ uint32_t bits_for(uint32_t nseg) {  // digits needed for keys < nseg
+    return nseg <= 1u ? 1u : 32u - (uint32_t)__builtin_clz(nseg - 1u);
+}
+__device__ __forceinline__ bool pass_live(uint32_t pass, uint32_t nseg) {
+    return pass == 0 || 8u * pass < bits_for(nseg);
+}
+
+// lanes of this wave holding the same digit (valid lanes only)
+__device__ __forceinline__ uint64_t digit_peers(bool v, uint32_t d) {
+    uint64_t peers = __ballot(v);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        const uint64_t m = __ballot(v && ((d >> b) & 1u));
+        peers &= ((d >> b) & 1u) ? m : ~m;
+    }
+    return peers;
+}
+
+__global__ __launch_bounds__(kBlock) void k_dm_hist(uint32_t pass, const uint32_t *nvp, const uint32_t *nsegp,
+                                                    const uint32_t *keys, uint32_t *hist, uint32_t nt) {
+    __shared__ uint32_t lh[256];
+    const uint32_t nv = *nvp;
+    if (!pass_live(pass, *nsegp)) return;  // block-uniform
+    const uint32_t t = threadIdx.x, lane = t & 63u;
+    lh[t] = 0;
+    __syncthreads();
+    const uint32_t sh = 8u * pass;
+    const uint32_t rounds = blockIdx.x * kTile < nv ? kItems : 0u;  // tiles past n_valid count zeros
+    for (uint32_t r = 0; r < rounds; ++r) {
+        const uint32_t k = blockIdx.x * kTile + r * kBlock + t;
+        const bool v = k < nv;
+        const uint32_t d = v ? (keys[k] >> sh) & 255u : 0u;
+        const uint64_t peers = digit_peers(v, d);
+        if (v && (peers & lanemask_lt(lane)) == 0) atomicAdd(&lh[d], (uint32_t)__popcll(peers));
+    }
+    __syncthreads();
+    hist[t * nt + blockIdx.x] = lh[t];
+}
+
+__global__ __launch_bounds__(kBlock) void k_dm_scatter(uint32_t pass, const uint32_t *nvp, const uint32_t *nsegp,
+                                                       const uint32_t *kin, const uint32_t *vin,
+                                                       const uint32_t *hoff, uint32_t nt, uint32_t *kout,
+                                                       uint32_t *vout) {
+    __shared__ uint32_t run[256];
+    __shared__ uint32_t wcnt[kWaves][256];
+    const uint32_t nv = *nvp;
+    if (!pass_live(pass, *nsegp) || blockIdx.x * kTile >= nv) return;  // block-uniform
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    run[t] = 0;
+#pragma unroll
+    for (int q = 0; q < kWaves; ++q) wcnt[q][t] = 0;
+    const uint32_t base = hoff[t * nt + blockIdx.x];  // this tile's first slot for digit t
+    __shared__ uint32_t dbase[256];
+    dbase[t] = base;
+    __syncthreads();
+    const uint32_t sh = 8u * pass;
+    for (uint32_t r = 0; r < kItems; ++r) {
+        const uint32_t k = blockIdx.x * kTile + r * kBlock + t;
+        const bool v = k < nv;
+        const uint32_t key = v ? kin[k] : 0u;
+        const uint32_t d = (key >> sh) & 255u;
+        const uint64_t peers = digit_peers(v, d);
+        const uint32_t lt = (uint32_t)__popcll(peers & lanemask_lt(lane));
+        if (v && lt == 0) wcnt[w][d] = (uint32_t)__popcll(peers);
+        __syncthreads();
+        if (v) {
+            uint32_t pos = dbase[d] + run[d] + lt;
+            for (uint32_t q = 0; q < w; ++q) pos += wcnt[q][d];
+            kout[pos] = key;
+            vout[pos] = vin[k];
+        }
+        __syncthreads();
+        uint32_t add = 0;
+#pragma unroll
+        for (int q = 0; q < kWaves; ++q) {
+            add += wcnt[q][t];
+            wcnt[q][t] = 0;
+        }
+        run[t] += add;
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_dm_final(const uint32_t *nvp, const uint32_t *nsegp, const uint32_t *kA,
+                                                     const uint32_t *vA, const uint32_t *kB, const uint32_t *vB,
+                                                     const uint32_t *cidx, uint32_t *perm, uint32_t *seg_off,
+                                                     uint32_t *n_seg, uint32_t *n_valid) {
+    const uint32_t nv = *nvp, ns = *nsegp;
+    const uint32_t passes = (bits_for(ns) + 7u) / 8u;  // effective passes; pass p writes B when p is even
+    const bool inB = ((passes - 1u) & 1u) == 0u;
+    const uint32_t *keys = inB ? kB : kA;
+    const uint32_t *vals = inB ? vB : vA;
+    const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
+    if (k == 0) {
+        *n_seg = ns;
+        *n_valid = nv;
+        seg_off[ns] = nv;
+    }
+    if (k >= nv) return;
+    perm[k] = cidx[vals[k]];
+    const uint32_t key = keys[k];
+    if (k == 0 || keys[k - 1] != key) seg_off[key] = k;
+}
+
+// ---- workspace ------------------------------------------------------------------------------
+struct DmWs {
+    uint64_t *mv, *mc, *ml;
+    uint32_t *cv, *ov, *cc, *oc, *cl, *ol;
+    uint32_t *cidx, *cep, *hslot, *lead_of, *rank_at;
+    uint32_t *kA, *vA, *kB, *vB;
+    uint32_t *owner, *tmin;
+    uint32_t *hist, *hoff;
+    uint32_t *nv, *nseg;
+    ScanWs scan;
+    uint32_t nb, nt, tsize;
+};
+
+uint32_t table_size(uint32_t n) {
+    uint32_t t = 64;
+    while (t < 2u * n) t <<= 1;
+    return t;
+}
+
+size_t dm_layout(uint32_t n, uint8_t *base, DmWs *w) {
+    const uint32_t nb = (n + kBlock - 1) / kBlock, nt = (n + kTile - 1) / kTile, T = table_size(n);
+    const uint32_t nh = 256u * nt, nc = (nh > nb ? nh : nb) / kScanChunk + 2;
+    size_t off = 0;
+    auto take = [&](size_t bytes) -> uint8_t * {
+        uint8_t *p = base ? base + off : nullptr;
+        off += (bytes + 255) & ~size_t(255);
+        return p;
+    };
+    DmWs d;
+    d.mv = (uint64_t *)take(8ull * nb * kWaves);
+    d.mc = (uint64_t *)take(8ull * nb * kWaves);
+    d.ml = (uint64_t *)take(8ull * nb * kWaves);
+    d.cv = (uint32_t *)take(4ull * nb);
+    d.ov = (uint32_t *)take(4ull * nb);
+    d.cc = (uint32_t *)take(4ull * nb);
+    d.oc = (uint32_t *)take(4ull * nb);
+    d.cl = (uint32_t *)take(4ull * nb);
+    d.ol = (uint32_t *)take(4ull * nb);
+    d.cidx = (uint32_t *)take(4ull * n);
+    d.cep = (uint32_t *)take(4ull * n);
+    d.hslot = (uint32_t *)take(4ull * n);
+    d.lead_of = (uint32_t *)take(4ull * n);
+    d.rank_at = (uint32_t *)take(4ull * n);
+    d.kA = (uint32_t *)take(4ull * n);
+    d.vA = (uint32_t *)take(4ull * n);
+    d.kB = (uint32_t *)take(4ull * n);
+    d.vB = (uint32_t *)take(4ull * n);
+    d.owner = (uint32_t *)take(4ull * T);
+    d.tmin = (uint32_t *)take(4ull * T);
+    d.hist = (uint32_t *)take(4ull * nh);
+    d.hoff = (uint32_t *)take(4ull * nh);
+    d.scan.sums = (uint32_t *)take(4ull * nc);
+    d.scan.sum_off = (uint32_t *)take(4ull * nc);
+    d.nv = (uint32_t *)take(8);
+    d.nseg = (uint32_t *)take(8);
+    d.nb = nb;
+    d.nt = nt;
+    d.tsize = T;
+    if (w) *w = d;
+    return off;
+}
+
+int ensure_dm_ws(rsk_ctx *c, uint32_t n) {
+    const size_t need = dm_layout(n, nullptr, nullptr);
+    if (c->dm_ws && c->dm_ws_bytes >= need) return RSK_OK;
+    if (c->dm_ws) {
+        hipError_t e = hipDeviceSynchronize();
+        if (e != hipSuccess) { rsk::set_error("hipDeviceSynchronize", e); return RSK_EDEVICE; }
+        (void)hipFree(c->dm_ws);
+        c->dm_ws = nullptr;
+        c->dm_ws_bytes = 0;
+    }
+    hipError_t e = hipMalloc(&c->dm_ws, need);
+    if (e != hipSuccess) { rsk::set_error("hipMalloc(demux workspace)", e); return RSK_ENOMEM; }
+    c->dm_ws_bytes = need;
+    return RSK_OK;
+}
+
+}  // namespace
+
+extern "C" int rsk_demux_batch(rsk_ctx *c, uint32_t n, const rsk_demux_in *in, uint32_t fields,
+                               const rsk_demux_out *out, void *stream) {
+    if (!c || !in || !out || !out->perm || !out->seg_off || !out->seg_first || !out->n_seg || !out->n_valid)
+        return RSK_EINVAL;
+    if (fields & ~0x1fu) return RSK_EINVAL;
+    if (n && (!in->status || !in->cmd)) return RSK_EINVAL;
+    if (n && (fields & RSK_DEMUX_ID) && (!in->id || (reinterpret_cast<uintptr_t>(in->id) & 7u))) return RSK_EINVAL;
+    if (n && (fields & RSK_DEMUX_CONN_KEY) && !in->conn_key) return RSK_EINVAL;
+    if (n && (fields & RSK_DEMUX_CONV) && !in->conv) return RSK_EINVAL;
+    if (n && (fields & RSK_DEMUX_DST) && !in->dst) return RSK_EINVAL;
+    if (n > 0x7fffffffu) return RSK_EINVAL;
+    rsk::DeviceGuard g(c->device);
+    if (!g.ok) return RSK_EDEVICE;
+    hipStream_t s = (hipStream_t)stream;
+    if (n == 0) {
+        hipError_t e = hipMemsetAsync(out->n_seg, 0, 4, s);
+        if (e == hipSuccess) e = hipMemsetAsync(out->n_valid, 0, 4, s);
+        if (e == hipSuccess) e = hipMemsetAsync(out->seg_off, 0, 4, s);
+        if (e != hipSuccess) { rsk::set_error("hipMemsetAsync", e); return RSK_EDEVICE; }
+        return RSK_OK;
+    }
+    int r = ensure_dm_ws(c, n);
+    if (r) return r;
+    DmWs w;
+    dm_layout(n, static_cast<uint8_t *>(c->dm_ws), &w);
+    DmIn a;
+    a.status = in->status;
+    a.cmd = in->cmd;
+    a.id = reinterpret_cast<const uint64_t *>(in->id);
+    a.conv = in->conv;
+    a.key = in->conn_key;
+    a.dst = in->dst;
+    a.n = n;
+    a.fields = fields;
+    hipError_t e = hipMemsetAsync(w.owner, 0xff, 8ull * w.tsize, s);  // owner + tmin (adjacent)
+    if (e != hipSuccess) { rsk::set_error("hipMemsetAsync(table)", e); return RSK_EDEVICE; }
+    const uint32_t nb = w.nb;
+    hipLaunchKernelGGL(k_dm_flags, dim3(nb), dim3(kBlock), 0, s, a, w.mv, w.cv, w.mc, w.cc);
+    if ((r = rsk::launch_check("k_dm_flags"))) return r;
+    if ((r = scan_u32(w.cv, w.ov, nb, w.nv, w.scan, s))) return r;
+    if ((r = scan_u32(w.cc, w.oc, nb, nullptr, w.scan, s))) return r;
+    hipLaunchKernelGGL(k_dm_prep, dim3(nb), dim3(kBlock), 0, s, a, w.mv, w.ov, w.mc, w.oc, w.cidx, w.cep);
+    hipLaunchKernelGGL(k_dm_insert, dim3(nb), dim3(kBlock), 0, s, a, w.nv, w.cidx, w.cep, w.owner, w.tmin,
+                       w.tsize - 1u, w.hslot);
+    hipLaunchKernelGGL(k_dm_leader, dim3(nb), dim3(kBlock), 0, s, w.nv, w.hslot, w.tmin, w.lead_of, w.ml, w.cl);
+    if ((r = rsk::launch_check("k_dm_leader"))) return r;
+    if ((r = scan_u32(w.cl, w.ol, nb, w.nseg, w.scan, s))) return r;
+    hipLaunchKernelGGL(k_dm_rank, dim3(nb), dim3(kBlock), 0, s, w.nv, w.ml, w.ol, w.cidx, w.rank_at, out->seg_first);
+    hipLaunchKernelGGL(k_dm_segof, dim3(nb), dim3(kBlock), 0, s, w.nv, w.lead_of, w.rank_at, w.kA, w.vA);
+    if ((r = rsk::launch_check("k_dm_segof"))) return r;
+    // passes for the worst case (every packet its own segment); surplus passes return at once
+    uint32_t maxbits = 1;
+    while (maxbits < 32 && (1ull << maxbits) < n) ++maxbits;
+    const uint32_t passes = (maxbits + 7) / 8;
+    for (uint32_t p = 0; p < passes; ++p) {
+        const uint32_t *kin = (p & 1u) ? w.kB : w.kA, *vin = (p & 1u) ? w.vB : w.vA;
+        uint32_t *kout = (p & 1u) ? w.kA : w.kB, *vout = (p & 1u) ? w.vA : w.vB;
+        hipLaunchKernelGGL(k_dm_hist, dim3(w.nt), dim3(kBlock), 0, s, p, w.nv, w.nseg, kin, w.hist, w.nt);
+        if ((r = scan_u32(w.hist, w.hoff, 256u * w.nt, nullptr, w.scan, s))) return r;
+        hipLaunchKernelGGL(k_dm_scatter, dim3(w.nt), dim3(kBlock), 0, s, p, w.nv, w.nseg, kin, vin, w.hoff, w.nt,
+                           kout, vout);
+        if ((r = rsk::launch_check("k_dm_scatter"))) return r;
+    }
+    hipLaunchKernelGGL(k_dm_final, dim3(nb), dim3(kBlock), 0, s, w.nv, w.nseg, w.kA, w.vA, w.kB, w.vB, w.cidx,
+                       out->perm, out->seg_off, out->n_seg, out->n_valid);
+    return rsk::launch_check("k_dm_final");
+}

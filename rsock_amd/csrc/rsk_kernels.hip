@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "../../include/rsk_codec.h"
+#include "rsk_ctx.h"
 #include "rsk_device.h"
 #include "rsk_md5.h"
 
@@ -30,11 +31,10 @@ namespace {
 constexpr int kBlock = 256;  // 4 waves of 64
 constexpr int kWavesPerBlock = kBlock / 64;
 
-thread_local char g_last_error[256] = "";
-
-void set_error(const char *what, hipError_t e) {
-    snprintf(g_last_error, sizeof g_last_error, "%s: %s", what, hipGetErrorString(e));
-}
+using rsk::DeviceGuard;
+using rsk::g_last_error;
+using rsk::launch_check;
+using rsk::set_error;
 
 // ---------------------------------------------------------------------------------------------
 // Encode
@@ -1113,10 +1113,12 @@ __global__ __launch_bounds__(kBlock) void k_tcpinfo_encode(TcpRecArgs a) {
 // ---------------------------------------------------------------------------------------------
 // Single-packet shims (compatibility surface for the reference's per-call signatures)
 // ---------------------------------------------------------------------------------------------
+}  // namespace
 struct ShimIO {
     uint8_t buf[64];   // in: op-specific input bytes; out: op-specific output bytes
     int32_t ret;
 };
+namespace {
 
 __global__ void k_shim(ShimIO *io, int op, int len_arg, KeySched ks) {
     if (threadIdx.x != 0) return;
@@ -1226,44 +1228,11 @@ void build_sched(const uint8_t *key, uint32_t klen, KeySched &ks) {
     ks.two_blocks = two ? 1 : 0;
 }
 
-struct DeviceGuard {
-    int prev = -1;
-    bool ok = true;
-    explicit DeviceGuard(int dev) {
-        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-        if (prev != dev) {
-            hipError_t e = hipSetDevice(dev);
-            if (e != hipSuccess) {
-                set_error("hipSetDevice", e);
-                ok = false;
-            }
-        }
-    }
-    ~DeviceGuard() {
-        int cur = -1;
-        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-    }
-};
-
 inline unsigned grid_for(uint64_t threads) { return (unsigned)((threads + kBlock - 1) / kBlock); }
 
 }  // namespace
 
-struct rsk_ctx {
-    int device = 0;
-    int enc_variant = 0;  // see rsk__set_encode_variant
-    int wire_variant = 0;  // see rsk__set_wire_variant
-    std::vector<uint8_t> key;
-    KeySched ks;
-    // compaction workspace
-    void *ws = nullptr;
-    uint32_t ws_n = 0;
-    // single-packet shim buffers
-    ShimIO *shim_dev = nullptr;
-    ShimIO *shim_host = nullptr;
-    hipStream_t shim_stream = nullptr;
-    std::mutex shim_mu;
-};
+thread_local char rsk::g_last_error[256] = "";
 
 namespace {
 
@@ -1292,12 +1261,6 @@ void ws_split(rsk_ctx *c, uint32_t n, uint64_t *&masks, uint32_t *&counts, uint3
     masks = reinterpret_cast<uint64_t *>(c->ws);
     counts = reinterpret_cast<uint32_t *>(masks + nb * kWavesPerBlock);
     offsets = counts + nb;
-}
-
-int launch_check(const char *what) {
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) { set_error(what, e); return RSK_EDEVICE; }
-    return RSK_OK;
 }
 
 int run_compaction(rsk_ctx *c, uint32_t n, uint64_t *masks, uint32_t *counts, uint32_t *offsets,
@@ -1382,6 +1345,7 @@ void rsk_destroy(rsk_ctx *c) {
     if (!c) return;
     DeviceGuard g(c->device);
     if (c->ws) (void)hipFree(c->ws);
+    if (c->dm_ws) (void)hipFree(c->dm_ws);
     if (c->shim_dev) (void)hipFree(c->shim_dev);
     if (c->shim_host) (void)hipHostFree(c->shim_host);
     if (c->shim_stream) (void)hipStreamDestroy(c->shim_stream);

@@ -61,6 +61,8 @@ class Oracle:
         L.orc_inet_csum.restype = ctypes.c_uint16
         L.orc_inet_csum.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32]
         L.orc_key_for_tcp.restype = ctypes.c_uint64
+        L.orc_demux_batch.argtypes = [ctypes.c_uint32] + [_vp] * 6 + [ctypes.c_uint32] + [_vp] * 5
+        L.orc_demux_batch.restype = ctypes.c_int
         L.orc_key_for_tcp.argtypes = [ctypes.c_uint16, ctypes.c_uint16]
         L.orc_key_for_udp.restype = ctypes.c_uint64
         L.orc_key_for_udp.argtypes = [ctypes.c_uint16, ctypes.c_uint16]
@@ -133,6 +135,22 @@ class Oracle:
         out = ctypes.create_string_buffer(len(frame) + 64)
         n = self.L.orc_build_wire(frame, len(frame), src, dst, sp, dp, seq, ack, flag, ip_id, eth, out)
         return out.raw[:n]
+
+    def demux_batch(self, status, cmd, fields: int, id=None, conv=None, conn_key=None, dst=None):
+        """-> list of (first packet, [packet indices]) in segment order (orc_demux_batch)."""
+        n = len(status)
+        arrs = [np.ascontiguousarray(status, np.int8), np.ascontiguousarray(cmd, np.uint8)]
+        opt = [None if x is None else np.ascontiguousarray(x, dt)
+               for x, dt in ((id, np.uint8), (conv, np.uint32), (conn_key, np.uint64), (dst, np.uint32))]
+        perm = np.zeros(max(n, 1), np.uint32)
+        seg_off = np.zeros(n + 1, np.uint32)
+        first = np.zeros(max(n, 1), np.uint32)
+        ns, nv = np.zeros(1, np.uint32), np.zeros(1, np.uint32)
+        r = self.L.orc_demux_batch(n, *[_p(a) for a in arrs], *[_p(a) for a in opt], fields, _p(perm), _p(seg_off),
+                                   _p(first), _p(ns), _p(nv))
+        assert r == 0
+        S = int(ns[0])
+        return [(int(first[s]), perm[seg_off[s]:seg_off[s + 1]].tolist()) for s in range(S)], int(nv[0])
 
     def splitmix_bytes(self, seed: int, n: int) -> np.ndarray:
         out = np.empty(n, np.uint8)

@@ -1,0 +1,106 @@
+"""GPU: rsk_demux_batch against the oracle (orc_demux_batch), segment for segment:
+random batches over every field selection, control-packet barriers, all-invalid / all-control /
+single-key / all-distinct batches (1, 2 and 3 radix passes), ragged sizes, and the decoded output
+of the real receive path (C4 frames through rsk_decode_batch, demuxed on the device)."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from rsock_amd import _abi as A
+from rsock_amd import workload
+from tests.test_demux_oracle import ALL, make_case
+
+pytestmark = pytest.mark.gpu
+
+
+def run_gpu(codec, gpu, status, cmd, fields, ids, conv, ckey, dst):
+    import torch
+
+    from rsock_amd.codec import DemuxBuffers
+
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).view(dt)).to(gpu)  # noqa: E731
+    n = len(status)
+    out = DemuxBuffers.alloc(n, gpu)
+    codec.demux_batch(t(status, np.int8), t(cmd, np.uint8), fields, out, id=t(ids, np.uint8),
+                      conv=t(conv, np.int32), conn_key=t(ckey, np.int64), dst=t(dst, np.int32))
+    torch.cuda.synchronize()
+    return out.segments(), int(out.n_valid.item())
+
+
+FIELDS = [ALL, A.DEMUX_CONN_KEY, A.DEMUX_ID | A.DEMUX_CONV | A.DEMUX_DST, A.DEMUX_CONV, 0,
+          ALL | A.DEMUX_CMD_BARRIER, A.DEMUX_CONN_KEY | A.DEMUX_CMD_BARRIER, A.DEMUX_CMD_BARRIER]
+SHAPES = [(1, 1, 0.0, 1.0), (63, 3, 0.1, 0.9), (500, 3, 0.05, 0.9), (4097, 40, 0.01, 0.7), (3000, 3000, 0.0, 1.0),
+          (800, 5, 0.5, 1.0), (300, 4, 0.0, 0.0), (400, 7, 1.0, 1.0), (70000, 300, 0.002, 0.8)]
+
+
+@pytest.mark.parametrize("fields", FIELDS)
+@pytest.mark.parametrize("shape", SHAPES)
+def test_demux_random(codec, gpu, oracle, fields, shape):
+    n, nkeys, p_ctrl, p_valid = shape
+    rng = np.random.default_rng(n * 31 + nkeys + fields)
+    case = make_case(rng, n, nkeys, p_ctrl, p_valid)
+    got = run_gpu(codec, gpu, *case[:2], fields, *case[2:])
+    exp = oracle.demux_batch(case[0], case[1], fields, *case[2:])
+    assert got[1] == exp[1]
+    assert got[0] == exp[0]
+
+
+@pytest.mark.parametrize("n,fields", [(300000, ALL), (200000, A.DEMUX_CONN_KEY | A.DEMUX_CMD_BARRIER),
+                                      (65537, A.DEMUX_CONV)])
+def test_demux_many_segments(codec, gpu, oracle, n, fields):
+    """Every packet its own key (segments = n_valid: 3 radix passes at 300K), and dense barriers."""
+    rng = np.random.default_rng(n)
+    status = np.where(rng.random(n) < 0.95, 1, -1).astype(np.int8)
+    cmd = np.where(rng.random(n) < (0.3 if fields & A.DEMUX_CMD_BARRIER else 0.0), 3, 0).astype(np.uint8)
+    ids = rng.integers(0, 256, 8 * n, dtype=np.uint8)
+    conv = np.arange(n, dtype=np.uint32)
+    ckey = rng.permutation(n).astype(np.uint64) * 7919
+    dst = rng.integers(0, 2, n).astype(np.uint32)
+    got = run_gpu(codec, gpu, status, cmd, fields, ids, conv, ckey, dst)
+    exp = oracle.demux_batch(status, cmd, fields, ids, conv, ckey, dst)
+    assert got[1] == exp[1] and len(got[0]) == len(exp[0])
+    assert got[0] == exp[0]
+
+
+def test_demux_empty_and_errors(codec, gpu):
+    import torch
+
+    from rsock_amd.codec import DemuxBuffers, RskError
+
+    out = DemuxBuffers.alloc(0, gpu)
+    e = torch.empty(0, dtype=torch.int8, device=gpu)
+    codec.demux_batch(e, e.view(torch.uint8), ALL, out, id=e.view(torch.uint8), conv=e, conn_key=e, dst=e)
+    torch.cuda.synchronize()
+    assert int(out.n_seg.item()) == 0 and int(out.n_valid.item()) == 0 and int(out.seg_off[0].item()) == 0
+    st = torch.ones(8, dtype=torch.int8, device=gpu)
+    with pytest.raises(RskError):
+        codec.demux_batch(st, st.view(torch.uint8), 0x40, DemuxBuffers.alloc(8, gpu))  # unknown field bit
+    with pytest.raises(RskError):
+        codec.demux_batch(st, st.view(torch.uint8), A.DEMUX_CONN_KEY, DemuxBuffers.alloc(8, gpu))  # key missing
+
+
+def test_demux_decoded_c4(codec, gpu, oracle):
+    """The receive path end to end on the device: C4 frames (1/16 corrupted, 5% control cmds) ->
+    rsk_decode_batch -> rsk_demux_batch on the decoded fields, vs the oracle on the same fields."""
+    import torch
+
+    from rsock_amd.codec import DecodeBuffers, DemuxBuffers
+
+    d = workload.describe("c4", 0, 50000, n=50000)
+    w = workload.DeviceWorkload(d, gpu)
+    codec.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off, w.status,
+                       id_uniform=workload.ID_UNIFORM)
+    w.corrupt_frames()
+    dec = DecodeBuffers.alloc(d.n, gpu)
+    codec.onrecv_batch(w.frame, w.frame_off, w.frame_len, dec)
+    fields = A.DEMUX_ID | A.DEMUX_CONN_KEY | A.DEMUX_CMD_BARRIER
+    out = DemuxBuffers.alloc(d.n, gpu)
+    codec.demux_batch(dec.status, dec.cmd, fields, out, id=dec.id, conv=dec.conv, conn_key=dec.conn_key)
+    torch.cuda.synchronize()
+    h = lambda x, dt: x.cpu().numpy().view(dt)  # noqa: E731
+    st = h(dec.status, np.int8)
+    assert 0 < (st == 1).sum() < d.n
+    exp = oracle.demux_batch(st, h(dec.cmd, np.uint8), fields, h(dec.id, np.uint8), h(dec.conv, np.uint32),
+                             h(dec.conn_key, np.uint64), None)
+    assert out.segments() == exp[0]
