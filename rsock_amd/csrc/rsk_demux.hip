@@ -12,17 +12,17 @@
 //   k_dm_flags   per-wave ballots of VALID and VALID-control packets + per-block counts
 //   scan x2      block offsets (compacted index, epoch = number of earlier control packets)
 //   k_dm_prep    cidx[j] = packet of compacted slot j, cep[j] = its epoch (CTRL for singletons)
-//   k_dm_insert  open-addressing table keyed by packet index: a slot holds the compacted index of
-//                one packet of its key, so key comparison reads the immutable input arrays (no
-//                lane ever waits on another lane's write); lanes of a wave with equal keys insert
-//                once; atomicMin leaves each key's first packet in tab_min
+//   k_dm_insert  open-addressing table: a slot holds a key fingerprint and the compacted index of
+//                one packet of its key, so key confirmation reads the immutable input arrays (no
+//                lane ever waits on another lane's write); atomicMin leaves each key's first
+//                packet in tmin
 //   k_dm_leader  leader of j = tab_min[slot] (or j for a control packet); ballots of leaders
 //   scan         leader ranks = dense segment ids in first-occurrence order
 //   k_dm_rank    rank_at[leader], seg_first[rank]
-//   k_dm_segof   radix keys = segment id of each compacted packet, values = j
+//   k_dm_segof   radix keys = segment id of each compacted packet, values = its packet index
 //   radix        stable LSD sort by segment id, 8-bit digits, as many passes as the segment count
 //                needs (passes beyond that return at once; the device-side count decides)
-//   k_dm_final   perm = cidx[sorted values], seg_off from the key boundaries, n_seg / n_valid
+//   k_dm_final   perm = sorted values, seg_off from the key boundaries, n_seg / n_valid
 #include <hip/hip_runtime.h>
 
 #include <cstring>
@@ -40,9 +40,6 @@ constexpr uint32_t kNone = 0xffffffffu;
 constexpr uint32_t kCtrl = 0xffffffffu;         // cep[] marker: control packet (singleton segment)
 constexpr uint32_t kScanChunk = 4096;           // elements per block in the multi-block scan
 
-__device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t j) {
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)j);
-}
 __device__ __forceinline__ uint64_t lanemask_lt(uint32_t lane) { return (1ull << lane) - 1ull; }
 
 // ---- scans ----------------------------------------------------------------------------------
@@ -196,57 +193,109 @@ __device__ __forceinline__ Key load_key(const DmIn &a, uint32_t i, uint32_t ep) 
 __device__ __forceinline__ bool key_eq(const Key &x, const Key &y) {
     return x.ep == y.ep && x.id == y.id && x.ck == y.ck && x.conv == y.conv && x.dst == y.dst;
 }
-__device__ __forceinline__ uint32_t key_hash(const Key &k, uint32_t mask) {
+__device__ __forceinline__ uint64_t key_hash(const Key &k) {
     uint64_t h = (uint64_t)k.ep * 0x9E3779B97F4A7C15ull ^ k.id * 0xC2B2AE3D27D4EB4Full ^
                  k.ck * 0x165667B19E3779F9ull ^ ((uint64_t)k.conv | (uint64_t)k.dst << 32) * 0xD6E8FEB86659FD93ull;
     h ^= h >> 31;
     h *= 0xBF58476D1CE4E5B9ull;
     h ^= h >> 29;
-    return (uint32_t)h & mask;
+    return h;
 }
 
-__global__ __launch_bounds__(kBlock) void k_dm_insert(DmIn a, const uint32_t *nvp, const uint32_t *cidx,
-                                                      const uint32_t *cep, uint32_t *owner, uint32_t *tmin,
-                                                      uint32_t mask, uint32_t *hslot) {
-    const uint32_t nv = *nvp;
-    const uint32_t j0 = (blockIdx.x * kBlock + threadIdx.x) & ~63u;
-    if (j0 >= nv) return;  // wave-uniform
-    const uint32_t lane = threadIdx.x & 63u, j = j0 + lane;
-    const bool active = j < nv;
-    const uint32_t ep = active ? cep[j] : kCtrl;
-    const bool need = active && ep != kCtrl;
-    Key k = {0, 0, 0, 0, 0};
-    if (need) k = load_key(a, cidx[j], ep);
-    uint32_t slot = kNone;
-    uint64_t pend = __ballot(need);
-    while (pend) {  // one insert per distinct key in the wave, by its lowest lane
-        const uint32_t L = (uint32_t)__builtin_ctzll(pend);
-        Key r;
-        r.ep = rdl(k.ep, L);
-        r.conv = rdl(k.conv, L);
-        r.dst = rdl(k.dst, L);
-        r.id = (uint64_t)rdl((uint32_t)k.id, L) | ((uint64_t)rdl((uint32_t)(k.id >> 32), L) << 32);
-        r.ck = (uint64_t)rdl((uint32_t)k.ck, L) | ((uint64_t)rdl((uint32_t)(k.ck >> 32), L) << 32);
-        const uint64_t same = __ballot(need && key_eq(k, r)) & pend;
-        uint32_t h = 0;
-        if (lane == L) {
-            h = key_hash(r, mask);
-            for (;;) {
-                uint32_t o = __hip_atomic_load(owner + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (o == kNone) {
-                    o = atomicCAS(owner + h, kNone, j);
-                    if (o == kNone) break;
-                }
-                if (key_eq(load_key(a, cidx[o], cep[o]), r)) break;
-                h = (h + 1u) & mask;
-            }
-            if (__hip_atomic_load(tmin + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > j) atomicMin(tmin + h, j);
+// Global table probe: a slot is one u64, fingerprint (hash bits 32..63) << 32 | the compacted index
+// of the packet that claimed it; a slot with another fingerprint is skipped without touching that
+// packet's fields, a matching fingerprint is confirmed on the full key.
+__device__ __forceinline__ uint32_t global_probe(const DmIn &a, const uint32_t *cidx, const uint32_t *cep,
+                                                 unsigned long long *slots, uint32_t mask, const Key &k,
+                                                 uint64_t hv, uint32_t j) {
+    const uint32_t fp = (uint32_t)(hv >> 32);
+    const unsigned long long mine = ((unsigned long long)fp << 32) | j;
+    uint32_t h = (uint32_t)hv & mask;
+    for (;;) {
+        unsigned long long e = __hip_atomic_load(slots + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (e == ~0ull) {
+            e = atomicCAS(slots + h, ~0ull, mine);
+            if (e == ~0ull) return h;  // claimed
         }
-        h = rdl(h, L);
-        if ((same >> lane) & 1ull) slot = h;
-        pend &= ~same;
+        if ((uint32_t)(e >> 32) == fp) {
+            const uint32_t o = (uint32_t)e;
+            if (key_eq(load_key(a, cidx[o], cep[o]), k)) return h;
+        }
+        h = (h + 1u) & mask;
     }
-    if (active) hslot[j] = slot;
+}
+
+// One block = kInsTile consecutive compacted packets.  Phase 1 groups them by key in an LDS table
+// (same fingerprint scheme, confirmed on the full key) and takes each key's block-minimum index
+// with LDS atomics; phase 2: that minimum packet alone probes the global table and lowers tmin,
+// so a hot key costs one global atomic per block, not one per packet (a single hot word takes
+// ~88 atomics/us: MI355X_MICROARCH.md, dequeue row); phase 3 hands every packet its key's slot.
+constexpr uint32_t kInsItems = 4;
+constexpr uint32_t kInsTile = kBlock * kInsItems;  // 1024 packets (24 KB LDS: 6 waves per SIMD)
+constexpr uint32_t kLtab = 2 * kInsTile;           // LDS table slots (power of 2)
+
+__global__ __launch_bounds__(kBlock) void k_dm_insert(DmIn a, const uint32_t *nvp, const uint32_t *cidx,
+                                                      const uint32_t *cep, unsigned long long *slots,
+                                                      uint32_t *tmin, uint32_t mask, uint32_t *hslot) {
+    __shared__ unsigned long long ltab[kLtab];
+    __shared__ uint32_t lmin[kLtab];  // block-minimum index per key, then (phase 2b) the key's global slot
+    const uint32_t nv = *nvp;
+    const uint32_t base = blockIdx.x * kInsTile, t = threadIdx.x;
+    if (base >= nv) return;  // block-uniform
+    for (uint32_t q = t; q < kLtab; q += kBlock) {
+        ltab[q] = ~0ull;
+        lmin[q] = kNone;
+    }
+    __syncthreads();
+    uint32_t lpos[kInsItems];
+#pragma unroll
+    for (uint32_t it = 0; it < kInsItems; ++it) {
+        const uint32_t li = it * kBlock + t, j = base + li;
+        lpos[it] = kNone;
+        if (j >= nv) continue;
+        const uint32_t ep = cep[j];
+        if (ep == kCtrl) continue;
+        const Key k = load_key(a, cidx[j], ep);
+        const uint64_t hv = key_hash(k);
+        const uint32_t fp = (uint32_t)(hv >> 32);
+        const unsigned long long mine = ((unsigned long long)fp << 32) | li;
+        uint32_t h = (uint32_t)(hv ^ (hv >> 40)) & (kLtab - 1u);
+        for (;;) {
+            unsigned long long e = ltab[h];
+            if (e == ~0ull) {
+                e = atomicCAS(&ltab[h], ~0ull, mine);
+                if (e == ~0ull) break;
+            }
+            if ((uint32_t)(e >> 32) == fp) {
+                const uint32_t jo = base + (uint32_t)e;
+                if (key_eq(load_key(a, cidx[jo], cep[jo]), k)) break;
+            }
+            h = (h + 1u) & (kLtab - 1u);
+        }
+        lpos[it] = h;
+        atomicMin(&lmin[h], j);
+    }
+    __syncthreads();
+    uint32_t rep = 0;  // bit it: this thread's item `it` is its key's first packet in the block
+#pragma unroll
+    for (uint32_t it = 0; it < kInsItems; ++it)
+        if (lpos[it] != kNone && lmin[lpos[it]] == base + it * kBlock + t) rep |= 1u << it;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t it = 0; it < kInsItems; ++it) {
+        if (!((rep >> it) & 1u)) continue;
+        const uint32_t j = base + it * kBlock + t;
+        const Key k = load_key(a, cidx[j], cep[j]);
+        const uint32_t gh = global_probe(a, cidx, cep, slots, mask, k, key_hash(k), j);
+        if (__hip_atomic_load(tmin + gh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > j) atomicMin(tmin + gh, j);
+        lmin[lpos[it]] = gh;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t it = 0; it < kInsItems; ++it) {
+        const uint32_t j = base + it * kBlock + t;
+        if (j < nv) hslot[j] = lpos[it] == kNone ? kNone : lmin[lpos[it]];
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void k_dm_leader(const uint32_t *nvp, const uint32_t *hslot, const uint32_t *tmin,
@@ -275,11 +324,12 @@ __global__ __launch_bounds__(kBlock) void k_dm_rank(const uint32_t *nvp, const u
 }
 
 __global__ __launch_bounds__(kBlock) void k_dm_segof(const uint32_t *nvp, const uint32_t *lead_of,
-                                                     const uint32_t *rank_at, uint32_t *keys, uint32_t *vals) {
+                                                     const uint32_t *rank_at, const uint32_t *cidx, uint32_t *keys,
+                                                     uint32_t *vals) {
     const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
     if (j >= *nvp) return;
     keys[j] = rank_at[lead_of[j]];
-    vals[j] = j;
+    vals[j] = cidx[j];  // the packet index rides through the sort
 }
 
 // ---- stable LSD radix sort by segment id ------------------------------------------------------
@@ -368,7 +418,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_scatter(uint32_t pass, const uint
 
 __global__ __launch_bounds__(kBlock) void k_dm_final(const uint32_t *nvp, const uint32_t *nsegp, const uint32_t *kA,
                                                      const uint32_t *vA, const uint32_t *kB, const uint32_t *vB,
-                                                     const uint32_t *cidx, uint32_t *perm, uint32_t *seg_off,
+                                                     uint32_t *perm, uint32_t *seg_off,
                                                      uint32_t *n_seg, uint32_t *n_valid) {
     const uint32_t nv = *nvp, ns = *nsegp;
     const uint32_t passes = (bits_for(ns) + 7u) / 8u;  // effective passes; pass p writes B when p is even
@@ -382,7 +432,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_final(const uint32_t *nvp, const 
         seg_off[ns] = nv;
     }
     if (k >= nv) return;
-    perm[k] = cidx[vals[k]];
+    perm[k] = vals[k];
     const uint32_t key = keys[k];
     if (k == 0 || keys[k - 1] != key) seg_off[key] = k;
 }
@@ -393,7 +443,8 @@ struct DmWs {
     uint32_t *cv, *ov, *cc, *oc, *cl, *ol;
     uint32_t *cidx, *cep, *hslot, *lead_of, *rank_at;
     uint32_t *kA, *vA, *kB, *vB;
-    uint32_t *owner, *tmin;
+    unsigned long long *slots;
+    uint32_t *tmin;
     uint32_t *hist, *hoff;
     uint32_t *nv, *nseg;
     ScanWs scan;
@@ -434,7 +485,7 @@ size_t dm_layout(uint32_t n, uint8_t *base, DmWs *w) {
     d.vA = (uint32_t *)take(4ull * n);
     d.kB = (uint32_t *)take(4ull * n);
     d.vB = (uint32_t *)take(4ull * n);
-    d.owner = (uint32_t *)take(4ull * T);
+    d.slots = (unsigned long long *)take(8ull * T);
     d.tmin = (uint32_t *)take(4ull * T);
     d.hist = (uint32_t *)take(4ull * nh);
     d.hoff = (uint32_t *)take(4ull * nh);
@@ -501,7 +552,7 @@ extern "C" int rsk_demux_batch(rsk_ctx *c, uint32_t n, const rsk_demux_in *in, u
     a.dst = in->dst;
     a.n = n;
     a.fields = fields;
-    hipError_t e = hipMemsetAsync(w.owner, 0xff, 8ull * w.tsize, s);  // owner + tmin (adjacent)
+    hipError_t e = hipMemsetAsync(w.slots, 0xff, 12ull * w.tsize, s);  // slots + tmin (adjacent)
     if (e != hipSuccess) { rsk::set_error("hipMemsetAsync(table)", e); return RSK_EDEVICE; }
     const uint32_t nb = w.nb;
     hipLaunchKernelGGL(k_dm_flags, dim3(nb), dim3(kBlock), 0, s, a, w.mv, w.cv, w.mc, w.cc);
@@ -509,13 +560,13 @@ extern "C" int rsk_demux_batch(rsk_ctx *c, uint32_t n, const rsk_demux_in *in, u
     if ((r = scan_u32(w.cv, w.ov, nb, w.nv, w.scan, s))) return r;
     if ((r = scan_u32(w.cc, w.oc, nb, nullptr, w.scan, s))) return r;
     hipLaunchKernelGGL(k_dm_prep, dim3(nb), dim3(kBlock), 0, s, a, w.mv, w.ov, w.mc, w.oc, w.cidx, w.cep);
-    hipLaunchKernelGGL(k_dm_insert, dim3(nb), dim3(kBlock), 0, s, a, w.nv, w.cidx, w.cep, w.owner, w.tmin,
-                       w.tsize - 1u, w.hslot);
+    hipLaunchKernelGGL(k_dm_insert, dim3((n + kInsTile - 1) / kInsTile), dim3(kBlock), 0, s, a, w.nv, w.cidx,
+                       w.cep, w.slots, w.tmin, w.tsize - 1u, w.hslot);
     hipLaunchKernelGGL(k_dm_leader, dim3(nb), dim3(kBlock), 0, s, w.nv, w.hslot, w.tmin, w.lead_of, w.ml, w.cl);
     if ((r = rsk::launch_check("k_dm_leader"))) return r;
     if ((r = scan_u32(w.cl, w.ol, nb, w.nseg, w.scan, s))) return r;
     hipLaunchKernelGGL(k_dm_rank, dim3(nb), dim3(kBlock), 0, s, w.nv, w.ml, w.ol, w.cidx, w.rank_at, out->seg_first);
-    hipLaunchKernelGGL(k_dm_segof, dim3(nb), dim3(kBlock), 0, s, w.nv, w.lead_of, w.rank_at, w.kA, w.vA);
+    hipLaunchKernelGGL(k_dm_segof, dim3(nb), dim3(kBlock), 0, s, w.nv, w.lead_of, w.rank_at, w.cidx, w.kA, w.vA);
     if ((r = rsk::launch_check("k_dm_segof"))) return r;
     // passes for the worst case (every packet its own segment); surplus passes return at once
     uint32_t maxbits = 1;
@@ -530,7 +581,7 @@ extern "C" int rsk_demux_batch(rsk_ctx *c, uint32_t n, const rsk_demux_in *in, u
                            kout, vout);
         if ((r = rsk::launch_check("k_dm_scatter"))) return r;
     }
-    hipLaunchKernelGGL(k_dm_final, dim3(nb), dim3(kBlock), 0, s, w.nv, w.nseg, w.kA, w.vA, w.kB, w.vB, w.cidx,
+    hipLaunchKernelGGL(k_dm_final, dim3(nb), dim3(kBlock), 0, s, w.nv, w.nseg, w.kA, w.vA, w.kB, w.vB,
                        out->perm, out->seg_off, out->n_seg, out->n_valid);
     return rsk::launch_check("k_dm_final");
 }

@@ -72,10 +72,30 @@ def main():
         "decode": lambda: cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, w.dec, stream=s),
         "parse_decode": lambda: cx.rawinput_batch(wiree, offe, ste, ste, 1, 0, tcp, pdec, stream=s),
     }
-    for f in ops.values():
+    # receive demux on the decoded fields (frames of this config; C4 marks 1/16 corrupted, 5% control)
+    w.corrupt_frames()
+    dmx = rc.DemuxBuffers.alloc(n, dev)
+    dfields = rc._abi.DEMUX_ID | rc._abi.DEMUX_CONN_KEY | rc._abi.DEMUX_CMD_BARRIER
+    ops["demux"] = lambda: cx.demux_batch(w.dec.status, w.dec.cmd, dfields, dmx, id=w.dec.id, conv=w.dec.conv,
+                                          conn_key=w.dec.conn_key, stream=s)
+    # realistic connection counts: 64 conns, 0.1% control packets, every packet VALID
+    gk = torch.Generator(device=dev)
+    gk.manual_seed(7)
+    k_st = torch.ones(n, dtype=torch.int8, device=dev)
+    k_cmd = (torch.rand(n, device=dev, generator=gk) < 0.001).to(torch.uint8) * 3
+    k_key = torch.randint(0, 64, (n,), device=dev, generator=gk, dtype=torch.int64) * 0x10001 + 0x10000000
+    k_id = torch.zeros(n * 8, dtype=torch.uint8, device=dev)
+    dmx64 = rc.DemuxBuffers.alloc(n, dev)
+    ops["demux_64conn"] = lambda: cx.demux_batch(k_st, k_cmd, dfields, dmx64, id=k_id, conn_key=k_key, stream=s)
+    for k, f in ops.items():
+        if k == "demux":
+            cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, w.dec, stream=s)
         f()
     torch.cuda.synchronize()
     assert bool((pdec.status == 1).all()) and int(pdec.n_valid.item()) == n
+    ops.pop("decode")  # decode now sees the corrupted frames; time it on them too
+    ops["decode"] = lambda: cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, w.dec, stream=s)
+    nseg = [int(dmx.n_seg.item()), int(dmx64.n_seg.item())]
     times = {k: [] for k in ops}
     for _ in range(args.rounds):
         for k, f in ops.items():
@@ -96,12 +116,15 @@ def main():
         "encode_wire_raw4_hyb1": 2 * p + 66 + 40 + 23,
         "decode": 73,
         "parse_decode": 54 + 32 + 16 + 21 + 4 + 73 - 42,
+        "demux": 1 + 1 + 8 + 8 + 4,  # status, cmd, id, conn_key in; perm out (+ per-segment words)
+        "demux_64conn": 1 + 1 + 8 + 8 + 4,
     }
     out = {}
     for k, t in times.items():
         m = float(np.median(t))
         out[k] = {"ms": round(m, 4), "Mpkt_s": round(n / m / 1e3, 1), "GBps_alg": round(n * alg[k] / m / 1e6, 1)}
-    print(json.dumps({"config": args.config, "packets": n, "wire_pitch": [p4, pe], "paths": out}))
+    print(json.dumps({"config": args.config, "packets": n, "wire_pitch": [p4, pe], "demux_segments": nseg,
+                      "paths": out}))
 
 
 if __name__ == "__main__":
