@@ -159,7 +159,12 @@ int rsk_encode_batch(rsk_ctx *ctx, uint32_t n, const rsk_encode_in *in, const rs
  * [eth 14 if with_eth] | IPv4 20 | TCP 20 | tag 8 | EncHead 23 | payload, with the IPv4 header checksum
  * and the TCP checksum (RFC 793 pseudo-header, RFC 1071 sum over header + frame) filled in.
  * status[i] = wire length (14? + 40 + 31 + P), RSK_SEND_OVERSIZE or RSK_SEND_RESET as for
- * rsk_encode_batch; out->flags as there (padding counts from the end of the wire packet). */
+ * rsk_encode_batch; out->flags as there (padding counts from the end of the wire packet).  The value
+ * RConn::Output returns for a sent frame is SendRawTcp's `payload_len` (RawTcp.cpp:340), i.e. the
+ * frame length status[i] - 40 - (with_eth ? 14 : 0).  seq and ip_id are the caller's per-packet
+ * values: the reference advances them per send (FakeTcp::Output: seq += 31 + nread, FakeTcp.cpp:43-49;
+ * RawTcp::Output: mIpId++, RawTcp.cpp:118-120), so one connection's batch carries
+ * seq[i] = seq0 + sum_{k<i} (31 + P_k) and ip_id[i] = id0 + i. */
 typedef struct rsk_wire_in {
     const uint32_t *src, *dst; /* [n] TcpInfo::src / dst: IPv4 addresses as stored (network order) */
     const uint16_t *sp, *dp;   /* [n] ports, host order                                           */
