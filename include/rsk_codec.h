@@ -19,6 +19,9 @@
  *   rsk_tcpinfo_encode_batch <- char* TcpInfo::Encode(char*, int) (21-B hand-off record)      bean/TcpInfo.cpp:20-32, bean/ConnInfo.cpp:12-20
  *   rsk_encode_wire_batch <- RConn::Output + RawTcp::SendRawTcp -> libnet_build_tcp/ipv4     conn/RawTcp.cpp:280-341
  *   rsk_key_for_tcp/udp   <- KeyGenerator::KeyForTcp / KeyForUdp                              src/util/KeyGenerator.cpp:16-36
+ *   rsk_capture_filter_batch <- the pcap filter RCap installs: BuildFilterStr("tcp", srcIp, dstIp, srcPorts,
+ *                            dstPorts, isServer) (cap/cap_util.cpp:67-144, cap/RCap.cpp:64-88) evaluated
+ *                            per captured packet; rsk_filter_str renders the same string
  *   rsk_demux_batch       <- the per-packet conn lookups of the receive path, batched:
  *                            INetGroup::Input by connKey (conn/INetGroup.cpp:57-83), IAppGroup::Input
  *                            by cmd (conn/IAppGroup.cpp:76-96), ServerGroup::OnRecv by IdBuf
@@ -259,6 +262,46 @@ typedef struct rsk_demux_out {
 } rsk_demux_out;
 int rsk_demux_batch(rsk_ctx *ctx, uint32_t n, const rsk_demux_in *in, uint32_t fields,
                     const rsk_demux_out *out, void *stream);
+
+/* ---- capture filter ------------------------------------------------------- */
+/* RCap::doInit (cap/RCap.cpp:64-88) compiles BuildFilterStr("tcp", srcIp, dstIp, srcPorts, dstPorts,
+ * isServer) (cap/cap_util.cpp:67-144) into the kernel's BPF filter.  For a client that string is
+ *   F  = tcp [and (ip src S)] [and (ip dst D)] [and ( src port p or ... src portrange a-b ... )]
+ *        [and ( dst port p or ... dst portrange a-b ... )]
+ * and for a server  ((tcp[tcpflags] & tcp-syn != 0) and F') or (F and (tcp[tcpflags] & (tcp-syn) == 0))
+ * where F' is F with every "dst" replaced by "src".  rsk_capture_filter_batch evaluates that
+ * predicate with libpcap's meaning of each primitive:
+ *   tcp          IPv4 with protocol 6, or IPv6 with next header 6 (directly, or after a fragment
+ *                header, 44);
+ *   ip src/dst   IPv4 only, the address field equals S / D;
+ *   [src|dst] port / portrange   IPv4 with protocol 6, 17 or 132 and fragment offset 0, or IPv6
+ *                with next header 6, 17 or 132; the port field (at 4 * IHL on IPv4, 40 on IPv6)
+ *                equals p / lies in [a, b];
+ *   tcp[tcpflags]  IPv4 with protocol 6 and fragment offset 0: TCP header byte 13.
+ * Link layer: DLT_EN10MB ethertype 0x0800 / 0x86dd at bytes 12-13; DLT_NULL a 4-byte family in
+ * host order, 2 = IPv4, 24 / 28 / 30 = IPv6 (BSD values).  Evaluation is left to right with
+ * short-circuit; a field read past cap_len rejects the packet (as a BPF load out of bounds does).
+ * match[i] = 1 / 0; match_idx / n_match (optional, may be NULL) list the matches in order. */
+#define RSK_FILTER_MAX_PORTS 64
+typedef struct rsk_port_list {
+    uint16_t n_single, n_range;            /* RPortList::GetSinglePortList / GetPortRangeList sizes */
+    uint16_t single[RSK_FILTER_MAX_PORTS]; /* in list order                                        */
+    uint16_t range[RSK_FILTER_MAX_PORTS][2]; /* [source, dest], source < dest (RPortList.cpp:21-27) */
+} rsk_port_list;
+typedef struct rsk_capture_filter {
+    uint32_t src_ip, dst_ip;  /* IPv4 as stored in the header (network-order bytes read LE)        */
+    uint8_t has_src_ip;       /* srcIp non-empty                                                  */
+    uint8_t has_dst_ip;       /* dstIp non-empty                                                  */
+    uint8_t is_server;
+    uint8_t reserved;         /* 0                                                                */
+    rsk_port_list src_ports, dst_ports;
+} rsk_capture_filter;
+int rsk_capture_filter_batch(rsk_ctx *ctx, uint32_t n, const uint8_t *cap_arena, const uint64_t *cap_off,
+                             const uint32_t *cap_len, int datalink, const rsk_capture_filter *filter,
+                             uint8_t *match, uint32_t *match_idx, uint32_t *n_match, void *stream);
+/* Host: the exact string BuildFilterStr returns for this filter (proto "tcp", addresses dotted),
+ * NUL-terminated into buf.  Returns its length, or -1 if buf_len is too small. */
+int rsk_filter_str(const rsk_capture_filter *filter, char *buf, size_t buf_len);
 
 /* ---- single-packet shims with the reference signatures (host pointers) ----------------------- */
 /* These run the same HIP kernels on a batch of one (device round trip, synchronous), so a caller

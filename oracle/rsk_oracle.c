@@ -8,6 +8,7 @@
 #include "rsk_oracle.h"
 
 #include <pthread.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -635,4 +636,201 @@ int orc_demux_batch(uint32_t n, const int8_t *status, const uint8_t *cmd, const 
     *n_valid = nv;
     free(tab); free(seg_of); free(cnt);
     return 0;
+}
+
+/* ---- capture filter ----------------------------------------------------------- */
+/* Each primitive returns 1 / 0, or -1 when a byte it reads lies past cap_len (the BPF program then
+ * returns 0 for the packet: libpcap bpf_filter's out-of-bounds load). */
+typedef struct orc_fpkt {
+    const uint8_t *p;
+    uint32_t cl;
+    uint32_t L;   /* link header bytes: 14 (EN10MB) or 4 (NULL) */
+    int datalink;
+} orc_fpkt;
+
+static int orc_f_link(const orc_fpkt *k) {  /* 4, 6, 0 or -1 */
+    if (k->datalink == RSK_DLT_EN10MB) {
+        if (k->cl < 14) return -1;
+        const unsigned et = ((unsigned)k->p[12] << 8) | k->p[13];
+        return et == 0x0800 ? 4 : et == 0x86dd ? 6 : 0;
+    }
+    if (k->cl < 4) return -1;
+    const uint32_t fam = (uint32_t)k->p[0] | (uint32_t)k->p[1] << 8 | (uint32_t)k->p[2] << 16 | (uint32_t)k->p[3] << 24;
+    return fam == 2 ? 4 : (fam == 24 || fam == 28 || fam == 30) ? 6 : 0;
+}
+
+static int orc_f_tcp(const orc_fpkt *k) {  /* "tcp" */
+    const int lt = orc_f_link(k);
+    if (lt < 0) return -1;
+    if (lt == 4) {
+        if (k->cl < k->L + 10) return -1;
+        return k->p[k->L + 9] == 6;
+    }
+    if (lt == 6) {
+        if (k->cl < k->L + 7) return -1;
+        const uint8_t nxt = k->p[k->L + 6];
+        if (nxt == 6) return 1;
+        if (nxt != 44) return 0;
+        if (k->cl < k->L + 41) return -1;
+        return k->p[k->L + 40] == 6;
+    }
+    return 0;
+}
+
+static int orc_f_addr(const orc_fpkt *k, uint32_t off, uint32_t val) {  /* "ip src|dst A" */
+    const int lt = orc_f_link(k);
+    if (lt < 0) return -1;
+    if (lt != 4) return 0;
+    if (k->cl < k->L + off + 4) return -1;
+    const uint8_t *q = k->p + k->L + off;
+    return ((uint32_t)q[0] | (uint32_t)q[1] << 8 | (uint32_t)q[2] << 16 | (uint32_t)q[3] << 24) == val;
+}
+
+static int orc_is_tus(uint8_t pr) { return pr == 6 || pr == 17 || pr == 132; }
+
+/* "( [src|dst] port p or ... [src|dst] portrange a-b ... )"; dir = 0 (src) or 2 (dst) */
+static int orc_f_ports(const orc_fpkt *k, const rsk_port_list *pl, uint32_t dir) {
+    if (pl->n_single == 0 && pl->n_range == 0) return 1;  /* no clause */
+    const int lt = orc_f_link(k);
+    if (lt < 0) return -1;
+    int have = 0;
+    unsigned port = 0;
+    if (lt == 4) {
+        if (k->cl < k->L + 10) return -1;
+        if (orc_is_tus(k->p[k->L + 9])) {
+            const unsigned frag = ((unsigned)(k->p[k->L + 6] & 0x1f) << 8) | k->p[k->L + 7];
+            if (frag == 0) {
+                const uint32_t th = k->L + 4u * (k->p[k->L] & 15u);
+                if (k->cl < th + dir + 2) return -1;
+                port = ((unsigned)k->p[th + dir] << 8) | k->p[th + dir + 1];
+                have = 1;
+            }
+        }
+    } else if (lt == 6) {
+        if (k->cl < k->L + 7) return -1;
+        if (orc_is_tus(k->p[k->L + 6])) {
+            const uint32_t th = k->L + 40;
+            if (k->cl < th + dir + 2) return -1;
+            port = ((unsigned)k->p[th + dir] << 8) | k->p[th + dir + 1];
+            have = 1;
+        }
+    }
+    if (!have) return 0;
+    for (unsigned q = 0; q < pl->n_single; q++)
+        if (port == pl->single[q]) return 1;
+    for (unsigned q = 0; q < pl->n_range; q++)
+        if (port >= pl->range[q][0] && port <= pl->range[q][1]) return 1;
+    return 0;
+}
+
+static int orc_f_syn(const orc_fpkt *k, int want_set) {  /* tcp[tcpflags] & tcp-syn != 0 / == 0 */
+    const int lt = orc_f_link(k);
+    if (lt < 0) return -1;
+    if (lt != 4) return 0;
+    if (k->cl < k->L + 10) return -1;
+    if (k->p[k->L + 9] != 6) return 0;
+    const unsigned frag = ((unsigned)(k->p[k->L + 6] & 0x1f) << 8) | k->p[k->L + 7];
+    if (frag != 0) return 0;
+    const uint32_t th = k->L + 4u * (k->p[k->L] & 15u);
+    if (k->cl < th + 14) return -1;
+    const int syn = (k->p[th + 13] & 0x02) != 0;
+    return want_set ? syn : !syn;
+}
+
+/* F (primed = 0) or F' ("dst" -> "src", primed = 1), left to right with short-circuit */
+static int orc_f_main(const orc_fpkt *k, const rsk_capture_filter *f, int primed) {
+    int r = orc_f_tcp(k);
+    if (r != 1) return r;
+    if (f->has_src_ip && (r = orc_f_addr(k, 12, f->src_ip)) != 1) return r;
+    if (f->has_dst_ip && (r = orc_f_addr(k, primed ? 12 : 16, f->dst_ip)) != 1) return r;
+    if ((r = orc_f_ports(k, &f->src_ports, 0)) != 1) return r;
+    return orc_f_ports(k, &f->dst_ports, primed ? 0 : 2);
+}
+
+int orc_capture_filter(const uint8_t *pkt, uint32_t cap_len, int datalink, const rsk_capture_filter *f) {
+    orc_fpkt k = {pkt, cap_len, datalink == RSK_DLT_EN10MB ? 14u : 4u, datalink};
+    int r;
+    if (!f->is_server) {
+        r = orc_f_main(&k, f, 0);
+    } else {  /* ((syn) and F') or (F and (no syn)) */
+        r = orc_f_syn(&k, 1);
+        if (r == 1) r = orc_f_main(&k, f, 1);
+        if (r == 0) {
+            r = orc_f_main(&k, f, 0);
+            if (r == 1) r = orc_f_syn(&k, 0);
+        }
+    }
+    return r == 1;
+}
+
+/* BuildFilterStr (cap/cap_util.cpp:67-144) */
+static size_t orc_put(char *buf, size_t cap, size_t at, const char *s) {
+    size_t n = strlen(s);
+    if (at + n < cap) memcpy(buf + at, s, n + 1);
+    return at + n;
+}
+
+static size_t orc_put_ports(char *buf, size_t cap, size_t at, const rsk_port_list *pl, const char *dir) {
+    if (pl->n_single == 0 && pl->n_range == 0) return at;
+    char tmp[64];
+    at = orc_put(buf, cap, at, " and ");
+    at = orc_put(buf, cap, at, "(");
+    int first = 1;  /* the reference deletes the first "or" (cap_util.cpp:116-121) */
+    for (unsigned q = 0; q < pl->n_single; q++, first = 0) {
+        snprintf(tmp, sizeof tmp, " %s %s port %u", first ? "" : "or", dir, (unsigned)pl->single[q]);
+        at = orc_put(buf, cap, at, tmp);
+    }
+    for (unsigned q = 0; q < pl->n_range; q++, first = 0) {
+        snprintf(tmp, sizeof tmp, " %s %s portrange %u-%u", first ? "" : "or", dir, (unsigned)pl->range[q][0],
+                 (unsigned)pl->range[q][1]);
+        at = orc_put(buf, cap, at, tmp);
+    }
+    return orc_put(buf, cap, at, " )");
+}
+
+static size_t orc_base_str(const rsk_capture_filter *f, char *buf, size_t cap) {
+    char ip[40];
+    size_t at = orc_put(buf, cap, 0, "tcp");
+    if (f->has_src_ip) {
+        snprintf(ip, sizeof ip, " and  (ip src %u.%u.%u.%u)", f->src_ip & 255, (f->src_ip >> 8) & 255,
+                 (f->src_ip >> 16) & 255, f->src_ip >> 24);
+        at = orc_put(buf, cap, at, ip);
+    }
+    if (f->has_dst_ip) {
+        snprintf(ip, sizeof ip, " and  (ip dst %u.%u.%u.%u)", f->dst_ip & 255, (f->dst_ip >> 8) & 255,
+                 (f->dst_ip >> 16) & 255, f->dst_ip >> 24);
+        at = orc_put(buf, cap, at, ip);
+    }
+    at = orc_put_ports(buf, cap, at, &f->src_ports, "src");
+    return orc_put_ports(buf, cap, at, &f->dst_ports, "dst");
+}
+
+int orc_filter_str(const rsk_capture_filter *f, char *buf, size_t buf_len) {
+    char base[8192];
+    const size_t bl = orc_base_str(f, base, sizeof base);
+    if (bl >= sizeof base) return -1;
+    if (!f->is_server) {
+        if (bl + 1 > buf_len) return -1;
+        memcpy(buf, base, bl + 1);
+        return (int)bl;
+    }
+    char primed[8192];
+    size_t o = 0;
+    for (size_t q = 0; q < bl;) {  /* every "dst" -> "src" */
+        if (q + 3 <= bl && memcmp(base + q, "dst", 3) == 0) {
+            memcpy(primed + o, "src", 3);
+            o += 3;
+            q += 3;
+        } else {
+            primed[o++] = base[q++];
+        }
+    }
+    primed[o] = 0;
+    size_t at = orc_put(buf, buf_len, 0, "((tcp[tcpflags] & tcp-syn != 0) and ");
+    at = orc_put(buf, buf_len, at, primed);
+    at = orc_put(buf, buf_len, at, ") or (");
+    at = orc_put(buf, buf_len, at, base);
+    at = orc_put(buf, buf_len, at, "and (tcp[tcpflags] & (tcp-syn) == 0))");
+    if (at + 1 > buf_len) return -1;
+    return (int)at;
 }

@@ -22,6 +22,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "../include/rsk_codec.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -97,6 +99,13 @@ int orc_demux_batch(uint32_t n, const int8_t *status, const uint8_t *cmd, const 
                     const uint32_t *conv, const uint64_t *conn_key, const uint32_t *dst,
                     uint32_t fields, uint32_t *perm, uint32_t *seg_off, uint32_t *seg_first,
                     uint32_t *n_seg, uint32_t *n_valid);
+
+/* Capture filter (semantics in include/rsk_codec.h rsk_capture_filter_batch): the
+ * pcap filter BuildFilterStr (cap/cap_util.cpp:67-144) builds, evaluated on one captured packet
+ * with libpcap's meaning of each primitive.  Returns 1 (match) or 0. */
+int orc_capture_filter(const uint8_t *pkt, uint32_t cap_len, int datalink, const rsk_capture_filter *f);
+/* BuildFilterStr("tcp", srcIp, dstIp, srcPorts, dstPorts, isServer) for this filter. */
+int orc_filter_str(const rsk_capture_filter *f, char *buf, size_t buf_len);
 
 /* KeyGenerator::KeyForTcp / KeyForUdp (src/util/KeyGenerator.cpp:16-36) */
 uint64_t orc_key_for_tcp(uint16_t sp, uint16_t dp);

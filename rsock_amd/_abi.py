@@ -30,6 +30,7 @@ SEND_OVERSIZE, SEND_RESET = -1, 0
 RECV_VALID, RECV_CLOSE, RECV_DROP = 1, 0, -1
 PARSE_DROP, PARSE_DELIVER, PARSE_SYN, PARSE_MALFORMED = 0, 1, 2, 3
 PARSE_HAS_ACK_POOL, PARSE_IS_SERVER = 0x1, 0x2
+FILTER_MAX_PORTS = 64
 DEMUX_ID, DEMUX_CONN_KEY, DEMUX_CONV, DEMUX_DST, DEMUX_CMD_BARRIER = 0x01, 0x02, 0x04, 0x08, 0x10
 
 _vp = ctypes.c_void_p
@@ -102,6 +103,17 @@ class DemuxOut(ctypes.Structure):
     _fields_ = [("perm", _vp), ("seg_off", _vp), ("seg_first", _vp), ("n_seg", _vp), ("n_valid", _vp)]
 
 
+class PortList(ctypes.Structure):
+    _fields_ = [("n_single", ctypes.c_uint16), ("n_range", ctypes.c_uint16),
+                ("single", ctypes.c_uint16 * FILTER_MAX_PORTS), ("range", (ctypes.c_uint16 * 2) * FILTER_MAX_PORTS)]
+
+
+class CaptureFilter(ctypes.Structure):
+    _fields_ = [("src_ip", ctypes.c_uint32), ("dst_ip", ctypes.c_uint32), ("has_src_ip", ctypes.c_uint8),
+                ("has_dst_ip", ctypes.c_uint8), ("is_server", ctypes.c_uint8), ("reserved", ctypes.c_uint8),
+                ("src_ports", PortList), ("dst_ports", PortList)]
+
+
 # (name, restype, argtypes) for every symbol the header declares
 SIGNATURES = [
     ("rsk_create", _vp, [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_int]),
@@ -120,6 +132,9 @@ SIGNATURES = [
       ctypes.POINTER(TcpInfoOut), ctypes.POINTER(DecodeOut), _vp]),
     ("rsk_tcpinfo_encode_batch", ctypes.c_int,
      [_vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("rsk_capture_filter_batch", ctypes.c_int,
+     [_vp, ctypes.c_uint32, _vp, _vp, _vp, ctypes.c_int, ctypes.POINTER(CaptureFilter), _vp, _vp, _vp, _vp]),
+    ("rsk_filter_str", ctypes.c_int, [ctypes.POINTER(CaptureFilter), ctypes.c_char_p, ctypes.c_size_t]),
     ("rsk_demux_batch", ctypes.c_int,
      [_vp, ctypes.c_uint32, ctypes.POINTER(DemuxIn), ctypes.c_uint32, ctypes.POINTER(DemuxOut), _vp]),
     ("rsk_compute_hash", _vp, [_vp, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]),

@@ -97,6 +97,40 @@ class DecodeBuffers:
         return out
 
 
+def ip_u32(ip: str) -> int:
+    """Dotted IPv4 -> the u32 the header stores (network-order bytes read little-endian)."""
+    b = bytes(int(x) for x in ip.split("."))
+    return int.from_bytes(b, "little")
+
+
+def make_filter(src_ip: str | None = None, dst_ip: str | None = None, src_singles=(), src_ranges=(), dst_singles=(),
+                dst_ranges=(), is_server: bool = False) -> _abi.CaptureFilter:
+    """rsk_capture_filter from BuildFilterStr's inputs (srcIp, dstIp, srcPorts, dstPorts, isServer)."""
+    f = _abi.CaptureFilter()
+    if src_ip:
+        f.src_ip, f.has_src_ip = ip_u32(src_ip), 1
+    if dst_ip:
+        f.dst_ip, f.has_dst_ip = ip_u32(dst_ip), 1
+    f.is_server = 1 if is_server else 0
+    for pl, singles, ranges in ((f.src_ports, src_singles, src_ranges), (f.dst_ports, dst_singles, dst_ranges)):
+        assert len(singles) <= _abi.FILTER_MAX_PORTS and len(ranges) <= _abi.FILTER_MAX_PORTS
+        pl.n_single, pl.n_range = len(singles), len(ranges)
+        for q, v in enumerate(singles):
+            pl.single[q] = v
+        for q, (a, b) in enumerate(ranges):
+            pl.range[q][0], pl.range[q][1] = a, b
+    return f
+
+
+def filter_str(filt: _abi.CaptureFilter) -> str:
+    """BuildFilterStr's string for this filter (host function of librsk; no GPU needed)."""
+    buf = ctypes.create_string_buffer(16384)
+    n = lib().rsk_filter_str(ctypes.byref(filt), buf, len(buf))
+    if n < 0:
+        raise RskError("rsk_filter_str: buffer too small")
+    return buf.value.decode()
+
+
 @dataclass
 class DemuxBuffers:
     """Outputs of rsk_demux_batch for a batch of n packets (rsk_demux_out)."""
@@ -250,6 +284,14 @@ class Codec:
         _check(lib().rsk_tcpinfo_encode_batch(self._ctx, n, _ptr(src), _ptr(dst), _ptr(sp), _ptr(dp),
                                               _ptr(seq), _ptr(ack), _ptr(flag), _ptr(rec),
                                               _stream(stream)), "rsk_tcpinfo_encode_batch")
+
+    def capture_filter_batch(self, cap, cap_off, cap_len, datalink: int, filt: "_abi.CaptureFilter", match,
+                             match_idx=None, n_match=None, stream=None) -> None:
+        """The capture filter RCap installs (rsk_capture_filter_batch) over a batch."""
+        n = cap_off.numel()
+        _check(lib().rsk_capture_filter_batch(self._ctx, n, _ptr(cap), _ptr(cap_off), _ptr(cap_len), datalink,
+                                              ctypes.byref(filt), _ptr(match), _ptr(match_idx), _ptr(n_match),
+                                              _stream(stream)), "rsk_capture_filter_batch")
 
     def demux_batch(self, status, cmd, fields: int, out: "DemuxBuffers", id=None, conv=None, conn_key=None,
                     dst=None, stream=None) -> None:

@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <string>
 #include <vector>
 
 #include "../../include/rsk_codec.h"
@@ -1008,6 +1009,139 @@ __global__ __launch_bounds__(kBlock) void k_parse_decode(ParseArgs a, DecOut d, 
 // ---------------------------------------------------------------------------------------------
 // Exclusive scan of the per-block VALID counts -> offsets (one workgroup; 4 counts per thread per
 // pass, wave scans via DPP-backed shuffles, one LDS exchange per pass), plus the total.
+// ---------------------------------------------------------------------------------------------
+// Capture filter: the pcap predicate BuildFilterStr builds (cap/cap_util.cpp:67-144), SURVEY §8f-4
+// (primitive semantics: include/rsk_codec.h).  One lane per captured packet: a 64-B window of the
+// link + network headers and a 16-B window at the transport header, both bounded by cap_len; every
+// primitive checks the bytes it reads against cap_len and a short read rejects the packet.
+// ---------------------------------------------------------------------------------------------
+struct FiltArgs {
+    const uint8_t *cap;
+    const uint64_t *cap_off;
+    const uint32_t *cap_len;
+    uint8_t *match;
+    uint32_t n;
+};
+
+template <int L>  // link header bytes: 14 (EN10MB) or 4 (NULL)
+struct FPkt {
+    uint32_t cl;
+    uint32_t w[16];  // packet bytes [0, 64)
+    uint32_t t[4];   // transport header bytes [0, 16) (IPv4: at L + 4 IHL; IPv6: at L + 40)
+    int lt;          // 4, 6, 0; -1 = link header cut off
+    __device__ __forceinline__ uint32_t b(int k) const { return (w[k >> 2] >> (8 * (k & 3))) & 0xffu; }
+    __device__ __forceinline__ uint32_t tb(int k) const { return (t[k >> 2] >> (8 * (k & 3))) & 0xffu; }
+    __device__ __forceinline__ uint32_t ihl4() const { return 4u * (b(L) & 15u); }
+};
+
+__device__ __forceinline__ bool is_tus(uint32_t pr) { return pr == 6u || pr == 17u || pr == 132u; }
+
+template <int L>
+__device__ __forceinline__ int fp_tcp(const FPkt<L> &k) {
+    if (k.lt < 0) return -1;
+    if (k.lt == 4) return k.cl < L + 10u ? -1 : (int)(k.b(L + 9) == 6u);
+    if (k.lt == 6) {
+        if (k.cl < L + 7u) return -1;
+        const uint32_t nxt = k.b(L + 6);
+        if (nxt == 6u) return 1;
+        if (nxt != 44u) return 0;
+        return k.cl < L + 41u ? -1 : (int)(k.b(L + 40) == 6u);
+    }
+    return 0;
+}
+
+template <int L, int OFF>
+__device__ __forceinline__ int fp_addr(const FPkt<L> &k, uint32_t val) {
+    if (k.lt < 0) return -1;
+    if (k.lt != 4) return 0;
+    if (k.cl < L + OFF + 4u) return -1;
+    const uint32_t a = k.b(L + OFF) | (k.b(L + OFF + 1) << 8) | (k.b(L + OFF + 2) << 16) | (k.b(L + OFF + 3) << 24);
+    return (int)(a == val);
+}
+
+template <int L>
+__device__ __forceinline__ int fp_ports(const FPkt<L> &k, const rsk_port_list &pl, uint32_t dir) {
+    if (pl.n_single == 0 && pl.n_range == 0) return 1;
+    if (k.lt < 0) return -1;
+    uint32_t port;
+    if (k.lt == 4) {
+        if (k.cl < L + 10u) return -1;
+        if (!is_tus(k.b(L + 9)) || (((k.b(L + 6) & 0x1fu) << 8) | k.b(L + 7)) != 0u) return 0;
+        if (k.cl < L + k.ihl4() + dir + 2u) return -1;
+    } else if (k.lt == 6) {
+        if (k.cl < L + 7u) return -1;
+        if (!is_tus(k.b(L + 6))) return 0;
+        if (k.cl < L + 40u + dir + 2u) return -1;
+    } else {
+        return 0;
+    }
+    port = dir ? ((k.tb(2) << 8) | k.tb(3)) : ((k.tb(0) << 8) | k.tb(1));
+    bool hit = false;
+    for (uint32_t q = 0; q < pl.n_single; ++q) hit |= port == pl.single[q];  // uniform loop bounds
+    for (uint32_t q = 0; q < pl.n_range; ++q) hit |= port >= pl.range[q][0] && port <= pl.range[q][1];
+    return (int)hit;
+}
+
+template <int L>
+__device__ __forceinline__ int fp_syn(const FPkt<L> &k, bool want_set) {
+    if (k.lt < 0) return -1;
+    if (k.lt != 4) return 0;
+    if (k.cl < L + 10u) return -1;
+    if (k.b(L + 9) != 6u || (((k.b(L + 6) & 0x1fu) << 8) | k.b(L + 7)) != 0u) return 0;
+    if (k.cl < L + k.ihl4() + 14u) return -1;
+    const bool syn = (k.tb(13) & 2u) != 0u;
+    return (int)(want_set ? syn : !syn);
+}
+
+template <int L>
+__device__ __forceinline__ int fp_main(const FPkt<L> &k, const rsk_capture_filter &f, bool primed) {
+    int r = fp_tcp(k);
+    if (r != 1) return r;
+    if (f.has_src_ip && (r = fp_addr<L, 12>(k, f.src_ip)) != 1) return r;
+    if (f.has_dst_ip && (r = primed ? fp_addr<L, 12>(k, f.dst_ip) : fp_addr<L, 16>(k, f.dst_ip)) != 1) return r;
+    if ((r = fp_ports(k, f.src_ports, 0u)) != 1) return r;
+    return fp_ports(k, f.dst_ports, primed ? 0u : 2u);
+}
+
+template <int L>
+__global__ __launch_bounds__(kBlock) void k_capture_filter(FiltArgs a, DecOut d, rsk_capture_filter f) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    bool m = false;
+    if (i < a.n) {
+        FPkt<L> k;
+        const uint8_t *p = a.cap + a.cap_off[i];
+        k.cl = a.cap_len[i];
+        const uint8_t *last = p + (k.cl ? k.cl - 1u : 0u);
+        if (k.cl) rsk::load_window<16>(p, last, k.w);
+        else
+#pragma unroll
+            for (int q = 0; q < 16; ++q) k.w[q] = 0;
+        if (L == 14) {
+            k.lt = k.cl < 14u ? -1 : ({ const uint32_t et = (k.b(12) << 8) | k.b(13); et == 0x0800u ? 4 : et == 0x86ddu ? 6 : 0; });
+        } else {
+            k.lt = k.cl < 4u ? -1 : (k.w[0] == 2u ? 4 : (k.w[0] == 24u || k.w[0] == 28u || k.w[0] == 30u) ? 6 : 0);
+        }
+        const uint32_t th = L + (k.lt == 6 ? 40u : k.ihl4());
+#pragma unroll
+        for (int q = 0; q < 4; ++q) k.t[q] = 0;
+        if (k.lt > 0 && th < k.cl) rsk::load_window<4>(p + th, last, k.t);
+        int r;
+        if (!f.is_server) {
+            r = fp_main(k, f, false);
+        } else {  // ((syn) and F') or (F and (no syn))
+            r = fp_syn(k, true);
+            if (r == 1) r = fp_main(k, f, true);
+            if (r == 0) {
+                r = fp_main(k, f, false);
+                if (r == 1) r = fp_syn(k, false);
+            }
+        }
+        m = r == 1;
+        a.match[i] = m ? 1 : 0;
+    }
+    if (d.masks) compact_epilogue(d, m);
+}
+
 __global__ __launch_bounds__(1024) void k_scan(const uint32_t *counts, uint32_t *offsets, uint32_t nb,
                                                uint32_t *n_valid) {
     __shared__ uint32_t wsum[16];
@@ -1507,6 +1641,86 @@ int rsk_parse_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *cap_arena, con
     int r = launch_check("k_parse_decode");
     if (r || !compact) return r;
     return run_compaction(c, n, masks, counts, offsets, dec, (hipStream_t)stream);
+}
+
+int rsk_capture_filter_batch(rsk_ctx *c, uint32_t n, const uint8_t *cap_arena, const uint64_t *cap_off,
+                             const uint32_t *cap_len, int datalink, const rsk_capture_filter *f, uint8_t *match,
+                             uint32_t *match_idx, uint32_t *n_match, void *stream) {
+    if (!c || !f || (n && (!cap_arena || !cap_off || !cap_len || !match))) return RSK_EINVAL;
+    if (datalink != RSK_DLT_EN10MB && datalink != RSK_DLT_NULL) return RSK_EINVAL;
+    for (const rsk_port_list *pl : {&f->src_ports, &f->dst_ports}) {
+        if (pl->n_single > RSK_FILTER_MAX_PORTS || pl->n_range > RSK_FILTER_MAX_PORTS) return RSK_EINVAL;
+        for (uint32_t q = 0; q < pl->n_range; ++q)
+            if (pl->range[q][0] >= pl->range[q][1]) return RSK_EINVAL;  // RPortList::AddPortRange
+    }
+    DeviceGuard g(c->device);
+    if (!g.ok) return RSK_EDEVICE;
+    if (n == 0) {
+        if (n_match) {
+            hipError_t e = hipMemsetAsync(n_match, 0, sizeof(uint32_t), (hipStream_t)stream);
+            if (e != hipSuccess) { set_error("hipMemsetAsync", e); return RSK_EDEVICE; }
+        }
+        return RSK_OK;
+    }
+    const bool compact = match_idx || n_match;
+    uint64_t *masks = nullptr;
+    uint32_t *counts = nullptr, *offsets = nullptr;
+    if (compact) {
+        int r = ensure_ws(c, n);
+        if (r) return r;
+        ws_split(c, n, masks, counts, offsets);
+    }
+    FiltArgs a;
+    a.cap = cap_arena; a.cap_off = cap_off; a.cap_len = cap_len; a.match = match; a.n = n;
+    DecOut d;
+    std::memset(&d, 0, sizeof d);
+    d.masks = masks;
+    d.counts = counts;
+    if (datalink == RSK_DLT_EN10MB)
+        hipLaunchKernelGGL(k_capture_filter<14>, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, a, d, *f);
+    else
+        hipLaunchKernelGGL(k_capture_filter<4>, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, a, d, *f);
+    int r = launch_check("k_capture_filter");
+    if (r || !compact) return r;
+    rsk_decode_out o;
+    std::memset(&o, 0, sizeof o);
+    o.valid_idx = match_idx;
+    o.n_valid = n_match;
+    return run_compaction(c, n, masks, counts, offsets, &o, (hipStream_t)stream);
+}
+
+// BuildFilterStr (cap/cap_util.cpp:67-144) with proto "tcp" (cap/RCap.cpp:64)
+int rsk_filter_str(const rsk_capture_filter *f, char *buf, size_t buf_len) {
+    if (!f || !buf) return -1;
+    auto ip = [](uint32_t v) {
+        return std::to_string(v & 255u) + "." + std::to_string((v >> 8) & 255u) + "." +
+               std::to_string((v >> 16) & 255u) + "." + std::to_string(v >> 24);
+    };
+    auto ports = [](const rsk_port_list &pl, const char *dir) -> std::string {
+        if (pl.n_single == 0 && pl.n_range == 0) return "";
+        std::string s = "(";
+        for (uint32_t q = 0; q < pl.n_single && q < RSK_FILTER_MAX_PORTS; ++q)
+            s += std::string(" or ") + dir + " port " + std::to_string(pl.single[q]);
+        for (uint32_t q = 0; q < pl.n_range && q < RSK_FILTER_MAX_PORTS; ++q)
+            s += std::string(" or ") + dir + " portrange " + std::to_string(pl.range[q][0]) + "-" +
+                 std::to_string(pl.range[q][1]);
+        s += " )";
+        s.replace(s.find("or"), 2, "");  // the reference removes the first "or"
+        return " and " + s;
+    };
+    std::string out = "tcp";
+    if (f->has_src_ip) out += " and  (ip src " + ip(f->src_ip) + ")";
+    if (f->has_dst_ip) out += " and  (ip dst " + ip(f->dst_ip) + ")";
+    out += ports(f->src_ports, "src");
+    out += ports(f->dst_ports, "dst");
+    if (f->is_server) {
+        std::string s = out;
+        for (size_t pos = s.find("dst"); pos != std::string::npos; pos = s.find("dst")) s.replace(pos, 3, "src");
+        out = "((tcp[tcpflags] & tcp-syn != 0) and " + s + ") or (" + out + "and (tcp[tcpflags] & (tcp-syn) == 0))";
+    }
+    if (out.size() + 1 > buf_len) return -1;
+    std::memcpy(buf, out.c_str(), out.size() + 1);
+    return (int)out.size();
 }
 
 int rsk_tcpinfo_encode_batch(rsk_ctx *c, uint32_t n, const uint32_t *src, const uint32_t *dst,

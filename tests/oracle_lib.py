@@ -61,6 +61,8 @@ class Oracle:
         L.orc_inet_csum.restype = ctypes.c_uint16
         L.orc_inet_csum.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32]
         L.orc_key_for_tcp.restype = ctypes.c_uint64
+        L.orc_capture_filter.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_int, _vp]
+        L.orc_filter_str.argtypes = [_vp, ctypes.c_char_p, ctypes.c_size_t]
         L.orc_demux_batch.argtypes = [ctypes.c_uint32] + [_vp] * 6 + [ctypes.c_uint32] + [_vp] * 5
         L.orc_demux_batch.restype = ctypes.c_int
         L.orc_key_for_tcp.argtypes = [ctypes.c_uint16, ctypes.c_uint16]
@@ -135,6 +137,16 @@ class Oracle:
         out = ctypes.create_string_buffer(len(frame) + 64)
         n = self.L.orc_build_wire(frame, len(frame), src, dst, sp, dp, seq, ack, flag, ip_id, eth, out)
         return out.raw[:n]
+
+    def capture_filter(self, pkt: bytes, datalink: int, filt, cap_len: int | None = None) -> int:
+        cl = len(pkt) if cap_len is None else cap_len
+        return self.L.orc_capture_filter(bytes(pkt) + b"\0" * 64, cl, datalink, ctypes.addressof(filt))
+
+    def filter_str(self, filt) -> str:
+        buf = ctypes.create_string_buffer(16384)
+        n = self.L.orc_filter_str(ctypes.addressof(filt), buf, len(buf))
+        assert n >= 0
+        return buf.value.decode()
 
     def demux_batch(self, status, cmd, fields: int, id=None, conv=None, conn_key=None, dst=None):
         """-> list of (first packet, [packet indices]) in segment order (orc_demux_batch)."""

@@ -78,6 +78,12 @@ def main():
     dfields = rc._abi.DEMUX_ID | rc._abi.DEMUX_CONN_KEY | rc._abi.DEMUX_CMD_BARRIER
     ops["demux"] = lambda: cx.demux_batch(w.dec.status, w.dec.cmd, dfields, dmx, id=w.dec.id, conv=w.dec.conv,
                                           conn_key=w.dec.conn_key, stream=s)
+    # capture filter (server form) over the Ethernet wire packets: a 4M-packet capture batch
+    fmatch = torch.empty(n, dtype=torch.uint8, device=dev)
+    fidx = torch.empty(n, dtype=torch.int32, device=dev)
+    fnm = torch.empty(1, dtype=torch.int32, device=dev)
+    filt = rc.make_filter(dst_singles=[10001, 10002], dst_ranges=[(20000, 30000)], is_server=True)
+    ops["capture_filter"] = lambda: cx.capture_filter_batch(wiree, offe, ste, 1, filt, fmatch, fidx, fnm, stream=s)
     # realistic connection counts: 64 conns, 0.1% control packets, every packet VALID
     gk = torch.Generator(device=dev)
     gk.manual_seed(7)
@@ -118,6 +124,7 @@ def main():
         "parse_decode": 54 + 32 + 16 + 21 + 4 + 73 - 42,
         "demux": 1 + 1 + 8 + 8 + 4,  # status, cmd, id, conn_key in; perm out (+ per-segment words)
         "demux_64conn": 1 + 1 + 8 + 8 + 4,
+        "capture_filter": 8 + 4 + 64 + 16 + 1 + 4,  # cap_off, cap_len, header windows, match, match_idx
     }
     out = {}
     for k, t in times.items():
