@@ -818,7 +818,7 @@ __device__ __forceinline__ Dec decode_frame(const uint8_t *base, int nread, bool
             w[0] = A.x; w[1] = A.y; w[2] = A.z; w[3] = A.w;
             w[4] = B.x; w[5] = B.y; w[6] = B.z; w[7] = B.w;
         } else {
-            rsk::load_window<8>(base, base + nread - 1, w);
+            rsk::load_window16<8>(base, base + nread - 1, w);
         }
         const uint32_t len = w[2] & 0xffu;                 // EncHead len byte (frame[8])
         const int dl = nread - 8 - (int)len;                // data_len handed to hash_equal
@@ -922,6 +922,9 @@ struct ParseArgs {
     uint32_t n;
 };
 
+// L = link header bytes: 14 (DLT_EN10MB) or 4 (DLT_NULL).  One 64-B window (five 16-B loads, bounded
+// by cap_len) holds the link, IPv4 and (IHL 5) TCP headers; other IHLs load the TCP header apart.
+template <int L>
 __global__ __launch_bounds__(kBlock) void k_parse_decode(ParseArgs a, DecOut d, KeySched ks) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     bool valid = false;
@@ -934,29 +937,31 @@ __global__ __launch_bounds__(kBlock) void k_parse_decode(ParseArgs a, DecOut d, 
         do {
             if (wl < 44u) break;                                   // :139
             const uint8_t *last = pkt + (cl ? cl - 1u : 0u);
-            uint32_t ipo;
-            if (a.datalink == RSK_DLT_EN10MB) {                     // :144-151
-                if (cl < 14u) { ps = RSK_PARSE_MALFORMED; break; }
-                uint32_t w[4];
-                rsk::load_window<4>(pkt, last, w);
-                if ((w[3] & 0xffffu) != 0x0008u) break;            // OM_PROTO_IP read LE
-                ipo = 14;
+            if (cl < (uint32_t)L) { ps = RSK_PARSE_MALFORMED; break; }
+            uint32_t hw[16];
+            rsk::load_window16<16>(pkt, last, hw);
+            if (L == 14) {                                          // :144-151
+                if ((hw[3] & 0xffffu) != 0x0008u) break;           // OM_PROTO_IP read LE
             } else {                                                // DLT_NULL :152-160
-                if (cl < 4u) { ps = RSK_PARSE_MALFORMED; break; }
-                uint32_t w[1];
-                rsk::load_window<1>(pkt, last, w);
-                if (w[0] != 2u) break;
-                ipo = 4;
+                if (hw[0] != 2u) break;
             }
+            constexpr uint32_t ipo = L;
             if (cl < ipo + 20u) { ps = RSK_PARSE_MALFORMED; break; }
             uint32_t ip[5];
-            rsk::load_window<5>(pkt + ipo, last, ip);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) ip[k] = rsk::funnel(hw[L / 4 + k + 1], hw[L / 4 + k], L & 3);
             if (((ip[2] >> 8) & 0xffu) != 6u) break;               // ip_p :167-172
             const uint32_t ihl = (ip[0] & 15u) * 4u;
             const uint32_t tcpo = ipo + ihl;
             if (cl < tcpo + 20u) { ps = RSK_PARSE_MALFORMED; break; }
             uint32_t th[4];
-            rsk::load_window<4>(pkt + tcpo, last, th);
+            if (ihl == 20u) {
+                constexpr int T = L + 20;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) th[k] = rsk::funnel(hw[T / 4 + k + 1], hw[T / 4 + k], T & 3);
+            } else {
+                rsk::load_window16<4>(pkt + tcpo, last, th);
+            }
             const uint32_t thl = ((th[3] & 0xffu) >> 4) * 4u;
             payo = tcpo + thl;
             const int payload_len = (int)rsk::bswap16(ip[0] >> 16) - (int)(ihl + thl);  // :177
@@ -1112,7 +1117,7 @@ __global__ __launch_bounds__(kBlock) void k_capture_filter(FiltArgs a, DecOut d,
         const uint8_t *p = a.cap + a.cap_off[i];
         k.cl = a.cap_len[i];
         const uint8_t *last = p + (k.cl ? k.cl - 1u : 0u);
-        if (k.cl) rsk::load_window<16>(p, last, k.w);
+        if (k.cl) rsk::load_window16<16>(p, last, k.w);
         else
 #pragma unroll
             for (int q = 0; q < 16; ++q) k.w[q] = 0;
@@ -1124,7 +1129,7 @@ __global__ __launch_bounds__(kBlock) void k_capture_filter(FiltArgs a, DecOut d,
         const uint32_t th = L + (k.lt == 6 ? 40u : k.ihl4());
 #pragma unroll
         for (int q = 0; q < 4; ++q) k.t[q] = 0;
-        if (k.lt > 0 && th < k.cl) rsk::load_window<4>(p + th, last, k.t);
+        if (k.lt > 0 && th < k.cl) rsk::load_window16<4>(p + th, last, k.t);
         int r;
         if (!f.is_server) {
             r = fp_main(k, f, false);
@@ -1637,7 +1642,10 @@ int rsk_parse_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *cap_arena, con
     a.flag = tcp->flag; a.pst = tcp->parse_status; a.cpo = tcp->cap_pay_off; a.cpl = tcp->cap_pay_len;
     a.datalink = datalink; a.flags = flags; a.n = n;
     DecOut d = make_dec_out(dec, masks, counts);
-    hipLaunchKernelGGL(k_parse_decode, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, a, d, c->ks);
+    if (datalink == RSK_DLT_EN10MB)
+        hipLaunchKernelGGL(k_parse_decode<14>, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, a, d, c->ks);
+    else
+        hipLaunchKernelGGL(k_parse_decode<4>, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, a, d, c->ks);
     int r = launch_check("k_parse_decode");
     if (r || !compact) return r;
     return run_compaction(c, n, masks, counts, offsets, dec, (hipStream_t)stream);
