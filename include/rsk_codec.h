@@ -203,6 +203,32 @@ int rsk_decode_batch(rsk_ctx *ctx, uint32_t n, const uint8_t *frame_arena, const
                      const uint16_t *frame_len, const uint8_t *is_tcp_close, const rsk_decode_out *out,
                      void *stream);
 
+/* ---- header-only batches (host-resident deployments) ------------------------------------------
+ * The codec reads one payload byte per frame (payload[0] for the tag) and writes / verifies the
+ * first 31 frame bytes: a caller whose payloads live in host memory ships only those bytes over PCIe
+ * and keeps the payload where it is (assembling frame = header(31) | payload with an iovec, or the
+ * memcpy RConn.cpp:104 does anyway).  Slots are 32 B, 16-B aligned, slot i at hdr + 32 i. */
+typedef struct rsk_encode_hdr_in {
+    const uint8_t *first_byte; /* [n] payload[0] (read only when 1 <= pay_len <= 1469)             */
+    const uint16_t *pay_len;   /* [n]                                                              */
+    const uint8_t *cmd;
+    const uint32_t *conv;
+    const uint64_t *conn_key;
+    const uint8_t *id;         /* [n*8] 8-B aligned, or NULL (then id_uniform)                     */
+    uint8_t id_uniform[8];
+} rsk_encode_hdr_in;
+/* slot i = frame bytes [0, 32): tag | EncHead | payload[0]; zero when status[i] <= 0.  status as
+ * rsk_encode_batch. */
+int rsk_encode_headers_batch(rsk_ctx *ctx, uint32_t n, const rsk_encode_hdr_in *in, uint8_t *hdr,
+                             int32_t *status, void *stream);
+/* slot i = frame bytes [0, 31) and, in byte 31, the byte OnRecv hashes: frame[8 + len] with
+ * len = frame[8] (= frame[31] for a well-formed frame); rsk_stage_decode_header builds it.
+ * frame_len[i] is the frame's full length; outputs exactly as rsk_decode_batch on the whole frame. */
+int rsk_decode_headers_batch(rsk_ctx *ctx, uint32_t n, const uint8_t *hdr, const uint16_t *frame_len,
+                             const uint8_t *is_tcp_close, const rsk_decode_out *out, void *stream);
+/* Host: the decode slot of one received frame (host pointers). */
+void rsk_stage_decode_header(const uint8_t *frame, int nread, uint8_t *slot);
+
 /* ---- fused pcap parse + decode (RawTcp::RawInput -> cap2uv -> RConn::OnRecv) ----------------- */
 typedef struct rsk_tcpinfo_out {
     uint32_t *src;  /* [n] ip_dst as stored (network byte order bytes, read LE) — "self" view   */

@@ -95,6 +95,11 @@ class TcpInfoOut(ctypes.Structure):
     ]
 
 
+class EncodeHdrIn(ctypes.Structure):
+    _fields_ = [("first_byte", _vp), ("pay_len", _vp), ("cmd", _vp), ("conv", _vp), ("conn_key", _vp), ("id", _vp),
+                ("id_uniform", ctypes.c_uint8 * 8)]
+
+
 class DemuxIn(ctypes.Structure):
     _fields_ = [("status", _vp), ("cmd", _vp), ("id", _vp), ("conv", _vp), ("conn_key", _vp), ("dst", _vp)]
 
@@ -125,6 +130,11 @@ SIGNATURES = [
      [_vp, ctypes.c_uint32, ctypes.POINTER(EncodeIn), ctypes.POINTER(EncodeOut), _vp]),
     ("rsk_encode_wire_batch", ctypes.c_int,
      [_vp, ctypes.c_uint32, ctypes.POINTER(EncodeIn), ctypes.POINTER(WireIn), ctypes.POINTER(EncodeOut), _vp]),
+    ("rsk_encode_headers_batch", ctypes.c_int,
+     [_vp, ctypes.c_uint32, ctypes.POINTER(EncodeHdrIn), _vp, _vp, _vp]),
+    ("rsk_decode_headers_batch", ctypes.c_int,
+     [_vp, ctypes.c_uint32, _vp, _vp, _vp, ctypes.POINTER(DecodeOut), _vp]),
+    ("rsk_stage_decode_header", None, [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p]),
     ("rsk_decode_batch", ctypes.c_int,
      [_vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, ctypes.POINTER(DecodeOut), _vp]),
     ("rsk_parse_decode_batch", ctypes.c_int,

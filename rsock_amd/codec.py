@@ -12,6 +12,8 @@ streams).  Every call goes through ``rsock_amd/librsk.so``; there is no CPU path
 from __future__ import annotations
 
 import ctypes
+
+import numpy as np
 from dataclasses import dataclass, fields
 
 import torch
@@ -95,6 +97,24 @@ class DecodeBuffers:
         for f in fields(self):
             out[f.name] = getattr(self, f.name).cpu().numpy()
         return out
+
+
+def stage_decode_headers(arena: np.ndarray, offs: np.ndarray, lens: np.ndarray) -> np.ndarray:
+    """Host staging for rsk_decode_headers_batch, vectorised (same bytes as rsk_stage_decode_header):
+    slot = frame[0:min(32, len)] zero-filled, byte 31 = frame[8 + frame[8]] when that is inside."""
+    n = len(offs)
+    offs = offs.astype(np.int64)
+    lens = lens.astype(np.int64)
+    k = np.arange(32)
+    idx = offs[:, None] + k[None, :]
+    inside = k[None, :] < lens[:, None]
+    slots = np.where(inside, arena[np.minimum(idx, len(arena) - 1)], 0).astype(np.uint8)
+    has8 = lens > 8
+    ln = np.where(has8, arena[np.minimum(offs + 8, len(arena) - 1)], 0).astype(np.int64)
+    at = 8 + ln
+    ok = has8 & (at < lens)
+    slots[ok, 31] = arena[(offs + at)[ok]]
+    return slots.reshape(n, 32)
 
 
 def ip_u32(ip: str) -> int:
@@ -284,6 +304,22 @@ class Codec:
         _check(lib().rsk_tcpinfo_encode_batch(self._ctx, n, _ptr(src), _ptr(dst), _ptr(sp), _ptr(dp),
                                               _ptr(seq), _ptr(ack), _ptr(flag), _ptr(rec),
                                               _stream(stream)), "rsk_tcpinfo_encode_batch")
+
+    def output_headers_batch(self, first_byte, pay_len, cmd, conv, conn_key, hdr, status, id=None,
+                             id_uniform: bytes = b"\0" * 8, stream=None) -> None:
+        """Header-only RConn::Output (rsk_encode_headers_batch): hdr[32 i:32 i+32] = frame bytes [0, 32)."""
+        n = pay_len.numel()
+        ein = _abi.EncodeHdrIn(_ptr(first_byte), _ptr(pay_len), _ptr(cmd), _ptr(conv), _ptr(conn_key), _ptr(id),
+                               (ctypes.c_uint8 * 8)(*bytes(id_uniform)[:8].ljust(8, b"\0")))
+        _check(lib().rsk_encode_headers_batch(self._ctx, n, ctypes.byref(ein), _ptr(hdr), _ptr(status),
+                                              _stream(stream)), "rsk_encode_headers_batch")
+
+    def onrecv_headers_batch(self, hdr, frame_len, out: DecodeBuffers, is_tcp_close=None, stream=None) -> None:
+        """Header-only RConn::OnRecv (rsk_decode_headers_batch) on 32-B slots (stage_decode_headers)."""
+        n = frame_len.numel()
+        _check(lib().rsk_decode_headers_batch(self._ctx, n, _ptr(hdr), _ptr(frame_len), _ptr(is_tcp_close),
+                                              ctypes.byref(out.abi()), _stream(stream)),
+               "rsk_decode_headers_batch")
 
     def capture_filter_batch(self, cap, cap_off, cap_len, datalink: int, filt: "_abi.CaptureFilter", match,
                              match_idx=None, n_match=None, stream=None) -> None:

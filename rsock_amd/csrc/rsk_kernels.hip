@@ -807,12 +807,15 @@ struct Dec {
 
 // RConn::OnRecv on frame bytes [base, base + nread)  (conn/RConn.cpp:64-85, EncHead.cpp:39-55,
 // util/rhash.cpp:71-92).
-__device__ __forceinline__ Dec decode_frame(const uint8_t *base, int nread, bool close,
-                                            const KeySched &ks) {
+// SLOT: base is a 32-B header slot (rsk_decode_headers_batch) whose byte 31 holds the hashed byte
+// frame[8 + len]; nread is still the frame's length.
+template <bool SLOT>
+__device__ __forceinline__ Dec decode_frame_t(const uint8_t *base, int nread, bool close,
+                                              const KeySched &ks) {
     Dec o = {0, 0, 0, 0, 0, 0, 0, 0, RSK_RECV_DROP};
     if (nread > RSK_HEAD_SIZE) {
         uint32_t w[8];
-        if ((reinterpret_cast<uintptr_t>(base) & 15u) == 0) {
+        if (SLOT || (reinterpret_cast<uintptr_t>(base) & 15u) == 0) {
             const uint4 A = reinterpret_cast<const uint4 *>(base)[0];
             const uint4 B = reinterpret_cast<const uint4 *>(base)[1];
             w[0] = A.x; w[1] = A.y; w[2] = A.z; w[3] = A.w;
@@ -823,7 +826,7 @@ __device__ __forceinline__ Dec decode_frame(const uint8_t *base, int nread, bool
         const uint32_t len = w[2] & 0xffu;                 // EncHead len byte (frame[8])
         const int dl = nread - 8 - (int)len;                // data_len handed to hash_equal
         if ((int)len <= nread - 8 && dl > 0) {              // DecodeBuf ok, hash_equal len > 0
-            const uint32_t b = len == (uint32_t)RSK_ENC_HEAD_SIZE ? (w[7] >> 24) : base[8 + len];
+            const uint32_t b = (SLOT || len == (uint32_t)RSK_ENC_HEAD_SIZE) ? (w[7] >> 24) : base[8 + len];
             uint32_t t0, t1;
             rsk::md5_tag(ks, b, t0, t1);
             if (t0 == w[0] && t1 == w[1]) {
@@ -843,6 +846,10 @@ __device__ __forceinline__ Dec decode_frame(const uint8_t *base, int nread, bool
         o.st = RSK_RECV_CLOSE;
     }
     return o;
+}
+
+__device__ __forceinline__ Dec decode_frame(const uint8_t *base, int nread, bool close, const KeySched &ks) {
+    return decode_frame_t<false>(base, nread, close, ks);
 }
 
 struct DecOut {
@@ -902,6 +909,54 @@ __global__ __launch_bounds__(kBlock) void k_decode(DecArgs a, DecOut d, KeySched
         valid = o.st == RSK_RECV_VALID;
     }
     if (d.masks) compact_epilogue(d, valid);
+}
+
+// Header-only decode: 32-B slots (frame bytes [0, 31) + the hashed byte), one lane per frame.
+__global__ __launch_bounds__(kBlock) void k_decode_hdr(DecArgs a, DecOut d, KeySched ks) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    bool valid = false;
+    if (i < a.n) {
+        const Dec o = decode_frame_t<true>(a.frame + 32u * i, (int)a.frame_len[i], a.close ? a.close[i] != 0 : false,
+                                           ks);
+        store_dec(d, i, o);
+        valid = o.st == RSK_RECV_VALID;
+    }
+    if (d.masks) compact_epilogue(d, valid);
+}
+
+// Header-only encode: frame bytes [0, 32) (tag, EncHead, payload[0]) per packet into 32-B slots.
+struct EncHdrArgs {
+    const uint8_t *b0;
+    const uint16_t *pay_len;
+    const uint8_t *cmd;
+    const uint32_t *conv;
+    const uint64_t *conn_key;
+    const uint8_t *id;
+    uint8_t *hdr;
+    int32_t *status;
+    uint32_t id_lo, id_hi, n;
+};
+
+__global__ __launch_bounds__(kBlock) void k_encode_hdr(EncHdrArgs a, KeySched ks) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= a.n) return;
+    const uint32_t P = a.pay_len[i];
+    const int32_t st = P == 0 ? RSK_SEND_RESET : (P > RSK_MAX_PAYLOAD ? RSK_SEND_OVERSIZE : (int32_t)(RSK_HEAD_SIZE + P));
+    uint32_t H[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (st > 0) {  // RConn.cpp:88-105
+        const uint32_t b0 = a.b0[i];
+        rsk::md5_tag(ks, b0, H[0], H[1]);
+        uint32_t id0 = a.id_lo, id1 = a.id_hi;
+        if (a.id) {
+            const uint2 v = *reinterpret_cast<const uint2 *>(a.id + 8 * i);
+            id0 = v.x;
+            id1 = v.y;
+        }
+        head_words(a.cmd[i], id0, id1, a.conv[i], a.conn_key[i], b0, H);
+    }
+    st16<0>(a.hdr + 32u * i, make_uint4(H[0], H[1], H[2], H[3]));
+    st16<0>(a.hdr + 32u * i + 16u, make_uint4(H[4], H[5], H[6], H[7]));
+    a.status[i] = st;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1609,6 +1664,66 @@ int rsk_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *frame_arena, const u
     int r = launch_check("k_decode");
     if (r || !compact) return r;
     return run_compaction(c, n, masks, counts, offsets, out, (hipStream_t)stream);
+}
+
+int rsk_encode_headers_batch(rsk_ctx *c, uint32_t n, const rsk_encode_hdr_in *in, uint8_t *hdr, int32_t *status,
+                             void *stream) {
+    if (!c || !in) return RSK_EINVAL;
+    if (n == 0) return RSK_OK;
+    if (!in->first_byte || !in->pay_len || !in->cmd || !in->conv || !in->conn_key || !hdr || !status)
+        return RSK_EINVAL;
+    if ((reinterpret_cast<uintptr_t>(hdr) & 15u) || (in->id && (reinterpret_cast<uintptr_t>(in->id) & 7u)))
+        return RSK_EINVAL;
+    DeviceGuard g(c->device);
+    if (!g.ok) return RSK_EDEVICE;
+    EncHdrArgs a;
+    a.b0 = in->first_byte; a.pay_len = in->pay_len; a.cmd = in->cmd; a.conv = in->conv; a.conn_key = in->conn_key;
+    a.id = in->id; a.hdr = hdr; a.status = status; a.n = n;
+    std::memcpy(&a.id_lo, in->id_uniform, 4);
+    std::memcpy(&a.id_hi, in->id_uniform + 4, 4);
+    hipLaunchKernelGGL(k_encode_hdr, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, a, c->ks);
+    return launch_check("k_encode_hdr");
+}
+
+int rsk_decode_headers_batch(rsk_ctx *c, uint32_t n, const uint8_t *hdr, const uint16_t *frame_len,
+                             const uint8_t *is_tcp_close, const rsk_decode_out *out, void *stream) {
+    if (!c || !hdr || !frame_len || !dec_out_ok(out)) return RSK_EINVAL;
+    if (reinterpret_cast<uintptr_t>(hdr) & 15u) return RSK_EINVAL;
+    DeviceGuard g(c->device);
+    if (!g.ok) return RSK_EDEVICE;
+    if (n == 0) {
+        if (out->n_valid) {
+            hipError_t e = hipMemsetAsync(out->n_valid, 0, sizeof(uint32_t), (hipStream_t)stream);
+            if (e != hipSuccess) { set_error("hipMemsetAsync", e); return RSK_EDEVICE; }
+        }
+        return RSK_OK;
+    }
+    const bool compact = out->valid_idx || out->n_valid;
+    uint64_t *masks = nullptr;
+    uint32_t *counts = nullptr, *offsets = nullptr;
+    if (compact) {
+        int r = ensure_ws(c, n);
+        if (r) return r;
+        ws_split(c, n, masks, counts, offsets);
+    }
+    DecArgs a{hdr, nullptr, frame_len, is_tcp_close, n};
+    DecOut d = make_dec_out(out, masks, counts);
+    hipLaunchKernelGGL(k_decode_hdr, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, a, d, c->ks);
+    int r = launch_check("k_decode_hdr");
+    if (r || !compact) return r;
+    return run_compaction(c, n, masks, counts, offsets, out, (hipStream_t)stream);
+}
+
+// Host: the 32-B decode slot of one received frame (EncHead::DecodeBuf reads frame[8] = len; the
+// hashed byte is frame[8 + len] when that lies inside the frame, RConn.cpp:64-75).
+void rsk_stage_decode_header(const uint8_t *frame, int nread, uint8_t *slot) {
+    const int k = nread < 0 ? 0 : (nread < 32 ? nread : 32);
+    std::memcpy(slot, frame, (size_t)k);
+    if (k < 32) std::memset(slot + k, 0, (size_t)(32 - k));
+    if (nread > 8) {
+        const int at = 8 + frame[8];
+        if (at < nread) slot[31] = frame[at];
+    }
 }
 
 int rsk_parse_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *cap_arena, const uint64_t *cap_off,

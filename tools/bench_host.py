@@ -10,6 +10,10 @@ Modes (one JSON line each):
   encode   host payloads + descriptors -> frames back to host               (send path)
   decode   host frames -> verify + compact -> fields / valid_idx to host    (receive path)
   both     both directions per chunk
+  encode_hdr / decode_hdr / both_hdr   header-only (rsk_encode_headers_batch / rsk_decode_headers_batch):
+           payload[0] + descriptors in, 32-B header slots + status out; staged 32-B frame-header slots
+           in, fields out — the payload never crosses PCIe (it stays in host memory for an iovec send /
+           in the capture buffer for delivery)
 """
 import argparse
 import json
@@ -29,6 +33,7 @@ def main():
     ap.add_argument("--chunk", type=int, default=262144)
     ap.add_argument("--streams", type=int, default=3)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--modes", default="encode,decode,both,encode_hdr,decode_hdr,both_hdr")
     args = ap.parse_args()
     import torch
 
@@ -52,6 +57,11 @@ def main():
     h_cmd, h_conv, h_key = w.cmd.cpu().pin_memory(), w.conv.cpu().pin_memory(), w.conn_key.cpu().pin_memory()
     h_flen = w.frame_len.cpu().pin_memory()
     h_frames_out = torch.empty_like(h_frames_in).pin_memory()
+    # header-only inputs: payload[0] per packet; staged decode slots of the captured frames
+    h_b0 = w.payload[w.pay_off].cpu().pin_memory()
+    h_slots = torch.from_numpy(rc.stage_decode_headers(h_frames_in.numpy(), w.frame_off.cpu().numpy(),
+                                                       h_flen.numpy().astype(np.int32) & 0xFFFF).reshape(-1)).pin_memory()
+    h_hdr_out = torch.empty(32 * n, dtype=torch.uint8).pin_memory()
     h_status = torch.empty(n, dtype=torch.int32).pin_memory()
     h_dstat = torch.empty(n, dtype=torch.int8).pin_memory()
     h_dconv = torch.empty(n, dtype=torch.int32).pin_memory()
@@ -79,6 +89,9 @@ def main():
             "pay_off": torch.arange(C, device=dev, dtype=torch.int64) * pp,
             "frame_off": torch.arange(C, device=dev, dtype=torch.int64) * fp,
             "dec": rc.DecodeBuffers.alloc(C, dev),
+            "b0": torch.empty(C, dtype=torch.uint8, device=dev),
+            "hdr": torch.empty(32 * C, dtype=torch.uint8, device=dev),
+            "slots": torch.empty(32 * C, dtype=torch.uint8, device=dev),
             "cx": rc.Codec(b"hello135", 0),
         }
         b["cx"].reserve(C)
@@ -101,6 +114,25 @@ def main():
                                          id_uniform=workload.ID_UNIFORM, pad16=True, stream=s)
                     h_frames_out[c0 * fp: (c0 + m) * fp].copy_(b["frame"][: m * fp], non_blocking=True)
                     h_status[c0: c0 + m].copy_(b["status"][:m], non_blocking=True)
+                if mode in ("encode_hdr", "both_hdr"):
+                    b["b0"][:m].copy_(h_b0[c0: c0 + m], non_blocking=True)
+                    b["len"][:m].copy_(h_len[c0: c0 + m], non_blocking=True)
+                    b["cmd"][:m].copy_(h_cmd[c0: c0 + m], non_blocking=True)
+                    b["conv"][:m].copy_(h_conv[c0: c0 + m], non_blocking=True)
+                    b["key"][:m].copy_(h_key[c0: c0 + m], non_blocking=True)
+                    b["cx"].output_headers_batch(b["b0"][:m], b["len"][:m], b["cmd"][:m], b["conv"][:m], b["key"][:m],
+                                                 b["hdr"], b["status"][:m], id_uniform=workload.ID_UNIFORM, stream=s)
+                    h_hdr_out[32 * c0: 32 * (c0 + m)].copy_(b["hdr"][: 32 * m], non_blocking=True)
+                    h_status[c0: c0 + m].copy_(b["status"][:m], non_blocking=True)
+                if mode in ("decode_hdr", "both_hdr"):
+                    b["slots"][: 32 * m].copy_(h_slots[32 * c0: 32 * (c0 + m)], non_blocking=True)
+                    b["flen"][:m].copy_(h_flen[c0: c0 + m], non_blocking=True)
+                    dec = b["dec"]
+                    b["cx"].onrecv_headers_batch(b["slots"], b["flen"][:m], dec, stream=s)
+                    h_dstat[c0: c0 + m].copy_(dec.status[:m], non_blocking=True)
+                    h_dconv[c0: c0 + m].copy_(dec.conv[:m], non_blocking=True)
+                    h_dkey[c0: c0 + m].copy_(dec.conn_key[:m], non_blocking=True)
+                    h_vidx[c0: c0 + m].copy_(dec.valid_idx[:m], non_blocking=True)
                 if mode in ("decode", "both"):
                     b["frame_in"][: m * fp].copy_(h_frames_in[c0 * fp: (c0 + m) * fp], non_blocking=True)
                     b["flen"][:m].copy_(h_flen[c0: c0 + m], non_blocking=True)
@@ -112,7 +144,7 @@ def main():
                     h_vidx[c0: c0 + m].copy_(dec.valid_idx[:m], non_blocking=True)
 
     out = {}
-    for mode in ("encode", "decode", "both"):
+    for mode in args.modes.split(","):
         run(mode)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -125,9 +157,13 @@ def main():
     assert bool((h_status == (h_len.to(torch.int32) & 0xFFFF) + 31).all())
     assert torch.equal(h_frames_out.view(n, fp)[:, :1431], h_frames_in.view(n, fp)[:, :1431]) or args.config != "c3"
     assert bool((h_dstat == 1).all())
+    if "encode_hdr" in out or "both_hdr" in out:
+        assert torch.equal(h_hdr_out.view(n, 32)[:, :31], h_frames_in.view(n, fp)[:, :31])
     print(json.dumps({"host_resident_Mpkt_s": out, "config": args.config, "packets": n, "chunk": C, "streams": S,
                       "pcie_bytes_per_pkt": {"encode": {"h2d": pp + 15, "d2h": fp + 4},
-                                             "decode": {"h2d": fp + 2, "d2h": 1 + 4 + 8 + 4}}}))
+                                             "decode": {"h2d": fp + 2, "d2h": 1 + 4 + 8 + 4},
+                                             "encode_hdr": {"h2d": 16, "d2h": 36},
+                                             "decode_hdr": {"h2d": 34, "d2h": 1 + 4 + 8 + 4}}}))
 
 
 if __name__ == "__main__":
