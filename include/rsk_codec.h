@@ -228,6 +228,14 @@ int rsk_decode_headers_batch(rsk_ctx *ctx, uint32_t n, const uint8_t *hdr, const
                              const uint8_t *is_tcp_close, const rsk_decode_out *out, void *stream);
 /* Host: the decode slot of one received frame (host pointers). */
 void rsk_stage_decode_header(const uint8_t *frame, int nread, uint8_t *slot);
+/* Host batch forms (host pointers; nthreads <= 1 runs on the caller's thread): stage the slots of n
+ * frames at arena + frame_off[i]; assemble frame i = hdr slot bytes [0, 31) | payload (status[i] - 31
+ * bytes at payload_arena + pay_off[i]) for status[i] > 0 — the copy RConn::Output makes
+ * (RConn.cpp:100-104) when the sender needs one contiguous frame. */
+int rsk_stage_decode_headers(uint32_t n, const uint8_t *arena, const uint64_t *frame_off,
+                             const uint16_t *frame_len, uint8_t *slots, int nthreads);
+int rsk_assemble_frames(uint32_t n, const uint8_t *hdr, const int32_t *status, const uint8_t *payload_arena,
+                        const uint64_t *pay_off, uint8_t *frame_arena, const uint64_t *frame_off, int nthreads);
 
 /* ---- fused pcap parse + decode (RawTcp::RawInput -> cap2uv -> RConn::OnRecv) ----------------- */
 typedef struct rsk_tcpinfo_out {

@@ -135,6 +135,8 @@ SIGNATURES = [
     ("rsk_decode_headers_batch", ctypes.c_int,
      [_vp, ctypes.c_uint32, _vp, _vp, _vp, ctypes.POINTER(DecodeOut), _vp]),
     ("rsk_stage_decode_header", None, [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p]),
+    ("rsk_stage_decode_headers", ctypes.c_int, [ctypes.c_uint32, _vp, _vp, _vp, _vp, ctypes.c_int]),
+    ("rsk_assemble_frames", ctypes.c_int, [ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int]),
     ("rsk_decode_batch", ctypes.c_int,
      [_vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, ctypes.POINTER(DecodeOut), _vp]),
     ("rsk_parse_decode_batch", ctypes.c_int,
