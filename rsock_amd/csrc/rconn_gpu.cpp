@@ -84,35 +84,25 @@ int RConnGpu::alloc_slots() {
     for (auto &s : enc_) {
         if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess) return -1;
         if (hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) return -1;
-        if (hmalloc(&s.h_pay, n * kPayPitch) || hmalloc(&s.h_frame, n * kFramePitch) || hmalloc(&s.h_cmd, n) ||
-            hmalloc(&s.h_id, 8 * n) || hmalloc(&s.h_pay_off, n) || hmalloc(&s.h_frame_off, n) ||
+        if (hmalloc(&s.h_b0, n) || hmalloc(&s.h_cmd, n) || hmalloc(&s.h_id, 8 * n) || hmalloc(&s.h_hdr, 32 * n) ||
             hmalloc(&s.h_key, n) || hmalloc(&s.h_len, n) || hmalloc(&s.h_conv, n) || hmalloc(&s.h_status, n))
             return -1;
-        if (dmalloc(&s.d_pay, n * kPayPitch) || dmalloc(&s.d_frame, n * kFramePitch) || dmalloc(&s.d_cmd, n) ||
-            dmalloc(&s.d_id, 8 * n) || dmalloc(&s.d_pay_off, n) || dmalloc(&s.d_frame_off, n) ||
+        if (dmalloc(&s.d_b0, n) || dmalloc(&s.d_cmd, n) || dmalloc(&s.d_id, 8 * n) || dmalloc(&s.d_hdr, 32 * n) ||
             dmalloc(&s.d_key, n) || dmalloc(&s.d_len, n) || dmalloc(&s.d_conv, n) || dmalloc(&s.d_status, n))
             return -1;
-        for (size_t i = 0; i < n; ++i) {
-            s.h_pay_off[i] = i * kPayPitch;
-            s.h_frame_off[i] = i * kFramePitch;
-        }
-        // offsets never change: upload once
-        if (hipMemcpy(s.d_pay_off, s.h_pay_off, 8 * n, hipMemcpyHostToDevice) != hipSuccess ||
-            hipMemcpy(s.d_frame_off, s.h_frame_off, 8 * n, hipMemcpyHostToDevice) != hipSuccess)
-            return -1;
+        if (hmalloc(&s.frame, n * kFramePitch)) return -1;
         s.user.resize(n);
     }
     for (auto &s : dec_) {
         if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess) return -1;
         if (hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) return -1;
-        if (hmalloc(&s.h_frame, n * kFramePitch) || hmalloc(&s.h_close, n) || hmalloc(&s.h_off, n) ||
-            hmalloc(&s.h_len, n) || hmalloc(&s.h_out, dec_out_bytes()))
+        if (hmalloc(&s.h_slot, 32 * n) || hmalloc(&s.h_close, n) || hmalloc(&s.h_len, n) ||
+            hmalloc(&s.h_out, dec_out_bytes()))
             return -1;
-        if (dmalloc(&s.d_frame, n * kFramePitch) || dmalloc(&s.d_close, n) || dmalloc(&s.d_off, n) ||
-            dmalloc(&s.d_len, n) || dmalloc(&s.d_out, dec_out_bytes()))
+        if (dmalloc(&s.d_slot, 32 * n) || dmalloc(&s.d_close, n) || dmalloc(&s.d_len, n) ||
+            dmalloc(&s.d_out, dec_out_bytes()))
             return -1;
-        for (size_t i = 0; i < n; ++i) s.h_off[i] = i * kFramePitch;
-        if (hipMemcpy(s.d_off, s.h_off, 8 * n, hipMemcpyHostToDevice) != hipSuccess) return -1;
+        if (hmalloc(&s.frame, n * kFramePitch)) return -1;
         s.user.resize(n);
         s.big.resize(n);
     }
@@ -122,10 +112,10 @@ int RConnGpu::alloc_slots() {
 void RConnGpu::free_slots() {
     for (auto &s : enc_) {
         if (s.stream) (void)hipStreamSynchronize(s.stream);
-        hfree(s.h_pay); hfree(s.h_frame); hfree(s.h_cmd); hfree(s.h_id); hfree(s.h_pay_off);
-        hfree(s.h_frame_off); hfree(s.h_key); hfree(s.h_len); hfree(s.h_conv); hfree(s.h_status);
-        dfree(s.d_pay); dfree(s.d_frame); dfree(s.d_cmd); dfree(s.d_id); dfree(s.d_pay_off);
-        dfree(s.d_frame_off); dfree(s.d_key); dfree(s.d_len); dfree(s.d_conv); dfree(s.d_status);
+        hfree(s.frame); hfree(s.h_b0); hfree(s.h_cmd); hfree(s.h_id); hfree(s.h_hdr); hfree(s.h_key); hfree(s.h_len);
+        hfree(s.h_conv); hfree(s.h_status);
+        dfree(s.d_b0); dfree(s.d_cmd); dfree(s.d_id); dfree(s.d_hdr); dfree(s.d_key); dfree(s.d_len);
+        dfree(s.d_conv); dfree(s.d_status);
         if (s.done) (void)hipEventDestroy(s.done);
         if (s.stream) (void)hipStreamDestroy(s.stream);
         s.done = nullptr;
@@ -133,8 +123,8 @@ void RConnGpu::free_slots() {
     }
     for (auto &s : dec_) {
         if (s.stream) (void)hipStreamSynchronize(s.stream);
-        hfree(s.h_frame); hfree(s.h_close); hfree(s.h_off); hfree(s.h_len); hfree(s.h_out);
-        dfree(s.d_frame); dfree(s.d_close); dfree(s.d_off); dfree(s.d_len); dfree(s.d_out);
+        hfree(s.frame); hfree(s.h_slot); hfree(s.h_close); hfree(s.h_len); hfree(s.h_out);
+        dfree(s.d_slot); dfree(s.d_close); dfree(s.d_len); dfree(s.d_out);
         if (s.done) (void)hipEventDestroy(s.done);
         if (s.stream) (void)hipStreamDestroy(s.stream);
         s.done = nullptr;
@@ -150,7 +140,8 @@ int RConnGpu::Output(ssize_t nread, const char *base, const EncHeadFields &head,
     if (!ok_) return RSK_EDEVICE;
     EncSlot &s = enc_[enc_cur_];
     const uint32_t i = s.count;
-    std::memcpy(s.h_pay + (size_t)i * kPayPitch, base, (size_t)nread);
+    std::memcpy(s.frame + (size_t)i * kFramePitch + RSK_HEAD_SIZE, base, (size_t)nread);  // RConn.cpp:104
+    s.h_b0[i] = (uint8_t)base[0];
     s.h_len[i] = (uint16_t)nread;
     s.h_cmd[i] = head.cmd;
     std::memcpy(s.h_id + 8 * (size_t)i, head.id, 8);
@@ -167,25 +158,19 @@ int RConnGpu::Output(ssize_t nread, const char *base, const EncHeadFields &head,
 int RConnGpu::launch_enc(EncSlot &s) {
     const size_t n = s.count;
     hipStream_t st = s.stream;
-    size_t pay_bytes = 0;
-    for (size_t i = 0; i < n; ++i) pay_bytes = (size_t)i * kPayPitch + s.h_len[i];
-    if (hipMemcpyAsync(s.d_pay, s.h_pay, pay_bytes, hipMemcpyHostToDevice, st) != hipSuccess ||
+    if (hipMemcpyAsync(s.d_b0, s.h_b0, n, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemcpyAsync(s.d_len, s.h_len, 2 * n, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemcpyAsync(s.d_cmd, s.h_cmd, n, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemcpyAsync(s.d_id, s.h_id, 8 * n, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemcpyAsync(s.d_conv, s.h_conv, 4 * n, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemcpyAsync(s.d_key, s.h_key, 8 * n, hipMemcpyHostToDevice, st) != hipSuccess)
         return RSK_EDEVICE;
-    rsk_encode_in in{};
-    in.payload_arena = s.d_pay; in.pay_off = s.d_pay_off; in.pay_len = s.d_len; in.cmd = s.d_cmd;
-    in.conv = s.d_conv; in.conn_key = s.d_key; in.id = s.d_id;
-    rsk_encode_out out{};
-    out.frame_arena = s.d_frame; out.frame_off = s.d_frame_off; out.status = s.d_status;
-    out.flags = RSK_ENC_ZERO_PAD16;  // 1504-B slots: the pad never reaches the next frame
-    int r = rsk_encode_batch(ctx_, (uint32_t)n, &in, &out, st);
+    rsk_encode_hdr_in in{};
+    in.first_byte = s.d_b0; in.pay_len = s.d_len; in.cmd = s.d_cmd; in.conv = s.d_conv; in.conn_key = s.d_key;
+    in.id = s.d_id;
+    int r = rsk_encode_headers_batch(ctx_, (uint32_t)n, &in, s.d_hdr, s.d_status, st);
     if (r) return r;
-    const size_t frame_bytes = (n - 1) * kFramePitch + RSK_MAX_PKT_SIZE;  // covers the last frame
-    if (hipMemcpyAsync(s.h_frame, s.d_frame, frame_bytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
+    if (hipMemcpyAsync(s.h_hdr, s.d_hdr, 32 * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipMemcpyAsync(s.h_status, s.d_status, 4 * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipEventRecord(s.done, st) != hipSuccess)
         return RSK_EDEVICE;
@@ -198,8 +183,9 @@ int RConnGpu::deliver_enc(EncSlot &s) {
     if (hipEventSynchronize(s.done) != hipSuccess) return RSK_EDEVICE;
     for (uint32_t i = 0; i < s.count; ++i) {
         const int st = s.h_status[i];
-        if (st > 0 && send_cb_)
-            send_cb_(reinterpret_cast<const char *>(s.h_frame) + (size_t)i * kFramePitch, st, s.user[i]);
+        char *f = reinterpret_cast<char *>(s.frame) + (size_t)i * kFramePitch;
+        if (st > 0) std::memcpy(f, s.h_hdr + 32 * (size_t)i, RSK_HEAD_SIZE);  // tag | EncHead (RConn.cpp:101-103)
+        if (st > 0 && send_cb_) send_cb_(f, st, s.user[i]);
         ++n_sent_;
     }
     s.count = 0;
@@ -223,12 +209,12 @@ int RConnGpu::OnRecv(ssize_t nread, const char *base, bool tcp_close, void *user
     if (nread > 0xFFFF) nread = 0xFFFF;  // frame_len is u16 (a UDP datagram is at most 65507 B)
     DecSlot &s = dec_[dec_cur_];
     const uint32_t i = s.count;
-    // The kernel reads only frame bytes [0, 32) and frame[8 + len] (< 264), so a frame longer than
-    // its slot is staged by its first kFramePitch bytes with the true nread; the full copy is kept
-    // on the heap for the payload hand-off.
+    // the caller may reuse `base` after the call: keep a copy for the payload hand-off (frames
+    // longer than a slot on the heap); only the 32-B header slot goes to the GPU
     const size_t cp = (size_t)nread < kFramePitch ? (size_t)nread : kFramePitch;
-    if (cp) std::memcpy(s.h_frame + (size_t)i * kFramePitch, base, cp);
+    if (cp) std::memcpy(s.frame + (size_t)i * kFramePitch, base, cp);
     if ((size_t)nread > kFramePitch) s.big[i].assign(base, base + nread);
+    rsk_stage_decode_header(reinterpret_cast<const uint8_t *>(base), (int)nread, s.h_slot + 32 * (size_t)i);
     s.h_len[i] = (uint16_t)nread;
     s.h_close[i] = tcp_close ? 1 : 0;
     s.user[i] = user;
@@ -239,9 +225,7 @@ int RConnGpu::OnRecv(ssize_t nread, const char *base, bool tcp_close, void *user
 int RConnGpu::launch_dec(DecSlot &s) {
     const size_t n = s.count;
     hipStream_t st = s.stream;
-    const size_t last = s.h_len[n - 1] < kFramePitch ? s.h_len[n - 1] : kFramePitch;
-    const size_t frame_bytes = (n - 1) * kFramePitch + last;
-    if ((frame_bytes && hipMemcpyAsync(s.d_frame, s.h_frame, frame_bytes, hipMemcpyHostToDevice, st) != hipSuccess) ||
+    if (hipMemcpyAsync(s.d_slot, s.h_slot, 32 * n, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemcpyAsync(s.d_len, s.h_len, 2 * n, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemcpyAsync(s.d_close, s.h_close, n, hipMemcpyHostToDevice, st) != hipSuccess)
         return RSK_EDEVICE;
@@ -249,7 +233,7 @@ int RConnGpu::launch_dec(DecSlot &s) {
     dec_ptrs(s.d_out, o);
     o.valid_idx = nullptr;  // delivery walks every frame in order; no compaction needed
     o.n_valid = nullptr;
-    int r = rsk_decode_batch(ctx_, (uint32_t)n, s.d_frame, s.d_off, s.d_len, s.d_close, &o, st);
+    int r = rsk_decode_headers_batch(ctx_, (uint32_t)n, s.d_slot, s.d_len, s.d_close, &o, st);
     if (r) return r;
     if (hipMemcpyAsync(s.h_out, s.d_out, dec_out_bytes(), hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipEventRecord(s.done, st) != hipSuccess)
@@ -273,7 +257,7 @@ int RConnGpu::deliver_dec(DecSlot &s) {
             std::memcpy(rr.id, o.id + 8 * (size_t)i, 8);
             rr.conv = o.conv[i];
             rr.conn_key = o.conn_key[i];
-            const char *fb = s.big[i].empty() ? reinterpret_cast<const char *>(s.h_frame) + (size_t)i * kFramePitch
+            const char *fb = s.big[i].empty() ? reinterpret_cast<const char *>(s.frame) + (size_t)i * kFramePitch
                                               : s.big[i].data();
             rr.payload = fb + o.pay_off[i];
             rr.payload_len = o.pay_len[i];

@@ -2,10 +2,14 @@
 //
 // The reference frames and verifies one packet per call on the libuv thread
 // (conn/RConn.cpp:64-128).  RConnGpu keeps RConn's per-packet surface and return contract but
-// queues the packets into pinned staging buffers and runs each full batch (or an explicit Flush)
-// through rsk_encode_batch / rsk_decode_batch, double-buffered: while batch k is on the GPU
-// (H2D -> kernel -> D2H on its own stream), batch k+1 is being filled.  Results are delivered
-// through callbacks in input order, i.e. the order RConn would have produced them.
+// queues the packets and runs each full batch (or an explicit Flush) through the header-only
+// entry points rsk_encode_headers_batch / rsk_decode_headers_batch, double-buffered: while batch k
+// is on the GPU (H2D -> kernel -> D2H on its own stream), batch k+1 is being filled.  Only
+// payload[0] + descriptors go to the GPU on the send side and only the 32-B header slot on the
+// receive side; payloads stay in host frame slots (Output copies the payload to offset 31 of its
+// slot, as RConn.cpp:104 copies it into the stack frame; the 31 header bytes land in front at
+// delivery).  Results are delivered through callbacks in input order, i.e. the order RConn would
+// have produced them.
 //
 //   Output(nread, base, head, user)      <- RConn::Output(nread, rbuf) with rbuf.data->head
 //       nread < 0  -> returns nread (RConn.cpp:127)
@@ -79,16 +83,17 @@ private:
         bool in_flight = false;
         hipStream_t stream = nullptr;
         hipEvent_t done = nullptr;
+        uint8_t *frame = nullptr;  // host frames (pinned pages): payload copied to +31 at Output, header at delivery
         // pinned host
-        uint8_t *h_pay = nullptr, *h_frame = nullptr, *h_cmd = nullptr, *h_id = nullptr;
-        uint64_t *h_pay_off = nullptr, *h_frame_off = nullptr, *h_key = nullptr;
+        uint8_t *h_b0 = nullptr, *h_cmd = nullptr, *h_id = nullptr, *h_hdr = nullptr;
+        uint64_t *h_key = nullptr;
         uint16_t *h_len = nullptr;
         uint32_t *h_conv = nullptr;
         int32_t *h_status = nullptr;
         std::vector<void *> user;
         // device
-        uint8_t *d_pay = nullptr, *d_frame = nullptr, *d_cmd = nullptr, *d_id = nullptr;
-        uint64_t *d_pay_off = nullptr, *d_frame_off = nullptr, *d_key = nullptr;
+        uint8_t *d_b0 = nullptr, *d_cmd = nullptr, *d_id = nullptr, *d_hdr = nullptr;
+        uint64_t *d_key = nullptr;
         uint16_t *d_len = nullptr;
         uint32_t *d_conv = nullptr;
         int32_t *d_status = nullptr;
@@ -98,14 +103,13 @@ private:
         bool in_flight = false;
         hipStream_t stream = nullptr;
         hipEvent_t done = nullptr;
-        uint8_t *h_frame = nullptr, *h_close = nullptr;
-        uint64_t *h_off = nullptr;
+        uint8_t *frame = nullptr;            // host copies of the frames (payload hand-off; pinned pages)
+        std::vector<std::vector<char>> big;  // full copies of frames longer than a slot
+        uint8_t *h_slot = nullptr, *h_close = nullptr;  // pinned: 32-B header slots
         uint16_t *h_len = nullptr;
         uint8_t *h_out = nullptr;  // packed SoA outputs (see dec_ptrs)
         std::vector<void *> user;
-        std::vector<std::vector<char>> big;  // full copies of frames longer than a slot
-        uint8_t *d_frame = nullptr, *d_close = nullptr, *d_out = nullptr;
-        uint64_t *d_off = nullptr;
+        uint8_t *d_slot = nullptr, *d_close = nullptr, *d_out = nullptr;
         uint16_t *d_len = nullptr;
     };
 
