@@ -389,6 +389,98 @@ __global__ __launch_bounds__(kBlock) void k_encode(EncArgs a, KeySched ks) {
 }
 
 
+// Block-interleaved per-packet copy (A/B variant 11): phase 1 as usual, then the block's 256
+// packet records go through LDS and wave w copies packets w, w + 4, w + 8, ... so the 4 waves of a
+// block stream adjacent frames instead of four regions 92 KB apart.
+struct alignas(16) PktRec {
+    const uint8_t *src;
+    uint8_t *dst;
+    uint32_t H[8];
+    int32_t st;
+    uint32_t slow;
+    uint32_t pad_[2];
+};
+
+template <int PU>
+__global__ __launch_bounds__(kBlock) void k_encode_blk(EncArgs a, KeySched ks) {
+    __shared__ PktRec rec[kBlock];
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    {
+        const Lane1 L = encode_phase1(a, ks, i);
+        PktRec r;
+        r.src = a.payload + L.po;
+        r.dst = a.frame + L.fo;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) r.H[q] = L.H[q];
+        r.st = L.st;
+        r.slow = L.slow ? 1u : 0u;
+        r.pad_[0] = r.pad_[1] = 0;
+        rec[threadIdx.x] = r;
+    }
+    __syncthreads();
+    for (uint32_t k0 = 0; k0 < 64u; k0 += PU) {
+        uint4 A[PU][2], B[PU][2];
+        uint32_t flen[PU], sh[PU];
+        const uint8_t *srcp[PU];
+        uint8_t *dstp[PU];
+        bool on[PU];
+#pragma unroll
+        for (int p = 0; p < PU; ++p) {
+            const PktRec &R = rec[w + 4u * (k0 + p)];
+            on[p] = R.st > 0 && !R.slow;
+            flen[p] = on[p] ? (uint32_t)R.st : 0u;
+            sh[p] = (uint32_t)((reinterpret_cast<uintptr_t>(R.src) + 1u) & 15u);
+            srcp[p] = R.src + 1 - sh[p];
+            dstp[p] = R.dst;
+            const int32_t last_rel = (int32_t)flen[p] - RSK_HEAD_SIZE + (int32_t)sh[p] - 2;
+            const uint32_t nch = (flen[p] + 15u) >> 4;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const uint32_t k = lane + 64u * q;
+                A[p][q] = make_uint4(0u, 0u, 0u, 0u);
+                B[p][q] = make_uint4(0u, 0u, 0u, 0u);
+                if (k >= 2u && k < nch) {
+                    const uint32_t ro = 16u * (k - 2u);
+                    A[p][q] = ld16<0>(srcp[p] + ro);
+                    if (sh[p] != 0u && (int32_t)(ro + 16u) <= last_rel) B[p][q] = ld16<0>(srcp[p] + ro + 16u);
+                }
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < PU; ++p) {
+            if (!on[p]) continue;
+            const uint32_t nch = (padded_len(dstp[p], flen[p], a.pad) + 15u) >> 4;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const uint32_t k = lane + 64u * q;
+                if (k >= nch) continue;
+                uint4 v;
+                if (k >= 2u) {
+                    v = rsk::funnel16(A[p][q], B[p][q], sh[p]);
+                } else {
+                    const PktRec &R = rec[w + 4u * (k0 + p)];
+                    v = k == 0u ? make_uint4(R.H[0], R.H[1], R.H[2], R.H[3]) : make_uint4(R.H[4], R.H[5], R.H[6], R.H[7]);
+                }
+                store_last16<0>(dstp[p] + 16u * k, v, (int)flen[p] - 16 * (int)k, a.pad != 0u);
+            }
+        }
+    }
+    // frames that are not 16-B aligned: byte path, one packet at a time
+    for (uint32_t k = 0; k < 64u; ++k) {
+        const PktRec &R = rec[w + 4u * k];
+        if (R.st <= 0 || !R.slow) continue;
+        const uint32_t fl = (uint32_t)R.st, fend = padded_len(R.dst, fl, a.pad);
+        for (uint32_t f = lane; f < fend; f += 64u) {
+            uint32_t byte;
+            if (f >= fl) byte = 0;
+            else if (f < (uint32_t)RSK_HEAD_SIZE) byte = (R.H[f >> 2] >> (8u * (f & 3u))) & 0xffu;
+            else byte = rsk::gptr(R.src)[f - RSK_HEAD_SIZE];
+            rsk::gptr(R.dst)[f] = (uint8_t)byte;
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Encode straight to wire packets (RConn::Output + RawTcp::SendRawTcp / libnet)
 // ---------------------------------------------------------------------------------------------
@@ -1502,8 +1594,9 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 //   0 = hybrid<4,4> (default)   1 = pkt PU=1   2 = flat U=2    3 = flat U=4    4 = pkt PU=2
 //   5 = pkt PU=4                6 = hybrid nt-stores           7 = pkt PU=4 nt loads+stores
 //   8 = pkt PU=4 nt stores      9 = hybrid PU=2               10 = pkt PU=2 nt stores
+//  11 = block-interleaved pkt PU=4   12 = block-interleaved pkt PU=2
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
-    if (!c || v < 0 || v > 10) return RSK_EINVAL;
+    if (!c || v < 0 || v > 12) return RSK_EINVAL;
     c->enc_variant = v;
     return RSK_OK;
 }
@@ -1586,6 +1679,8 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         case 8: hipLaunchKernelGGL((k_encode<0, 4, 4, 2>), gd, bd, 0, st, a, c->ks); break;
         case 9: hipLaunchKernelGGL((k_encode<2, 2, 4, 0>), gd, bd, 0, st, a, c->ks); break;
         case 10: hipLaunchKernelGGL((k_encode<0, 2, 4, 2>), gd, bd, 0, st, a, c->ks); break;
+        case 11: hipLaunchKernelGGL((k_encode_blk<4>), gd, bd, 0, st, a, c->ks); break;
+        case 12: hipLaunchKernelGGL((k_encode_blk<2>), gd, bd, 0, st, a, c->ks); break;
         default: hipLaunchKernelGGL((k_encode<2, 4, 4, 0>), gd, bd, 0, st, a, c->ks); break;
     }
     return launch_check("k_encode");

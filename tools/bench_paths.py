@@ -84,6 +84,15 @@ def main():
     fnm = torch.empty(1, dtype=torch.int32, device=dev)
     filt = rc.make_filter(dst_singles=[10001, 10002], dst_ranges=[(20000, 30000)], is_server=True)
     ops["capture_filter"] = lambda: cx.capture_filter_batch(wiree, offe, ste, 1, filt, fmatch, fidx, fnm, stream=s)
+    # header-only kernels: contiguous 32-B slots (no dependent offset load, no scattered headers)
+    slots = w.frame[w.frame_off.view(-1, 1) + torch.arange(32, device=dev).view(1, -1)].reshape(-1).contiguous()
+    hdec = rc.DecodeBuffers.alloc(n, dev)
+    b0 = w.payload[w.pay_off].contiguous()
+    hslot = torch.empty(32 * n, dtype=torch.uint8, device=dev)
+    hst = torch.empty(n, dtype=torch.int32, device=dev)
+    ops["decode_hdr"] = lambda: cx.onrecv_headers_batch(slots, w.frame_len, hdec, stream=s)
+    ops["encode_hdr"] = lambda: cx.output_headers_batch(b0, w.pay_len, w.cmd, w.conv, w.conn_key, hslot, hst,
+                                                        id_uniform=workload.ID_UNIFORM, stream=s)
     # realistic connection counts: 64 conns, 0.1% control packets, every packet VALID
     gk = torch.Generator(device=dev)
     gk.manual_seed(7)
@@ -125,6 +134,8 @@ def main():
         "demux": 1 + 1 + 8 + 8 + 4,  # status, cmd, id, conn_key in; perm out (+ per-segment words)
         "demux_64conn": 1 + 1 + 8 + 8 + 4,
         "capture_filter": 8 + 4 + 64 + 16 + 1 + 4,  # cap_off, cap_len, header windows, match, match_idx
+        "decode_hdr": 32 + 2 + 27 + 4,
+        "encode_hdr": 1 + 2 + 1 + 4 + 8 + 32 + 4,
     }
     out = {}
     for k, t in times.items():
