@@ -294,6 +294,7 @@ typedef struct rsk_demux_out {
     uint32_t *n_seg;     /* [1]                                                                   */
     uint32_t *n_valid;   /* [1]                                                                   */
 } rsk_demux_out;
+/* n <= 2^30.  Workspace (per context, grown on demand): about 70 B per packet. */
 int rsk_demux_batch(rsk_ctx *ctx, uint32_t n, const rsk_demux_in *in, uint32_t fields,
                     const rsk_demux_out *out, void *stream);
 

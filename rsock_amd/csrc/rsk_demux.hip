@@ -451,10 +451,10 @@ struct DmWs {
     uint32_t nb, nt, tsize;
 };
 
-uint32_t table_size(uint32_t n) {
-    uint32_t t = 64;
-    while (t < 2u * n) t <<= 1;
-    return t;
+uint32_t table_size(uint32_t n) {  // power of two >= 2 n (n <= 2^30, checked by the entry point)
+    uint64_t t = 64;
+    while (t < 2ull * n) t <<= 1;
+    return (uint32_t)t;
 }
 
 size_t dm_layout(uint32_t n, uint8_t *base, DmWs *w) {
@@ -528,7 +528,7 @@ extern "C" int rsk_demux_batch(rsk_ctx *c, uint32_t n, const rsk_demux_in *in, u
     if (n && (fields & RSK_DEMUX_CONN_KEY) && !in->conn_key) return RSK_EINVAL;
     if (n && (fields & RSK_DEMUX_CONV) && !in->conv) return RSK_EINVAL;
     if (n && (fields & RSK_DEMUX_DST) && !in->dst) return RSK_EINVAL;
-    if (n > 0x7fffffffu) return RSK_EINVAL;
+    if (n > (1u << 30)) return RSK_EINVAL;  // table of 2^31 slots max (uint32 slot indices)
     rsk::DeviceGuard g(c->device);
     if (!g.ok) return RSK_EDEVICE;
     hipStream_t s = (hipStream_t)stream;
