@@ -42,6 +42,14 @@ constexpr uint32_t kScanChunk = 4096;           // elements per block in the mul
 
 __device__ __forceinline__ uint64_t lanemask_lt(uint32_t lane) { return (1ull << lane) - 1ull; }
 
+// XCD-aware tile index (bijective for any grid size): blocks are dealt round-robin over the 8 XCDs
+// (MI355X_MICROARCH.md), so block b runs tile xcd_tile(b) and each XCD streams a contiguous range of
+// tiles; the sectors two neighbouring tiles both write half of then meet in the same L2 (speed only).
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nwg) {
+    const uint32_t x = b % 8u, q = nwg / 8u, r = nwg % 8u;
+    return (x < r ? x * (q + 1u) : r * (q + 1u) + (x - r) * q) + b / 8u;
+}
+
 // ---- scans ----------------------------------------------------------------------------------
 // exclusive scan of 4096 u32 per pass by one 1024-thread block; carry across passes
 __device__ __forceinline__ void block_scan_4096(const uint32_t *in, uint32_t *out, uint32_t base, uint32_t cnt,
@@ -247,15 +255,20 @@ __global__ __launch_bounds__(kBlock) void k_dm_insert(DmIn a, const uint32_t *nv
         lmin[q] = kNone;
     }
     __syncthreads();
+    // (keys stay in registers; confirming another packet's key reads the immutable inputs: keeping
+    // the tile's keys in LDS too cost more occupancy than it saved, 157 -> 179 us on C3)
+    Key kr[kInsItems];
     uint32_t lpos[kInsItems];
 #pragma unroll
     for (uint32_t it = 0; it < kInsItems; ++it) {
         const uint32_t li = it * kBlock + t, j = base + li;
         lpos[it] = kNone;
+        kr[it] = Key{kCtrl, 0, 0, 0, 0};
         if (j >= nv) continue;
         const uint32_t ep = cep[j];
         if (ep == kCtrl) continue;
-        const Key k = load_key(a, cidx[j], ep);
+        kr[it] = load_key(a, cidx[j], ep);
+        const Key &k = kr[it];
         const uint64_t hv = key_hash(k);
         const uint32_t fp = (uint32_t)(hv >> 32);
         const unsigned long long mine = ((unsigned long long)fp << 32) | li;
@@ -285,7 +298,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_insert(DmIn a, const uint32_t *nv
     for (uint32_t it = 0; it < kInsItems; ++it) {
         if (!((rep >> it) & 1u)) continue;
         const uint32_t j = base + it * kBlock + t;
-        const Key k = load_key(a, cidx[j], cep[j]);
+        const Key &k = kr[it];
         const uint32_t gh = global_probe(a, cidx, cep, slots, mask, k, key_hash(k), j);
         if (__hip_atomic_load(tmin + gh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > j) atomicMin(tmin + gh, j);
         lmin[lpos[it]] = gh;
@@ -333,18 +346,21 @@ __global__ __launch_bounds__(kBlock) void k_dm_segof(const uint32_t *nvp, const 
 }
 
 // ---- stable LSD radix sort by segment id ------------------------------------------------------
-__device__ __forceinline__ uint32_t bits_for(uint32_t nseg) {  // digits needed for keys < nseg
+__device__ __forceinline__ uint32_t bits_for(uint32_t nseg) {  // bits of the largest key (< nseg)
     return nseg <= 1u ? 1u : 32u - (uint32_t)__builtin_clz(nseg - 1u);
 }
-__device__ __forceinline__ bool pass_live(uint32_t pass, uint32_t nseg) {
-    return pass == 0 || 8u * pass < bits_for(nseg);
+// passes = ceil(bits / 8); the digit width spreads the bits evenly over them (18 bits: 3 x 6, not
+// 8 + 8 + 2), so each pass has as few buckets as it can -> longer contiguous runs per tile
+__device__ __forceinline__ uint32_t n_passes(uint32_t nseg) { return (bits_for(nseg) + 7u) / 8u; }
+__device__ __forceinline__ uint32_t digit_width(uint32_t nseg) {
+    const uint32_t b = bits_for(nseg), p = (b + 7u) / 8u;
+    return (b + p - 1u) / p;
 }
 
 // lanes of this wave holding the same digit (valid lanes only)
-__device__ __forceinline__ uint64_t digit_peers(bool v, uint32_t d) {
+__device__ __forceinline__ uint64_t digit_peers(bool v, uint32_t d, uint32_t width) {
     uint64_t peers = __ballot(v);
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
+    for (uint32_t b = 0; b < width; ++b) {  // width is uniform
         const uint64_t m = __ballot(v && ((d >> b) & 1u));
         peers &= ((d >> b) & 1u) ? m : ~m;
     }
@@ -354,55 +370,101 @@ __device__ __forceinline__ uint64_t digit_peers(bool v, uint32_t d) {
 __global__ __launch_bounds__(kBlock) void k_dm_hist(uint32_t pass, const uint32_t *nvp, const uint32_t *nsegp,
                                                     const uint32_t *keys, uint32_t *hist, uint32_t nt) {
     __shared__ uint32_t lh[256];
-    const uint32_t nv = *nvp;
-    if (!pass_live(pass, *nsegp)) return;  // block-uniform
-    const uint32_t t = threadIdx.x, lane = t & 63u;
+    const uint32_t nv = *nvp, ns = *nsegp;
+    if (pass >= n_passes(ns)) return;  // block-uniform
+    const uint32_t width = digit_width(ns), sh = width * pass, dm = (1u << width) - 1u;
+    const uint32_t t = threadIdx.x, lane = t & 63u, tile = xcd_tile(blockIdx.x, gridDim.x);
     lh[t] = 0;
     __syncthreads();
-    const uint32_t sh = 8u * pass;
-    const uint32_t rounds = blockIdx.x * kTile < nv ? kItems : 0u;  // tiles past n_valid count zeros
-    for (uint32_t r = 0; r < rounds; ++r) {
-        const uint32_t k = blockIdx.x * kTile + r * kBlock + t;
-        const bool v = k < nv;
-        const uint32_t d = v ? (keys[k] >> sh) & 255u : 0u;
-        const uint64_t peers = digit_peers(v, d);
-        if (v && (peers & lanemask_lt(lane)) == 0) atomicAdd(&lh[d], (uint32_t)__popcll(peers));
+    if (tile * kTile < nv) {  // tiles past n_valid count zeros
+        uint32_t kk[kItems];  // all of the thread's loads in flight before the first ballot
+#pragma unroll
+        for (uint32_t r = 0; r < kItems; ++r) {
+            const uint32_t k = tile * kTile + r * kBlock + t;
+            kk[r] = k < nv ? keys[k] : 0u;
+        }
+#pragma unroll
+        for (uint32_t r = 0; r < kItems; ++r) {
+            const bool v = tile * kTile + r * kBlock + t < nv;
+            const uint32_t d = (kk[r] >> sh) & dm;
+            const uint64_t peers = digit_peers(v, d, width);
+            if (v && (peers & lanemask_lt(lane)) == 0) atomicAdd(&lh[d], (uint32_t)__popcll(peers));
+        }
     }
     __syncthreads();
-    hist[t * nt + blockIdx.x] = lh[t];
+    hist[t * nt + tile] = lh[t];  // bins >= 2^width stay 0
 }
 
+// Stable scatter of one tile: rank every item among the tile's equal digits (16 rounds of 256, in
+// input order), place it at its tile-local sorted position in LDS, then write the tile out digit
+// run by digit run — consecutive threads, consecutive addresses — so global stores are contiguous
+// runs instead of 4-B scatters (partially written sectors cost read-modify-write).
 __global__ __launch_bounds__(kBlock) void k_dm_scatter(uint32_t pass, const uint32_t *nvp, const uint32_t *nsegp,
                                                        const uint32_t *kin, const uint32_t *vin,
                                                        const uint32_t *hoff, uint32_t nt, uint32_t *kout,
                                                        uint32_t *vout) {
-    __shared__ uint32_t run[256];
+    __shared__ uint32_t run[256], lbase[256], dbase[256];
     __shared__ uint32_t wcnt[kWaves][256];
-    const uint32_t nv = *nvp;
-    if (!pass_live(pass, *nsegp) || blockIdx.x * kTile >= nv) return;  // block-uniform
+    __shared__ uint32_t sk[kTile], sv[kTile];
+    const uint32_t nv = *nvp, ns = *nsegp, tile = xcd_tile(blockIdx.x, gridDim.x);
+    if (pass >= n_passes(ns) || tile * kTile >= nv) return;  // block-uniform
+    const uint32_t width = digit_width(ns), sh = width * pass, dm = (1u << width) - 1u;
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    const uint32_t base = tile * kTile;
+    const uint32_t cnt = nv - base < kTile ? nv - base : kTile;
     run[t] = 0;
 #pragma unroll
     for (int q = 0; q < kWaves; ++q) wcnt[q][t] = 0;
-    const uint32_t base = hoff[t * nt + blockIdx.x];  // this tile's first slot for digit t
-    __shared__ uint32_t dbase[256];
-    dbase[t] = base;
+    dbase[t] = hoff[t * nt + tile];  // this tile's first global slot for digit t
     __syncthreads();
-    const uint32_t sh = 8u * pass;
+    // the thread's 16 items, all loads in flight at once (the rounds below are barrier-separated)
+    uint32_t kk[kItems], vv[kItems];
+#pragma unroll
     for (uint32_t r = 0; r < kItems; ++r) {
-        const uint32_t k = blockIdx.x * kTile + r * kBlock + t;
-        const bool v = k < nv;
-        const uint32_t key = v ? kin[k] : 0u;
-        const uint32_t d = (key >> sh) & 255u;
-        const uint64_t peers = digit_peers(v, d);
+        const uint32_t k = base + r * kBlock + t;
+        kk[r] = k < nv ? kin[k] : 0u;
+        vv[r] = k < nv ? vin[k] : 0u;
+    }
+    // tile histogram -> tile-local exclusive bases
+#pragma unroll
+    for (uint32_t r = 0; r < kItems; ++r) {
+        const bool v = base + r * kBlock + t < nv;
+        const uint32_t d = (kk[r] >> sh) & dm;
+        const uint64_t peers = digit_peers(v, d, width);
+        if (v && (peers & lanemask_lt(lane)) == 0) atomicAdd(&run[d], (uint32_t)__popcll(peers));
+    }
+    __syncthreads();
+    if (w == 0) {  // exclusive scan of the 256 bins by wave 0 (4 per lane)
+        uint32_t c[4], s4 = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { c[q] = run[4 * lane + q]; s4 += c[q]; }
+        uint32_t inc = s4;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t v = __shfl_up(inc, off);
+            if (lane >= (uint32_t)off) inc += v;
+        }
+        uint32_t acc = inc - s4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { lbase[4 * lane + q] = acc; acc += c[q]; }
+    }
+    __syncthreads();
+    run[t] = 0;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t r = 0; r < kItems; ++r) {
+        const bool v = base + r * kBlock + t < nv;
+        const uint32_t key = kk[r];
+        const uint32_t d = (key >> sh) & dm;
+        const uint64_t peers = digit_peers(v, d, width);
         const uint32_t lt = (uint32_t)__popcll(peers & lanemask_lt(lane));
         if (v && lt == 0) wcnt[w][d] = (uint32_t)__popcll(peers);
         __syncthreads();
         if (v) {
-            uint32_t pos = dbase[d] + run[d] + lt;
+            uint32_t pos = lbase[d] + run[d] + lt;
             for (uint32_t q = 0; q < w; ++q) pos += wcnt[q][d];
-            kout[pos] = key;
-            vout[pos] = vin[k];
+            sk[pos] = key;
+            sv[pos] = vv[r];
         }
         __syncthreads();
         uint32_t add = 0;
@@ -414,6 +476,12 @@ __global__ __launch_bounds__(kBlock) void k_dm_scatter(uint32_t pass, const uint
         run[t] += add;
         __syncthreads();
     }
+    for (uint32_t p = t; p < cnt; p += kBlock) {
+        const uint32_t key = sk[p], d = (key >> sh) & dm;
+        const uint32_t g = dbase[d] + (p - lbase[d]);
+        kout[g] = key;
+        vout[g] = sv[p];
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void k_dm_final(const uint32_t *nvp, const uint32_t *nsegp, const uint32_t *kA,
@@ -421,7 +489,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_final(const uint32_t *nvp, const 
                                                      uint32_t *perm, uint32_t *seg_off,
                                                      uint32_t *n_seg, uint32_t *n_valid) {
     const uint32_t nv = *nvp, ns = *nsegp;
-    const uint32_t passes = (bits_for(ns) + 7u) / 8u;  // effective passes; pass p writes B when p is even
+    const uint32_t passes = n_passes(ns);  // effective passes; pass p writes B when p is even
     const bool inB = ((passes - 1u) & 1u) == 0u;
     const uint32_t *keys = inB ? kB : kA;
     const uint32_t *vals = inB ? vB : vA;
