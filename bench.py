@@ -110,7 +110,9 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4"])
+    ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4", "c5"],
+                    help="c2/c3/c4: that config per GPU (weak scaling); c5: BASELINE config 5, 64M 1400-B "
+                         "packets in total split over the ranks (strong scaling; 1 GPU holds all 64M: ~185 GB)")
     ap.add_argument("--packets", type=int, default=0, help="packets per GPU (default: the config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1 << 20)
@@ -141,9 +143,16 @@ def main() -> None:
             dist.init_process_group(args.dist_backend)
 
     cfg = args.config
-    n = args.packets or workload.CONFIGS[cfg][1]
-    # weak scaling: rank r owns packets [r*n, (r+1)*n) of the config's global stream
-    d = workload.describe(cfg, rank * n, (rank + 1) * n, n=world * n)
+    strong = cfg == "c5"
+    if strong:
+        # strong scaling: the config's total is split over the ranks (contiguous shards)
+        n_total = args.packets or workload.CONFIGS[cfg][1]
+        lo, hi = workload.shard_range(n_total, rank, world)
+        d = workload.describe(cfg, lo, hi, n=n_total)
+    else:
+        n = args.packets or workload.CONFIGS[cfg][1]
+        # weak scaling: rank r owns packets [r*n, (r+1)*n) of the config's global stream
+        d = workload.describe(cfg, rank * n, (rank + 1) * n, n=world * n)
     w = workload.DeviceWorkload(d, dev)
     cx = rc.Codec(b"hello135", gpu)
     cx.reserve(d.n)
@@ -187,7 +196,7 @@ def main() -> None:
 
     enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
-    total_pkts = world * d.n * args.steps
+    total_pkts = (n_total if strong else world * d.n) * args.steps
     mpkts = total_pkts / elapsed_max / 1e6
     p = int(d.pay_len[0]) if workload.CONFIGS[cfg][2] == workload.CONFIGS[cfg][3] else int(d.pay_len.mean())
     bytes_step = d.n * (enc_bytes_per_pkt(p) + dec_bytes_per_pkt())
@@ -205,7 +214,7 @@ def main() -> None:
             "warmup": args.warmup,
             "ms_per_step": round(elapsed_max / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (splitmix64 payloads/fields, SURVEY.md §8d)",
@@ -213,6 +222,7 @@ def main() -> None:
                 "workload": f"{cfg.upper()}: {d.n} packets/GPU, {p}-B payloads, encode(tag+EncHead+copy) then "
                             f"decode+verify+compact, device-resident",
                 "packets_per_gpu": d.n,
+                "packets_total": n_total if strong else world * d.n,
                 "payload_bytes": p,
                 "key": "hello135",
                 "parallelism": f"shard{world} (no collective)",
