@@ -1,16 +1,23 @@
 // rsk_kernels.hip — MI355X (gfx950) HIP implementation of the rsock framing codec + its C ABI.
 //
-// Kernels (DESIGN.md §Kernels has the roofline and the algorithmic bytes of each):
-//   k_encode        RConn::Output framing (conn/RConn.cpp:87-105): per 64-packet tile, one lane per
-//                   packet computes status, the MD5 tag and the 31 header bytes; then the whole wave
-//                   streams each frame as 16-B chunks (wave-cooperative, coalesced, funnel-shifted
-//                   payload loads, v_alignbyte).
+// Kernels (DESIGN.md §4 has the roofline and the algorithmic bytes of each):
+//   k_encode        RConn::Output framing (conn/RConn.cpp:87-105): per 64-packet set, one lane per
+//                   packet computes status, the MD5 tag and the 31 header bytes; then, per wave, the
+//                   per-packet path (the wave streams each frame as 16-B chunks, funnel-shifted
+//                   payload loads) or the flat chunk list for short frames.  k_encode_blk: A/B variant.
+//   k_encode_wire   RConn::Output + RawTcp::SendRawTcp (conn/RawTcp.cpp:280-341): frames plus the
+//                   IPv4/TCP headers and checksums libnet writes, two-launch hybrid.
+//   k_encode_hdr /  header-only framing / verification on 32-B slots (host-resident deployments:
+//   k_decode_hdr    the payload never crosses PCIe).
 //   k_decode        RConn::OnRecv (conn/RConn.cpp:64-85): one lane per frame, 32-B header window,
 //                   MD5 verify, SoA field stores, per-wave ballot mask + per-block count.
 //   k_parse_decode  RawTcp::RawInput (conn/RawTcp.cpp:138-244) fused with k_decode's body.
+//   k_capture_filter the pcap predicate of BuildFilterStr (cap/cap_util.cpp:67-144), SURVEY §8f-4.
 //   k_scan/k_scatter order-stable compaction of the VALID indices from the ballot masks.
 //   k_tcpinfo_encode 21-B TcpInfo hand-off records (bean/TcpInfo.cpp:20-32), staged through LDS.
+//   k_shim          the single-call shims (reference signatures) on a batch of one.
 //   k_fill_splitmix synthetic workload generator (bench/tests only).
+// The receive demux is in rsk_demux.hip; host batch helpers in rsk_host.cpp.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
