@@ -3,8 +3,9 @@
 // Kernels (DESIGN.md §4 has the roofline and the algorithmic bytes of each):
 //   k_encode        RConn::Output framing (conn/RConn.cpp:87-105): per 64-packet set, one lane per
 //                   packet computes status, the MD5 tag and the 31 header bytes; then, per wave, the
-//                   per-packet path (the wave streams each frame as 16-B chunks, funnel-shifted
-//                   payload loads) or the flat chunk list for short frames.  k_encode_blk: A/B variant.
+//                   per-packet path (the wave streams 16 frames at a time as 16-B chunks, one aligned
+//                   payload load per chunk, funnel partner from the next lane by DPP) or the flat
+//                   chunk list for short frames.  k_encode_blk and the two-load copy: A/B variants.
 //   k_encode_wire   RConn::Output + RawTcp::SendRawTcp (conn/RawTcp.cpp:280-341): frames plus the
 //                   IPv4/TCP headers and checksums libnet writes, two-launch hybrid.
 //   k_encode_hdr /  header-only framing / verification on 32-B slots (host-resident deployments:
@@ -218,6 +219,68 @@ __device__ __forceinline__ void copy_pkt(const EncArgs &a, const Lane1 &L, uint3
     }
 }
 
+// ---- per-packet copy, one load per chunk: lane k loads aligned source chunk k - 2 and takes the
+// second funnel operand (chunk k - 1) from lane k + 1 by a DPP wave shift (lane 63 of slot 0 from
+// lane 0 of slot 1), so a packet holds 2 instead of 4 uint4 registers per lane and more waves fit
+// per SIMD.  The shifts run with every lane active (DPP reads disabled lanes as 0). -------------
+__device__ __forceinline__ uint32_t wave_shl1(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false);  // wave_shl:1
+}
+
+template <int PU, int NT>
+__device__ __forceinline__ void copy_pkt_dpp(const EncArgs &a, const Lane1 &L, uint32_t lane, uint64_t vm) {
+    while (vm) {
+        uint32_t js[PU];
+        bool on[PU];
+#pragma unroll
+        for (int p = 0; p < PU; ++p) {
+            on[p] = vm != 0ull;
+            js[p] = on[p] ? (uint32_t)__builtin_ctzll(vm) : 0u;
+            if (on[p]) vm &= vm - 1ull;
+        }
+        uint4 A[PU][2];
+        uint8_t *dstp[PU];
+        uint32_t flen[PU], sh[PU];
+#pragma unroll
+        for (int p = 0; p < PU; ++p) {
+            flen[p] = on[p] ? rdl((uint32_t)L.st, js[p]) : 0u;
+            const uint8_t *src = a.payload + rdl64(L.po, js[p]);
+            dstp[p] = a.frame + rdl64(L.fo, js[p]);
+            sh[p] = (uint32_t)((reinterpret_cast<uintptr_t>(src) + 1u) & 15u);
+            const uint8_t *srcp = src + 1 - sh[p];  // aligned source chunk m = payload bytes around [16m-sh+1, ...)
+            const int32_t last_rel = (int32_t)flen[p] - RSK_HEAD_SIZE + (int32_t)sh[p] - 2;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const uint32_t k = lane + 64u * q;
+                A[p][q] = make_uint4(0u, 0u, 0u, 0u);
+                if (on[p] && k >= 2u && (int32_t)(16u * (k - 2u)) <= last_rel) A[p][q] = ld16<NT>(srcp + 16u * (k - 2u));
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < PU; ++p) {
+            if (!on[p]) continue;
+            uint4 B[2];
+            B[0] = make_uint4(wave_shl1(A[p][0].x), wave_shl1(A[p][0].y), wave_shl1(A[p][0].z), wave_shl1(A[p][0].w));
+            B[1] = make_uint4(wave_shl1(A[p][1].x), wave_shl1(A[p][1].y), wave_shl1(A[p][1].z), wave_shl1(A[p][1].w));
+            if (lane == 63u)
+                B[0] = make_uint4(rdl(A[p][1].x, 0), rdl(A[p][1].y, 0), rdl(A[p][1].z, 0), rdl(A[p][1].w, 0));
+            uint32_t Hj[8];  // packet's head words, read out in uniform control flow (SGPRs)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) Hj[t] = rdl(L.H[t], js[p]);
+            const uint32_t nch = (padded_len(dstp[p], flen[p], a.pad) + 15u) >> 4;  // chunks stored
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const uint32_t k = lane + 64u * q;
+                if (k >= nch) continue;
+                uint4 v;
+                if (k >= 2u) v = rsk::funnel16(A[p][q], B[q], sh[p]);
+                else v = k == 0u ? make_uint4(Hj[0], Hj[1], Hj[2], Hj[3]) : make_uint4(Hj[4], Hj[5], Hj[6], Hj[7]);
+                store_last16<NT>(dstp[p] + 16u * k, v, (int)flen[p] - 16 * (int)k, a.pad != 0u);
+            }
+        }
+    }
+}
+
 // ---- flat copy: the payload chunks (k >= 2) of every packet in `vm` as one list of 16-B chunks;
 // lane l of iteration t takes chunk g = 64(U t + u) + l and finds its packet by a 6-step binary
 // search over the tile's prefix sums in this wave's LDS slice.  Chunks 0 and 1 (frame bytes
@@ -369,7 +432,7 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
     const bool vec = L.st > 0 && !L.slow;
     const uint64_t vm = __ballot(vec);
     bool flat = MODE == 1;
-    if constexpr (MODE == 2) {
+    if constexpr (MODE == 2 || MODE == 3) {
         // set mean frame length over framed packets (wave reduction)
         uint32_t fl = vec ? (uint32_t)L.st : 0u;
 #pragma unroll
@@ -378,11 +441,13 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
         flat = fl < kFlatBelowMeanBytes * cnt;
     }
     if (flat) copy_flat<U, NT>(a, L, lane, vec, recs, cend);
+    else if constexpr (MODE >= 3) copy_pkt_dpp<PU, NT>(a, L, lane, vm);
     else copy_pkt<PU, NT>(a, L, lane, vm);
     copy_bytes(a, L, lane, __ballot(L.st > 0 && L.slow));
 }
 
-// MODE: 0 per-packet, 1 flat, 2 hybrid (per-wave choice).
+// MODE: 0 per-packet, 1 flat, 2 hybrid (per-wave choice), 3 hybrid with the DPP per-packet copy,
+// 4 DPP per-packet only.
 // Tiled mapping: wave t takes packets [64t, 64t + 64) (coalesced descriptor loads, but the 5000+
 // co-resident waves each stream their own ~92 KB region).
 template <int MODE, int PU, int U, int NT>
@@ -1595,15 +1660,18 @@ const char *rsk_last_error(void) { return g_last_error; }
 const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 
 // Internal tuning knob (not part of include/rsk_codec.h): selects the encode kernel variant for
-// in-process A/B measurements.  k_encode<MODE, PU, U, NT>: MODE 0 per-packet, 1 flat, 2 hybrid;
-// PU packets per per-packet iteration; U chunks per lane per flat iteration; NT bit0 nontemporal
-// loads, bit1 nontemporal stores.
-//   0 = hybrid<4,4> (default)   1 = pkt PU=1   2 = flat U=2    3 = flat U=4    4 = pkt PU=2
+// in-process A/B measurements.  k_encode<MODE, PU, U, NT>: MODE 0 per-packet, 1 flat, 2 hybrid,
+// 3 hybrid with the one-load DPP per-packet copy, 4 DPP per-packet only; PU packets per per-packet
+// iteration; U chunks per lane per flat iteration; NT bit0 nontemporal loads, bit1 nontemporal stores.
+//   0 = hybrid-DPP<16,4> (default)  1 = pkt PU=1   2 = flat U=2    3 = flat U=4    4 = pkt PU=2
 //   5 = pkt PU=4                6 = hybrid nt-stores           7 = pkt PU=4 nt loads+stores
 //   8 = pkt PU=4 nt stores      9 = hybrid PU=2               10 = pkt PU=2 nt stores
 //  11 = block-interleaved pkt PU=4   12 = block-interleaved pkt PU=2
+//  13 = two-load hybrid<4,4> (the default before the DPP copy)
+//  14/15/16 = hybrid-DPP PU=4/8/12   17 = DPP per-packet only PU=16
+// v + 100 * cap (cap 1..4): the same kernel held to `cap` blocks per CU by unused dynamic LDS.
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
-    if (!c || v < 0 || v > 12) return RSK_EINVAL;
+    if (!c || v < 0 || v % 100 > 17 || v / 100 > 4) return RSK_EINVAL;
     c->enc_variant = v;
     return RSK_OK;
 }
@@ -1675,7 +1743,15 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
     const unsigned grid = (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
     hipStream_t st = (hipStream_t)stream;
     const dim3 gd(grid), bd(kBlock);
-    switch (c->enc_variant) {
+    // A/B only: variant + 100 * cap limits residency to `cap` blocks per CU through unused dynamic LDS
+    const int cap = c->enc_variant / 100;
+    const size_t lds = cap ? (size_t)(163840 / cap) - 16384 : 0;
+    switch (c->enc_variant % 100) {
+        case 13: hipLaunchKernelGGL((k_encode<2, 4, 4, 0>), gd, bd, lds, st, a, c->ks); break;
+        case 14: hipLaunchKernelGGL((k_encode<3, 4, 4, 0>), gd, bd, lds, st, a, c->ks); break;
+        case 15: hipLaunchKernelGGL((k_encode<3, 8, 4, 0>), gd, bd, lds, st, a, c->ks); break;
+        case 16: hipLaunchKernelGGL((k_encode<3, 12, 4, 0>), gd, bd, lds, st, a, c->ks); break;
+        case 17: hipLaunchKernelGGL((k_encode<4, 16, 4, 0>), gd, bd, lds, st, a, c->ks); break;
         case 1: hipLaunchKernelGGL((k_encode<0, 1, 4, 0>), gd, bd, 0, st, a, c->ks); break;
         case 2: hipLaunchKernelGGL((k_encode<1, 4, 2, 0>), gd, bd, 0, st, a, c->ks); break;
         case 3: hipLaunchKernelGGL((k_encode<1, 4, 4, 0>), gd, bd, 0, st, a, c->ks); break;
@@ -1688,7 +1764,7 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         case 10: hipLaunchKernelGGL((k_encode<0, 2, 4, 2>), gd, bd, 0, st, a, c->ks); break;
         case 11: hipLaunchKernelGGL((k_encode_blk<4>), gd, bd, 0, st, a, c->ks); break;
         case 12: hipLaunchKernelGGL((k_encode_blk<2>), gd, bd, 0, st, a, c->ks); break;
-        default: hipLaunchKernelGGL((k_encode<2, 4, 4, 0>), gd, bd, 0, st, a, c->ks); break;
+        default: hipLaunchKernelGGL((k_encode<3, 16, 4, 0>), gd, bd, lds, st, a, c->ks); break;
     }
     return launch_check("k_encode");
 }
