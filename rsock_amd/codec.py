@@ -240,8 +240,8 @@ class Codec:
         _check(fn(self._ctx, v), "rsk__set_encode_variant")
 
     def set_wire_variant(self, v: int) -> None:
-        """Internal tuning knob for k_encode_wire: 0 two-launch hybrid (default), 1 per-packet, 2 flat,
-        3 one-launch hybrid."""
+        """Internal tuning knob for k_encode_wire: 0 two-launch hybrid with the DPP per-packet copy
+        (default), 1 per-packet, 2 flat, 3 one-launch hybrid, 4-7 A/B variants (rsk_kernels.hip)."""
         fn = lib().rsk__set_wire_variant
         fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
         _check(fn(self._ctx, v), "rsk__set_wire_variant")

@@ -739,6 +739,85 @@ __device__ __forceinline__ void copy_wire_pkt(const EncArgs &a, const Lane1 &L, 
     }
 }
 
+// ---- the same with one aligned load per chunk: the funnel partner comes from lane + 1 by DPP (as
+// copy_pkt_dpp), all PU packets' loads issued before the first shift. ------------------------------
+template <int E, int PU>
+__device__ __forceinline__ void copy_wire_pkt_dpp(const EncArgs &a, const Lane1 &L, const uint32_t *stage,
+                                                  uint32_t sum_pre, int32_t wst, uint32_t lane, uint64_t vm) {
+    using G = WireGeom<E>;
+    while (vm) {
+        uint32_t js[PU];
+        bool on[PU];
+#pragma unroll
+        for (int p = 0; p < PU; ++p) {
+            on[p] = vm != 0ull;
+            js[p] = on[p] ? (uint32_t)__builtin_ctzll(vm) : 0u;
+            if (on[p]) vm &= vm - 1ull;
+        }
+        uint4 A[PU][2];
+        uint32_t wlen[PU], shp[PU];
+        uint8_t *dstp[PU];
+#pragma unroll
+        for (int p = 0; p < PU; ++p) {
+            wlen[p] = on[p] ? (uint32_t)rdl((uint32_t)wst, js[p]) : 0u;
+            const uint32_t P = wlen[p] - G::HB;
+            const uint8_t *pay = a.payload + rdl64(L.po, js[p]);
+            dstp[p] = a.frame + rdl64(L.fo, js[p]);
+            shp[p] = (uint32_t)((reinterpret_cast<uintptr_t>(pay) + G::D0) & 15u);
+            const uint8_t *src_al = pay + G::D0 - shp[p];
+            const int32_t last_rel = (int32_t)P - 1 - G::D0 + (int32_t)shp[p];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const uint32_t m = lane + 64u * q;  // source chunk of frame chunk NPRE + m
+                A[p][q] = make_uint4(0u, 0u, 0u, 0u);
+                if (on[p] && (int32_t)(16u * m) <= last_rel) A[p][q] = ld16<0>(src_al + 16u * m);
+            }
+        }
+        uint4 v[PU][2];
+        uint32_t ck[PU];
+#pragma unroll
+        for (int p = 0; p < PU; ++p) {
+            uint4 B[2];
+            B[0] = make_uint4(wave_shl1(A[p][0].x), wave_shl1(A[p][0].y), wave_shl1(A[p][0].z), wave_shl1(A[p][0].w));
+            B[1] = make_uint4(wave_shl1(A[p][1].x), wave_shl1(A[p][1].y), wave_shl1(A[p][1].z), wave_shl1(A[p][1].w));
+            if (lane == 63u)
+                B[0] = make_uint4(rdl(A[p][1].x, 0), rdl(A[p][1].y, 0), rdl(A[p][1].z, 0), rdl(A[p][1].w, 0));
+            const uint32_t nch = (wlen[p] + 15u) >> 4;
+            uint32_t part = 0;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const uint32_t k = G::NPRE + lane + 64u * q;
+                v[p][q] = rsk::funnel16(A[p][q], B[q], shp[p]);
+                const int lim = (int)wlen[p] - 16 * (int)k;
+                if (k < nch) {
+                    if (lim < 16) v[p][q] = rsk::keep_bytes16(v[p][q], lim);
+                    part += hsum(v[p][q].x) + hsum(v[p][q].y) + hsum(v[p][q].z) + hsum(v[p][q].w);
+                }
+            }
+            ck[p] = part;
+        }
+#pragma unroll
+        for (int p = 0; p < PU; ++p) ck[p] = ~fold16(wave_sum(ck[p]) + rdl(sum_pre, js[p])) & 0xffffu;
+#pragma unroll
+        for (int p = 0; p < PU; ++p) {
+            if (!on[p]) continue;
+            const uint32_t nst = (padded_len(dstp[p], wlen[p], a.pad) + 15u) >> 4;
+            if (lane < (uint32_t)G::NPRE && lane < nst) {
+                const uint4 sv = *reinterpret_cast<const uint4 *>(stage + js[p] * G::NPW + 4u * lane);
+                uint32_t w4[4] = {sv.x, sv.y, sv.z, sv.w};
+                if (lane == (uint32_t)(G::CK / 16)) w4[(G::CK & 15) >> 2] |= ck[p] << (8 * (G::CK & 3));
+                store_last16<0>(dstp[p] + 16u * lane, make_uint4(w4[0], w4[1], w4[2], w4[3]),
+                                (int)wlen[p] - 16 * (int)lane, a.pad != 0u);
+            }
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const uint32_t k = G::NPRE + lane + 64u * q;
+                if (k < nst) store_last16<0>(dstp[p] + 16u * k, v[p][q], (int)wlen[p] - 16 * (int)k, a.pad != 0u);
+            }
+        }
+    }
+}
+
 // ---- flat copy for short packets, two passes over the set: (1) the payload chunks of all packets as
 // one flat chunk list (as copy_flat), each lane adding its chunk's halfword sum into the packet's
 // LDS slot; (2) the NPRE prefix chunks of every packet as a dense (packet, chunk) grid read from the
@@ -950,7 +1029,8 @@ __global__ __launch_bounds__(kBlock) void k_encode_wire(EncArgs a, WireArgs wa, 
     }
     if (!flat) {
         wave_lds_sync();
-        copy_wire_pkt<E, PU>(a, L, stage, sum_pre, wst, lane, vm);
+        if constexpr (PU >= 100) copy_wire_pkt_dpp<E, PU - 100>(a, L, stage, sum_pre, wst, lane, vm);
+        else copy_wire_pkt<E, PU>(a, L, stage, sum_pre, wst, lane, vm);
     }
     const uint64_t sm = __ballot(L.st > 0 && L.slow);
     if (sm) {
@@ -1676,10 +1756,12 @@ int rsk__set_encode_variant(rsk_ctx *c, int v) {
     return RSK_OK;
 }
 
-// Internal (A/B and tests): wire-build copy path.  0 = two-launch hybrid (default), 1 = per-packet,
-// 2 = flat, 3 = one-launch hybrid.
+// Internal (A/B and tests): wire-build copy path.  0 = two-launch hybrid whose per-packet half uses the
+// one-load DPP copy, 8 packets per iteration (default), 1 = per-packet, 2 = flat, 3 = one-launch
+// hybrid, 4 = two-launch hybrid with the two-load copy PU=2 (the default before), 5 = the same PU=4,
+// 6 / 7 = DPP copy PU=4 / 16.
 int rsk__set_wire_variant(rsk_ctx *c, int v) {
-    if (!c || v < 0 || v > 3) return RSK_EINVAL;
+    if (!c || v < 0 || v > 7) return RSK_EINVAL;
     c->wire_variant = v;
     return RSK_OK;
 }
@@ -1803,12 +1885,20 @@ int rsk_encode_wire_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const
         if (v == 1) RSK_WIRE(14, 0, 2, 4);
         else if (v == 2) RSK_WIRE(14, 1, 2, 2);
         else if (v == 3) RSK_WIRE(14, 2, 2, 2);
-        else { RSK_WIRE(14, 3, 2, 2); RSK_WIRE(14, 4, 2, 2); }
+        else if (v == 4) { RSK_WIRE(14, 3, 2, 2); RSK_WIRE(14, 4, 2, 2); }
+        else if (v == 5) { RSK_WIRE(14, 3, 4, 2); RSK_WIRE(14, 4, 2, 2); }
+        else if (v == 6) { RSK_WIRE(14, 3, 104, 2); RSK_WIRE(14, 4, 2, 2); }
+        else if (v == 7) { RSK_WIRE(14, 3, 116, 2); RSK_WIRE(14, 4, 2, 2); }
+        else { RSK_WIRE(14, 3, 108, 2); RSK_WIRE(14, 4, 2, 2); }
     } else {
         if (v == 1) RSK_WIRE(0, 0, 2, 4);
         else if (v == 2) RSK_WIRE(0, 1, 2, 2);
         else if (v == 3) RSK_WIRE(0, 2, 2, 2);
-        else { RSK_WIRE(0, 3, 2, 2); RSK_WIRE(0, 4, 2, 2); }
+        else if (v == 4) { RSK_WIRE(0, 3, 2, 2); RSK_WIRE(0, 4, 2, 2); }
+        else if (v == 5) { RSK_WIRE(0, 3, 4, 2); RSK_WIRE(0, 4, 2, 2); }
+        else if (v == 6) { RSK_WIRE(0, 3, 104, 2); RSK_WIRE(0, 4, 2, 2); }
+        else if (v == 7) { RSK_WIRE(0, 3, 116, 2); RSK_WIRE(0, 4, 2, 2); }
+        else { RSK_WIRE(0, 3, 108, 2); RSK_WIRE(0, 4, 2, 2); }
     }
 #undef RSK_WIRE
     return launch_check("k_encode_wire");

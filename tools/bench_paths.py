@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--wire-align", type=int, default=16, help="wire packet pitch alignment (bytes)")
+    ap.add_argument("--wire-variants", default="", help="also time these rsk__set_wire_variant values (A/B)")
     args = ap.parse_args()
     import torch
 
@@ -72,6 +73,13 @@ def main():
         "decode": lambda: cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, w.dec, stream=s),
         "parse_decode": lambda: cx.rawinput_batch(wiree, offe, ste, ste, 1, 0, tcp, pdec, stream=s),
     }
+    for v in [int(x) for x in args.wire_variants.split(",") if x]:
+        ops[f"encode_wire_raw4_v{v}"] = (lambda v=v: (cx.set_wire_variant(v), cx.output_wire_batch(
+            *common, src, dst, sp, dp, seq, ack, flag, ipid, wire4, off4, st4, id_uniform=workload.ID_UNIFORM,
+            pad16=True, stream=s), cx.set_wire_variant(0)))
+        ops[f"encode_wire_eth_v{v}"] = (lambda v=v: (cx.set_wire_variant(v), cx.output_wire_batch(
+            *common, src, dst, sp, dp, seq, ack, flag, ipid, wiree, offe, ste, eth=eth, id_uniform=workload.ID_UNIFORM,
+            pad16=True, stream=s), cx.set_wire_variant(0)))
     # receive demux on the decoded fields (frames of this config; C4 marks 1/16 corrupted, 5% control)
     w.corrupt_frames()
     dmx = rc.DemuxBuffers.alloc(n, dev)
@@ -140,7 +148,8 @@ def main():
     out = {}
     for k, t in times.items():
         m = float(np.median(t))
-        out[k] = {"ms": round(m, 4), "Mpkt_s": round(n / m / 1e3, 1), "GBps_alg": round(n * alg[k] / m / 1e6, 1)}
+        a = alg.get(k, alg["encode_wire_eth" if "_eth_" in k else "encode_wire_raw4"])
+        out[k] = {"ms": round(m, 4), "Mpkt_s": round(n / m / 1e3, 1), "GBps_alg": round(n * a / m / 1e6, 1)}
     print(json.dumps({"config": args.config, "packets": n, "wire_pitch": [p4, pe], "demux_segments": nseg,
                       "paths": out}))
 
