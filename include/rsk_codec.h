@@ -15,6 +15,7 @@
  *   rsk_encode_batch      <- int RConn::Output(ssize_t, const rbuf_t&), framing part          conn/RConn.h:37, conn/RConn.cpp:87-105
  *   rsk_decode_batch      <- int RConn::OnRecv(ssize_t, const rbuf_t&)                        conn/RConn.h:34, conn/RConn.cpp:64-85
  *   rsk_parse_decode_batch<- int RawTcp::RawInput(u_char*, const pcap_pkthdr*, const u_char*) conn/RawTcp.h:38, conn/RawTcp.cpp:138-237
+ *   rsk_parse_decode_slots_batch <- the same on host-staged header slots (payloads stay in the capture buffer)
  *                            + RawTcp::cap2uv size check (RawTcp.cpp:239-244) fused with RConn::OnRecv
  *   rsk_tcpinfo_encode_batch <- char* TcpInfo::Encode(char*, int) (21-B hand-off record)      bean/TcpInfo.cpp:20-32, bean/ConnInfo.cpp:12-20
  *   rsk_encode_wire_batch <- RConn::Output + RawTcp::SendRawTcp -> libnet_build_tcp/ipv4     conn/RawTcp.cpp:280-341
@@ -91,6 +92,8 @@ extern "C" {
 #define RSK_PARSE_MALFORMED 3 /* header runs past cap_len, or negative payload_len with FIN|RST
                                  (the reference memcpy's a negative length there: UB,
                                  RawTcp.cpp:251) — defined here as a drop                      */
+#define RSK_PARSE_SLOT_SHORT 4 /* rsk_parse_decode_slots_batch only: a byte the parse or decode
+                                  reads lies past the staged slot; resubmit the packet whole   */
 
 /* parse flags */
 #define RSK_PARSE_HAS_ACK_POOL 0x1 /* RawTcp::mTcpAckPool != nullptr                          */
@@ -256,6 +259,23 @@ typedef struct rsk_tcpinfo_out {
 int rsk_parse_decode_batch(rsk_ctx *ctx, uint32_t n, const uint8_t *cap_arena, const uint64_t *cap_off,
                            const uint32_t *wire_len, const uint32_t *cap_len, int datalink, int flags,
                            const rsk_tcpinfo_out *tcp, const rsk_decode_out *dec, void *stream);
+
+/* Host-resident capture (copy only the first ~86 B of each captured packet, keep the
+ * payloads host-side): packet i's first min(cap_len[i], slot) bytes at slots + slot * i (slot a
+ * multiple of 16, >= RSK_CAP_SLOT_MIN; slots 16-B aligned), staged by rsk_stage_capture_slots.  Same
+ * outputs as rsk_parse_decode_batch on the whole capture (decisions use the real cap_len), except
+ * that a packet whose parse or decode must read a byte past its slot (IP/TCP options, an EncHead
+ * len byte that moves the hashed byte) gets parse_status RSK_PARSE_SLOT_SHORT with zero outputs
+ * and dec->status RSK_RECV_DROP: resubmit those through rsk_parse_decode_batch.  With slot = 96 a
+ * rsock packet (IHL 5, data offset 5, len 23) needs 86 B (EN10MB) or 76 B (NULL). */
+#define RSK_CAP_SLOT_MIN 64
+int rsk_parse_decode_slots_batch(rsk_ctx *ctx, uint32_t n, const uint8_t *slots, uint32_t slot,
+                                 const uint32_t *wire_len, const uint32_t *cap_len, int datalink, int flags,
+                                 const rsk_tcpinfo_out *tcp, const rsk_decode_out *dec, void *stream);
+/* Host: stage the slots of n captured packets at arena + cap_off[i] (first min(cap_len[i], slot)
+ * bytes, the rest of the slot zeroed). */
+int rsk_stage_capture_slots(uint32_t n, const uint8_t *arena, const uint64_t *cap_off, const uint32_t *cap_len,
+                            uint32_t slot, uint8_t *slots, int nthreads);
 
 /* ---- TcpInfo hand-off records (cap2uv's 21-B TcpInfo::Encode) ---------------- */
 /* rec[21*i ..] = src LE32 | dst LE32 | sp LE16 | dp LE16 | seq LE32 | ack LE32 | flag. */

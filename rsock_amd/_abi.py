@@ -28,7 +28,8 @@ DLT_NULL, DLT_EN10MB = 0, 1
 OK, EINVAL, ENOMEM, EDEVICE = 0, -22, -12, -5
 SEND_OVERSIZE, SEND_RESET = -1, 0
 RECV_VALID, RECV_CLOSE, RECV_DROP = 1, 0, -1
-PARSE_DROP, PARSE_DELIVER, PARSE_SYN, PARSE_MALFORMED = 0, 1, 2, 3
+PARSE_DROP, PARSE_DELIVER, PARSE_SYN, PARSE_MALFORMED, PARSE_SLOT_SHORT = 0, 1, 2, 3, 4
+CAP_SLOT_MIN = 64
 PARSE_HAS_ACK_POOL, PARSE_IS_SERVER = 0x1, 0x2
 FILTER_MAX_PORTS = 64
 DEMUX_ID, DEMUX_CONN_KEY, DEMUX_CONV, DEMUX_DST, DEMUX_CMD_BARRIER = 0x01, 0x02, 0x04, 0x08, 0x10
@@ -142,6 +143,10 @@ SIGNATURES = [
     ("rsk_parse_decode_batch", ctypes.c_int,
      [_vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, ctypes.c_int, ctypes.c_int,
       ctypes.POINTER(TcpInfoOut), ctypes.POINTER(DecodeOut), _vp]),
+    ("rsk_parse_decode_slots_batch", ctypes.c_int,
+     [_vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp, _vp, ctypes.c_int, ctypes.c_int,
+      ctypes.POINTER(TcpInfoOut), ctypes.POINTER(DecodeOut), _vp]),
+    ("rsk_stage_capture_slots", ctypes.c_int, [ctypes.c_uint32, _vp, _vp, _vp, ctypes.c_uint32, _vp, ctypes.c_int]),
     ("rsk_tcpinfo_encode_batch", ctypes.c_int,
      [_vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("rsk_capture_filter_batch", ctypes.c_int,

@@ -99,6 +99,20 @@ class DecodeBuffers:
         return out
 
 
+def stage_capture_slots(arena: np.ndarray, offs: np.ndarray, cap_len: np.ndarray, slot: int,
+                        nthreads: int = 8) -> np.ndarray:
+    """Host staging for rsk_parse_decode_slots_batch (rsk_stage_capture_slots): an (n, slot) uint8
+    array, row i = the first min(cap_len[i], slot) captured bytes of packet i, zero-filled."""
+    n = len(offs)
+    arena = np.ascontiguousarray(arena, np.uint8)
+    offs = np.ascontiguousarray(offs, np.uint64)
+    cap_len = np.ascontiguousarray(cap_len, np.uint32)
+    slots = np.empty((n, slot), np.uint8)
+    _check(lib().rsk_stage_capture_slots(n, arena.ctypes.data, offs.ctypes.data, cap_len.ctypes.data, slot,
+                                         slots.ctypes.data, nthreads), "rsk_stage_capture_slots")
+    return slots
+
+
 def stage_decode_headers(arena: np.ndarray, offs: np.ndarray, lens: np.ndarray) -> np.ndarray:
     """Host staging for rsk_decode_headers_batch, vectorised (same bytes as rsk_stage_decode_header):
     slot = frame[0:min(32, len)] zero-filled, byte 31 = frame[8 + frame[8]] when that is inside."""
@@ -299,6 +313,17 @@ class Codec:
                                             _ptr(cap_len), datalink, flags, ctypes.byref(tout),
                                             ctypes.byref(dout), _stream(stream)),
                "rsk_parse_decode_batch")
+
+    def rawinput_slots_batch(self, slots, slot: int, wire_len, cap_len, datalink: int, flags: int,
+                             tcp: TcpInfoBuffers, out: DecodeBuffers, compact: bool = True, stream=None) -> None:
+        """rawinput_batch on host-staged header slots (rsk_parse_decode_slots_batch): packet i's first
+        min(cap_len, slot) bytes at slots[slot * i:]; RSK_PARSE_SLOT_SHORT marks packets to resubmit whole."""
+        n = wire_len.numel()
+        tout = tcp.abi()
+        dout = out.abi(compact)
+        _check(lib().rsk_parse_decode_slots_batch(self._ctx, n, _ptr(slots), slot, _ptr(wire_len), _ptr(cap_len),
+                                                  datalink, flags, ctypes.byref(tout), ctypes.byref(dout),
+                                                  _stream(stream)), "rsk_parse_decode_slots_batch")
 
     def tcpinfo_encode_batch(self, src, dst, sp, dp, seq, ack, flag, rec, stream=None) -> None:
         n = src.numel()

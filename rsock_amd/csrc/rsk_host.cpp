@@ -48,3 +48,18 @@ extern "C" int rsk_assemble_frames(uint32_t n, const uint8_t *hdr, const int32_t
     });
     return RSK_OK;
 }
+
+extern "C" int rsk_stage_capture_slots(uint32_t n, const uint8_t *arena, const uint64_t *cap_off, const uint32_t *cap_len,
+                                       uint32_t slot, uint8_t *slots, int nthreads) {
+    if (slot < RSK_CAP_SLOT_MIN || (slot & 15u)) return RSK_EINVAL;
+    if (n && (!arena || !cap_off || !cap_len || !slots)) return RSK_EINVAL;
+    for_shards(n, nthreads, [=](uint32_t lo, uint32_t hi) {
+        for (uint32_t i = lo; i < hi; ++i) {
+            const uint32_t k = cap_len[i] < slot ? cap_len[i] : slot;
+            uint8_t *d = slots + (uint64_t)slot * i;
+            std::memcpy(d, arena + cap_off[i], k);
+            std::memset(d + k, 0, slot - k);
+        }
+    });
+    return RSK_OK;
+}

@@ -1219,23 +1219,28 @@ struct ParseArgs {
     uint16_t *cpo, *cpl;
     int datalink, flags;
     uint32_t n;
+    uint32_t slot;  // SLOT form: packet i's first min(cap_len, slot) bytes at cap + slot * i
 };
 
 // L = link header bytes: 14 (DLT_EN10MB) or 4 (DLT_NULL).  One 64-B window (five 16-B loads, bounded
 // by cap_len) holds the link, IPv4 and (IHL 5) TCP headers; other IHLs load the TCP header apart.
-template <int L>
+// SLOT: host-resident capture, only the first min(cap_len, slot) bytes of each packet were staged
+// (slot >= 64); every decision still uses the real cap_len, and a packet whose parse or decode needs
+// a byte past its slot gets RSK_PARSE_SLOT_SHORT (zero outputs) instead, for a whole resubmission.
+template <int L, bool SLOT>
 __global__ __launch_bounds__(kBlock) void k_parse_decode(ParseArgs a, DecOut d, KeySched ks) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     bool valid = false;
     if (i < a.n) {
-        const uint8_t *pkt = a.cap + a.cap_off[i];
+        const uint8_t *pkt = SLOT ? a.cap + (uint64_t)a.slot * i : a.cap + a.cap_off[i];
         const uint32_t wl = a.wire_len[i], cl = a.cap_len[i];
+        const uint32_t av = SLOT ? (cl < a.slot ? cl : a.slot) : cl;  // bytes present at pkt
         int ps = RSK_PARSE_DROP;
         uint32_t src = 0, dst = 0, sp = 0, dp = 0, seq = 0, ack = 0, fl = 0, payo = 0, plen = 0;
         Dec o = {0, 0, 0, 0, 0, 0, 0, 0, RSK_RECV_DROP};
         do {
             if (wl < 44u) break;                                   // :139
-            const uint8_t *last = pkt + (cl ? cl - 1u : 0u);
+            const uint8_t *last = pkt + (av ? av - 1u : 0u);
             if (cl < (uint32_t)L) { ps = RSK_PARSE_MALFORMED; break; }
             uint32_t hw[16];
             rsk::load_window16<16>(pkt, last, hw);
@@ -1259,6 +1264,7 @@ __global__ __launch_bounds__(kBlock) void k_parse_decode(ParseArgs a, DecOut d, 
 #pragma unroll
                 for (int k = 0; k < 4; ++k) th[k] = rsk::funnel(hw[T / 4 + k + 1], hw[T / 4 + k], T & 3);
             } else {
+                if (SLOT && tcpo + 16u > av) { ps = RSK_PARSE_SLOT_SHORT; break; }
                 rsk::load_window16<4>(pkt + tcpo, last, th);
             }
             const uint32_t thl = ((th[3] & 0xffu) >> 4) * 4u;
@@ -1286,6 +1292,14 @@ __global__ __launch_bounds__(kBlock) void k_parse_decode(ParseArgs a, DecOut d, 
             if (payload_len < 0) { ps = RSK_PARSE_MALFORMED; break; }
             if (payload_len + 32 > RSK_MAX_PKT_SIZE) break;        // cap2uv :240-244
             if ((uint64_t)payo + (uint64_t)payload_len > cl) { ps = RSK_PARSE_MALFORMED; break; }
+            if (SLOT && payload_len > RSK_HEAD_SIZE) {  // decode reads frame [0, 32) and frame[8 + len]
+                if (payo + 32u > av) { ps = RSK_PARSE_SLOT_SHORT; break; }
+                const uint32_t len = pkt[payo + 8u];
+                if (len != (uint32_t)RSK_ENC_HEAD_SIZE && (int)len < payload_len - 8 && payo + 9u + len > av) {
+                    ps = RSK_PARSE_SLOT_SHORT;
+                    break;
+                }
+            }
             seq += (uint32_t)payload_len;                           // :235
             plen = (uint32_t)payload_len;
             ps = RSK_PARSE_DELIVER;
@@ -1994,10 +2008,11 @@ void rsk_stage_decode_header(const uint8_t *frame, int nread, uint8_t *slot) {
     }
 }
 
-int rsk_parse_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *cap_arena, const uint64_t *cap_off,
-                           const uint32_t *wire_len, const uint32_t *cap_len, int datalink, int flags,
-                           const rsk_tcpinfo_out *tcp, const rsk_decode_out *dec, void *stream) {
-    if (!c || !cap_arena || !cap_off || !wire_len || !cap_len || !tcp || !dec_out_ok(dec)) return RSK_EINVAL;
+namespace {
+int parse_decode(rsk_ctx *c, uint32_t n, const uint8_t *cap_arena, const uint64_t *cap_off, uint32_t slot,
+                 const uint32_t *wire_len, const uint32_t *cap_len, int datalink, int flags,
+                 const rsk_tcpinfo_out *tcp, const rsk_decode_out *dec, void *stream) {
+    if (!c || !cap_arena || (!slot && !cap_off) || !wire_len || !cap_len || !tcp || !dec_out_ok(dec)) return RSK_EINVAL;
     if (datalink != RSK_DLT_EN10MB && datalink != RSK_DLT_NULL) return RSK_EINVAL;  // RawTcp.cpp:161-164
     if (!tcp->src || !tcp->dst || !tcp->sp || !tcp->dp || !tcp->seq || !tcp->ack || !tcp->flag ||
         !tcp->parse_status || !tcp->cap_pay_off || !tcp->cap_pay_len)
@@ -2025,13 +2040,34 @@ int rsk_parse_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *cap_arena, con
     a.flag = tcp->flag; a.pst = tcp->parse_status; a.cpo = tcp->cap_pay_off; a.cpl = tcp->cap_pay_len;
     a.datalink = datalink; a.flags = flags; a.n = n;
     DecOut d = make_dec_out(dec, masks, counts);
-    if (datalink == RSK_DLT_EN10MB)
-        hipLaunchKernelGGL(k_parse_decode<14>, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, a, d, c->ks);
-    else
-        hipLaunchKernelGGL(k_parse_decode<4>, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, a, d, c->ks);
+    a.slot = slot;
+    const bool sl = slot != 0;
+    const hipStream_t st = (hipStream_t)stream;
+    const dim3 gd(grid_for(n)), bd(kBlock);
+    if (datalink == RSK_DLT_EN10MB) {
+        if (sl) hipLaunchKernelGGL((k_parse_decode<14, true>), gd, bd, 0, st, a, d, c->ks);
+        else hipLaunchKernelGGL((k_parse_decode<14, false>), gd, bd, 0, st, a, d, c->ks);
+    } else {
+        if (sl) hipLaunchKernelGGL((k_parse_decode<4, true>), gd, bd, 0, st, a, d, c->ks);
+        else hipLaunchKernelGGL((k_parse_decode<4, false>), gd, bd, 0, st, a, d, c->ks);
+    }
     int r = launch_check("k_parse_decode");
     if (r || !compact) return r;
     return run_compaction(c, n, masks, counts, offsets, dec, (hipStream_t)stream);
+}
+}  // namespace
+
+int rsk_parse_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *cap_arena, const uint64_t *cap_off,
+                           const uint32_t *wire_len, const uint32_t *cap_len, int datalink, int flags,
+                           const rsk_tcpinfo_out *tcp, const rsk_decode_out *dec, void *stream) {
+    return parse_decode(c, n, cap_arena, cap_off, 0u, wire_len, cap_len, datalink, flags, tcp, dec, stream);
+}
+
+int rsk_parse_decode_slots_batch(rsk_ctx *c, uint32_t n, const uint8_t *slots, uint32_t slot,
+                                 const uint32_t *wire_len, const uint32_t *cap_len, int datalink, int flags,
+                                 const rsk_tcpinfo_out *tcp, const rsk_decode_out *dec, void *stream) {
+    if (slot < RSK_CAP_SLOT_MIN || (slot & 15u) || (reinterpret_cast<uintptr_t>(slots) & 15u)) return RSK_EINVAL;
+    return parse_decode(c, n, slots, nullptr, slot, wire_len, cap_len, datalink, flags, tcp, dec, stream);
 }
 
 int rsk_capture_filter_batch(rsk_ctx *c, uint32_t n, const uint8_t *cap_arena, const uint64_t *cap_off,

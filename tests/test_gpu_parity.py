@@ -404,3 +404,113 @@ def test_shims(codec, oracle):
     assert codec.decodebuf(hb, 100) is None and oracle.enchead_decode(hb, 100) is None
     assert codec.decodebuf(hb, 200) == oracle.enchead_decode(hb, 200)
     assert codec.decodebuf(h, 22) is None
+
+
+# ---- parse + decode on host-staged header slots (rsk_parse_decode_slots_batch) -------------------
+def _slot_short(p, wl, cl, dl, slot, flags):
+    """The kernel's RSK_PARSE_SLOT_SHORT rule restated over the reference's parse order
+    (RawTcp.cpp:138-244): True when the whole-capture path would read a byte past the slot."""
+    av = min(cl, slot)
+    L = 14 if dl == 1 else 4
+    if wl < 44 or cl < L:
+        return False
+    if dl == 1 and p[12:14] != b"\x08\x00":
+        return False
+    if dl == 0 and int.from_bytes(p[0:4], "little") != 2:
+        return False
+    if cl < L + 20 or p[L + 9] != 6:
+        return False
+    ihl = (p[L] & 15) * 4
+    tcpo = L + ihl
+    if cl < tcpo + 20:
+        return False
+    if ihl != 20 and tcpo + 16 > av:
+        return True
+    thl = (p[tcpo + 12] >> 4) * 4
+    payo = tcpo + thl
+    plen = int.from_bytes(p[L + 2:L + 4], "big") - (ihl + thl)
+    fl = p[tcpo + 13]
+    if (fl & 0x02) and (flags & 1):
+        return False
+    close = (fl & 0x05) != 0
+    if (plen < 9 and not close) or plen < 0 or plen + 32 > 1500 or payo + plen > cl:
+        return False
+    if plen > 31:
+        if payo + 32 > av:
+            return True
+        ln = p[payo + 8]
+        if ln != 23 and ln < plen - 8 and payo + 9 + ln > av:
+            return True
+    return False
+
+
+@pytest.mark.parametrize("slot", [64, 96, 128, 2048])
+@pytest.mark.parametrize("flags", [0, 3])
+def test_parse_decode_slots(codec, gpu, oracle, slot, flags):
+    """Host-resident receive: slots of the first min(cap_len, slot) bytes give the whole-capture
+    outputs (oracle) for every packet whose parse/decode stays inside its slot, and SLOT_SHORT with
+    zero outputs exactly for the others; rsock's own packets (IHL 5, data offset 5, len 23) fit 96 B."""
+    import torch
+
+    from rsock_amd import _abi
+    from rsock_amd.codec import DecodeBuffers, TcpInfoBuffers, stage_capture_slots
+
+    rng = np.random.default_rng(5)
+    pk, meta = _parse_cases(oracle, rng)
+    # a len-byte variant whose hashed byte sits past 96 B (must come back SLOT_SHORT at small slots)
+    st, f = oracle.rconn_output(KEY, bytes(rng.integers(0, 256, 200, dtype=np.uint8)), 0, b"abcdefgh", 1, 2)
+    f = bytearray(f)
+    f[8] = 100
+    f[:8] = oracle.tag(KEY, f[8 + 100])
+    p = P.ipv4_tcp("10.0.0.1", 1, "10.0.0.2", 2, 3, 4, 0x18, bytes(f))
+    pk.append(p)
+    meta.append((len(p), len(p)))
+    for dl in (1, 0):
+        sel = [i for i, p in enumerate(pk) if (p[12:14] in (b"\x08\x00", b"\x86\xdd")) == (dl == 1)]
+        recs = [pk[i] for i in sel]
+        wl = np.array([meta[i][0] for i in sel], np.uint32)
+        cl = np.array([meta[i][1] for i in sel], np.uint32)
+        arena, offs, _ = P.pack_records(recs, align=16)
+        n = len(recs)
+        slots = stage_capture_slots(arena, offs, cl, slot)
+        tcp = TcpInfoBuffers.alloc(n, gpu)
+        out = DecodeBuffers.alloc(n, gpu)
+        codec.rawinput_slots_batch(dev(slots.reshape(-1), gpu), slot, dev(wl, gpu, np.int32), dev(cl, gpu, np.int32),
+                                   dl, flags, tcp, out)
+        torch.cuda.synchronize()
+        exp = oracle.parse_decode_batch(KEY, arena, offs, wl, cl, dl, flags)
+        short = np.array([_slot_short(r, int(w_), int(c_), dl, slot, flags) for r, w_, c_ in zip(recs, wl, cl)])
+        th = tcp.to_host()
+        ps = th["parse_status"].view(np.int8)
+        assert np.array_equal(ps == _abi.PARSE_SLOT_SHORT, short), (slot, dl, np.nonzero((ps == 4) != short))
+        if slot >= 2048:
+            assert not short.any()
+        keep = ~short
+        for k, dt in (("src", np.uint32), ("dst", np.uint32), ("sp", np.uint16), ("dp", np.uint16),
+                      ("seq", np.uint32), ("ack", np.uint32), ("flag", np.uint8), ("parse_status", np.int8),
+                      ("cap_pay_off", np.uint16), ("cap_pay_len", np.uint16)):
+            g = th[k].view(dt)
+            assert np.array_equal(g[keep], exp[k][keep]), (slot, dl, k)
+            if k != "parse_status":
+                assert not g[short].any(), (slot, dl, k)
+        got = out.to_host()
+        for k, dt in DEC_VIEWS.items():
+            g = got[k].view(dt)
+            if k == "id":
+                g8, e8 = g.reshape(n, 8), exp[k].reshape(n, 8)
+                assert np.array_equal(g8[keep], e8[keep]) and not g8[short].any()
+            else:
+                assert np.array_equal(g[keep], exp[k][keep]), (slot, dl, k)
+        assert (got["status"].view(np.int8)[short] == -1).all()
+        ev = exp["valid_idx"][:exp["n_valid"]]
+        ev = ev[keep[ev]]
+        nv = int(got["n_valid"][0])
+        assert nv == len(ev) and np.array_equal(got["valid_idx"][:nv].view(np.uint32), ev)
+        # rsock's own packets: IHL 5, data offset 5, EncHead len 23 -> never short at 96 B
+        if slot >= 96:
+            L = 14 if dl == 1 else 4
+            plain = np.array([r[L] == 0x45 and (r[L + 32] >> 4) == 5 and (len(r) < L + 49 or r[L + 48] == 23)
+                              for r in recs])
+            assert plain.any() and not (short & plain).any()
+        if slot == 64:
+            assert short.any()

@@ -52,3 +52,27 @@ def test_assemble_frames_matches_oracle(oracle):
     for i in range(d.n):
         if status[i] > 0:
             assert out[fo[i]: fo[i] + status[i]].tobytes() == frames[fo[i]: fo[i] + status[i]].tobytes(), i
+
+
+def test_stage_capture_slots_matches_numpy():
+    rng = np.random.default_rng(12)
+    n = 9000
+    cl = rng.integers(0, 400, n).astype(np.uint32)
+    offs = np.concatenate([[0], np.cumsum(cl.astype(np.uint64) + 5)[:-1]]).astype(np.uint64)
+    arena = rng.integers(0, 256, int(offs[-1]) + 400, dtype=np.uint8)
+    for slot in (64, 96, 128, 512):
+        got = rc.stage_capture_slots(arena, offs, cl, slot)
+        k = np.arange(slot)
+        idx = offs.astype(np.int64)[:, None] + k[None, :]
+        exp = np.where(k[None, :] < cl.astype(np.int64)[:, None], arena[np.minimum(idx, len(arena) - 1)], 0)
+        assert np.array_equal(got, exp.astype(np.uint8)), slot
+
+
+def test_stage_capture_slots_rejects_bad_slot():
+    lib = _abi.load()
+    a = np.zeros(256, np.uint8)
+    o = np.zeros(1, np.uint64)
+    c = np.full(1, 100, np.uint32)
+    out = np.zeros(256, np.uint8)
+    for slot in (0, 48, 72, 100):  # below RSK_CAP_SLOT_MIN or not a multiple of 16
+        assert lib.rsk_stage_capture_slots(1, _p(a), _p(o), _p(c), slot, _p(out), 1) == _abi.EINVAL

@@ -1,5 +1,3 @@
-mkdir -p gpurun_out/wire
-timeout -k 10 300 python -u -m pytest tests/test_gpu_wire.py -x -q --timeout 120 --timeout-method thread > gpurun_out/wire/tests.log 2>&1 &&
-timeout -k 10 300 python tools/bench_paths.py --config c3 --wire-variants 4,5,6,7,0 > gpurun_out/wire/c3.json 2>/dev/null &&
-timeout -k 10 300 python tools/bench_paths.py --config c4 --wire-variants 4,5,6,7,0 > gpurun_out/wire/c4.json 2>/dev/null &&
-timeout -k 10 300 python tools/bench_paths.py --config c2 --wire-variants 4,5,6,7,0 > gpurun_out/wire/c2.json 2>/dev/null
+mkdir -p gpurun_out/slots
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_wire.py -x -q --timeout 120 --timeout-method thread -k "slots or parse_decode or wire" > gpurun_out/slots/tests.log 2>&1 &&
+timeout -k 10 300 python tools/bench_pcap_host.py > gpurun_out/slots/pcap_host.json 2> gpurun_out/slots/pcap_host.err
