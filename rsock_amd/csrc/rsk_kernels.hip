@@ -426,6 +426,15 @@ constexpr uint32_t kFlatBelowMeanBytes = 256;
 
 // One 64-packet set per wave: phase 1, then the chosen copy path.
 template <int MODE, int PU, int U, int NT>
+__device__ __forceinline__ void encode_copy(const EncArgs &a, const Lane1 &L, uint32_t lane, bool vec, uint64_t vm,
+                                            bool flat, CopyRec *recs, uint32_t *cend) {
+    if (flat) copy_flat<U, NT>(a, L, lane, vec, recs, cend);
+    else if constexpr (MODE >= 3) copy_pkt_dpp<PU, NT>(a, L, lane, vm);
+    else copy_pkt<PU, NT>(a, L, lane, vm);
+}
+
+// NT < 0: store policy chosen per set (below).
+template <int MODE, int PU, int U, int NT>
 __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks, uint64_t i, uint32_t lane,
                                            CopyRec *recs, uint32_t *cend) {
     const Lane1 L = encode_phase1(a, ks, i);
@@ -440,9 +449,23 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
         const uint32_t cnt = (uint32_t)__popcll(vm);
         flat = fl < kFlatBelowMeanBytes * cnt;
     }
-    if (flat) copy_flat<U, NT>(a, L, lane, vec, recs, cend);
-    else if constexpr (MODE >= 3) copy_pkt_dpp<PU, NT>(a, L, lane, vm);
-    else copy_pkt<PU, NT>(a, L, lane, vm);
+    if constexpr (NT < 0) {
+        // Store policy per set: frames packed back to back (each frame's padded end is the next
+        // frame's start, so every line of the span is written in full) keep normal stores; any gap
+        // leaves partially written lines, which nontemporal stores write without the memory-side
+        // read-modify-write (C4's 1440-B slots: -13 %; C3's packed frames: +4 % if streamed).  The
+        // flat path (short frames) keeps normal stores: streamed 95-B frames lose 10 %.
+        const uint32_t fend = vec ? padded_len(a.frame + L.fo, (uint32_t)L.st, a.pad) : 0u;
+        const uint64_t end = L.fo + fend;
+        const uint64_t nfo = (uint64_t)(uint32_t)__shfl_down((int)(uint32_t)L.fo, 1) |
+                             ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(L.fo >> 32), 1) << 32);
+        const bool nvec = __shfl_down((int)vec, 1) != 0;
+        const bool gap = vec && nvec && lane != 63u && end != nfo;
+        if (!flat && __ballot(gap)) encode_copy<MODE, PU, U, 2>(a, L, lane, vec, vm, flat, recs, cend);
+        else encode_copy<MODE, PU, U, 0>(a, L, lane, vec, vm, flat, recs, cend);
+    } else {
+        encode_copy<MODE, PU, U, NT>(a, L, lane, vec, vm, flat, recs, cend);
+    }
     copy_bytes(a, L, lane, __ballot(L.st > 0 && L.slow));
 }
 
@@ -1757,15 +1780,19 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 // in-process A/B measurements.  k_encode<MODE, PU, U, NT>: MODE 0 per-packet, 1 flat, 2 hybrid,
 // 3 hybrid with the one-load DPP per-packet copy, 4 DPP per-packet only; PU packets per per-packet
 // iteration; U chunks per lane per flat iteration; NT bit0 nontemporal loads, bit1 nontemporal stores.
-//   0 = hybrid-DPP<16,4> (default)  1 = pkt PU=1   2 = flat U=2    3 = flat U=4    4 = pkt PU=2
+//   0 = hybrid-DPP<12,4> with the per-set store policy (default: nontemporal stores for
+//       per-packet sets whose frames leave gaps, normal stores otherwise)
+//   1 = pkt PU=1   2 = flat U=2    3 = flat U=4    4 = pkt PU=2
 //   5 = pkt PU=4                6 = hybrid nt-stores           7 = pkt PU=4 nt loads+stores
 //   8 = pkt PU=4 nt stores      9 = hybrid PU=2               10 = pkt PU=2 nt stores
 //  11 = block-interleaved pkt PU=4   12 = block-interleaved pkt PU=2
 //  13 = two-load hybrid<4,4> (the default before the DPP copy)
 //  14/15/16 = hybrid-DPP PU=4/8/12   17 = DPP per-packet only PU=16
+//  18/19 = hybrid-DPP PU=16/8 with nontemporal stores   20 = hybrid-DPP PU=16 (normal stores)
+//  21 = hybrid-DPP PU=16 with the per-set store policy (169 VGPRs: 2 waves/SIMD)
 // v + 100 * cap (cap 1..4): the same kernel held to `cap` blocks per CU by unused dynamic LDS.
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
-    if (!c || v < 0 || v % 100 > 17 || v / 100 > 4) return RSK_EINVAL;
+    if (!c || v < 0 || v % 100 > 21 || v / 100 > 4) return RSK_EINVAL;
     c->enc_variant = v;
     return RSK_OK;
 }
@@ -1848,6 +1875,10 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         case 15: hipLaunchKernelGGL((k_encode<3, 8, 4, 0>), gd, bd, lds, st, a, c->ks); break;
         case 16: hipLaunchKernelGGL((k_encode<3, 12, 4, 0>), gd, bd, lds, st, a, c->ks); break;
         case 17: hipLaunchKernelGGL((k_encode<4, 16, 4, 0>), gd, bd, lds, st, a, c->ks); break;
+        case 18: hipLaunchKernelGGL((k_encode<3, 16, 4, 2>), gd, bd, lds, st, a, c->ks); break;
+        case 19: hipLaunchKernelGGL((k_encode<3, 8, 4, 2>), gd, bd, lds, st, a, c->ks); break;
+        case 20: hipLaunchKernelGGL((k_encode<3, 16, 4, 0>), gd, bd, lds, st, a, c->ks); break;
+        case 21: hipLaunchKernelGGL((k_encode<3, 16, 4, -1>), gd, bd, lds, st, a, c->ks); break;
         case 1: hipLaunchKernelGGL((k_encode<0, 1, 4, 0>), gd, bd, 0, st, a, c->ks); break;
         case 2: hipLaunchKernelGGL((k_encode<1, 4, 2, 0>), gd, bd, 0, st, a, c->ks); break;
         case 3: hipLaunchKernelGGL((k_encode<1, 4, 4, 0>), gd, bd, 0, st, a, c->ks); break;
@@ -1860,7 +1891,7 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         case 10: hipLaunchKernelGGL((k_encode<0, 2, 4, 2>), gd, bd, 0, st, a, c->ks); break;
         case 11: hipLaunchKernelGGL((k_encode_blk<4>), gd, bd, 0, st, a, c->ks); break;
         case 12: hipLaunchKernelGGL((k_encode_blk<2>), gd, bd, 0, st, a, c->ks); break;
-        default: hipLaunchKernelGGL((k_encode<3, 16, 4, 0>), gd, bd, lds, st, a, c->ks); break;
+        default: hipLaunchKernelGGL((k_encode<3, 12, 4, -1>), gd, bd, lds, st, a, c->ks); break;
     }
     return launch_check("k_encode");
 }
