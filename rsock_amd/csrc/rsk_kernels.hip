@@ -764,7 +764,7 @@ __device__ __forceinline__ void copy_wire_pkt(const EncArgs &a, const Lane1 &L, 
 
 // ---- the same with one aligned load per chunk: the funnel partner comes from lane + 1 by DPP (as
 // copy_pkt_dpp), all PU packets' loads issued before the first shift. ------------------------------
-template <int E, int PU>
+template <int E, int PU, int NT>
 __device__ __forceinline__ void copy_wire_pkt_dpp(const EncArgs &a, const Lane1 &L, const uint32_t *stage,
                                                   uint32_t sum_pre, int32_t wst, uint32_t lane, uint64_t vm) {
     using G = WireGeom<E>;
@@ -829,13 +829,13 @@ __device__ __forceinline__ void copy_wire_pkt_dpp(const EncArgs &a, const Lane1 
                 const uint4 sv = *reinterpret_cast<const uint4 *>(stage + js[p] * G::NPW + 4u * lane);
                 uint32_t w4[4] = {sv.x, sv.y, sv.z, sv.w};
                 if (lane == (uint32_t)(G::CK / 16)) w4[(G::CK & 15) >> 2] |= ck[p] << (8 * (G::CK & 3));
-                store_last16<0>(dstp[p] + 16u * lane, make_uint4(w4[0], w4[1], w4[2], w4[3]),
+                store_last16<NT>(dstp[p] + 16u * lane, make_uint4(w4[0], w4[1], w4[2], w4[3]),
                                 (int)wlen[p] - 16 * (int)lane, a.pad != 0u);
             }
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
                 const uint32_t k = G::NPRE + lane + 64u * q;
-                if (k < nst) store_last16<0>(dstp[p] + 16u * k, v[p][q], (int)wlen[p] - 16 * (int)k, a.pad != 0u);
+                if (k < nst) store_last16<NT>(dstp[p] + 16u * k, v[p][q], (int)wlen[p] - 16 * (int)k, a.pad != 0u);
             }
         }
     }
@@ -1052,7 +1052,18 @@ __global__ __launch_bounds__(kBlock) void k_encode_wire(EncArgs a, WireArgs wa, 
     }
     if (!flat) {
         wave_lds_sync();
-        if constexpr (PU >= 100) copy_wire_pkt_dpp<E, PU - 100>(a, L, stage, sum_pre, wst, lane, vm);
+        if constexpr (PU >= 100) {
+            // store policy per set, as k_encode: stream the stores when the wire packets leave gaps
+            const uint32_t wend = vec ? padded_len(a.frame + L.fo, (uint32_t)wst, a.pad) : 0u;
+            const uint64_t end = L.fo + wend;
+            const uint64_t nfo = (uint64_t)(uint32_t)__shfl_down((int)(uint32_t)L.fo, 1) |
+                                 ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(L.fo >> 32), 1) << 32);
+            const bool nvec = __shfl_down((int)vec, 1) != 0;
+            if (__ballot(vec && nvec && lane != 63u && end != nfo))
+                copy_wire_pkt_dpp<E, PU - 100, 2>(a, L, stage, sum_pre, wst, lane, vm);
+            else
+                copy_wire_pkt_dpp<E, PU - 100, 0>(a, L, stage, sum_pre, wst, lane, vm);
+        }
         else copy_wire_pkt<E, PU>(a, L, stage, sum_pre, wst, lane, vm);
     }
     const uint64_t sm = __ballot(L.st > 0 && L.slow);
