@@ -1,5 +1,3 @@
-mkdir -p gpurun_out/pack
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "encv22 or encv23" > gpurun_out/pack/tests.log 2>&1 &&
-timeout -k 10 200 python tools/ab_encode.py --config c4 --variants 0,22,23 --pads 16,0 > gpurun_out/pack/c4.json 2>/dev/null &&
-timeout -k 10 200 python tools/ab_encode.py --config c3 --variants 0,22,23 --pads 16 > gpurun_out/pack/c3.json 2>/dev/null &&
-timeout -k 10 200 python tools/ab_encode.py --config c2 --variants 0,22 --pads 16 > gpurun_out/pack/c2.json 2>/dev/null
+mkdir -p gpurun_out/pcap2
+timeout -k 10 300 python tools/bench_pcap_host.py > gpurun_out/pcap2/c3.json 2> gpurun_out/pcap2/c3.err &&
+timeout -k 10 300 python tools/bench_pcap_host.py --chunk 1048576 > gpurun_out/pcap2/c3_1m.json 2>> gpurun_out/pcap2/c3.err
