@@ -5,7 +5,9 @@
  * error code.  Batch entry points are stream-ordered (the `stream` argument is a hipStream_t,
  * passed as void* so this header needs no HIP include; NULL = the legacy default stream) and take
  * no ownership: the caller owns every device and host buffer.  All batch array pointers are
- * DEVICE pointers unless a comment says otherwise.
+ * DEVICE pointers unless a comment says otherwise.  An empty batch (n == 0) is a no-op that may
+ * pass null arrays (the ctx and the in/out structs must still be given); it zeroes a given
+ * n_valid / n_match / n_seg count.
  *
  * Reference interfaces replaced (paths relative to the rsock tree):
  *   rsk_compute_hash      <- char* compute_hash(char*, const std::string&, const char*, int)   util/rhash.h:17, util/rhash.cpp:20-41

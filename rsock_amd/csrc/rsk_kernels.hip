@@ -1763,6 +1763,16 @@ int run_compaction(rsk_ctx *c, uint32_t n, uint64_t *masks, uint32_t *counts, ui
     return r;
 }
 
+// An empty batch (n == 0) is a no-op that may pass null arrays; it still zeroes a given n_valid.
+int empty_batch(rsk_ctx *c, uint32_t *n_valid, void *stream) {
+    if (!n_valid) return RSK_OK;
+    DeviceGuard g(c->device);
+    if (!g.ok) return RSK_EDEVICE;
+    hipError_t e = hipMemsetAsync(n_valid, 0, sizeof(uint32_t), (hipStream_t)stream);
+    if (e != hipSuccess) { set_error("hipMemsetAsync", e); return RSK_EDEVICE; }
+    return RSK_OK;
+}
+
 bool dec_out_ok(const rsk_decode_out *o) {
     return o && o->hlen && o->cmd && o->id && o->conv && o->conn_key && o->pay_off && o->pay_len &&
            o->status && ((reinterpret_cast<uintptr_t>(o->id) & 7u) == 0);
@@ -1963,15 +1973,9 @@ int rsk_encode_wire_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const
 int rsk_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *frame_arena, const uint64_t *frame_off,
                      const uint16_t *frame_len, const uint8_t *is_tcp_close, const rsk_decode_out *out,
                      void *stream) {
-    if (!c || !frame_arena || !frame_off || !frame_len || !dec_out_ok(out)) return RSK_EINVAL;
-    if (n == 0) {
-        if (out->n_valid) {
-            DeviceGuard g(c->device);
-            hipError_t e = hipMemsetAsync(out->n_valid, 0, sizeof(uint32_t), (hipStream_t)stream);
-            if (e != hipSuccess) { set_error("hipMemsetAsync", e); return RSK_EDEVICE; }
-        }
-        return RSK_OK;
-    }
+    if (!c || !out) return RSK_EINVAL;
+    if (n == 0) return empty_batch(c, out->n_valid, stream);
+    if (!frame_arena || !frame_off || !frame_len || !dec_out_ok(out)) return RSK_EINVAL;
     DeviceGuard g(c->device);
     if (!g.ok) return RSK_EDEVICE;
     const bool compact = out->valid_idx || out->n_valid;
@@ -2011,17 +2015,12 @@ int rsk_encode_headers_batch(rsk_ctx *c, uint32_t n, const rsk_encode_hdr_in *in
 
 int rsk_decode_headers_batch(rsk_ctx *c, uint32_t n, const uint8_t *hdr, const uint16_t *frame_len,
                              const uint8_t *is_tcp_close, const rsk_decode_out *out, void *stream) {
-    if (!c || !hdr || !frame_len || !dec_out_ok(out)) return RSK_EINVAL;
+    if (!c || !out) return RSK_EINVAL;
+    if (n == 0) return empty_batch(c, out->n_valid, stream);
+    if (!hdr || !frame_len || !dec_out_ok(out)) return RSK_EINVAL;
     if (reinterpret_cast<uintptr_t>(hdr) & 15u) return RSK_EINVAL;
     DeviceGuard g(c->device);
     if (!g.ok) return RSK_EDEVICE;
-    if (n == 0) {
-        if (out->n_valid) {
-            hipError_t e = hipMemsetAsync(out->n_valid, 0, sizeof(uint32_t), (hipStream_t)stream);
-            if (e != hipSuccess) { set_error("hipMemsetAsync", e); return RSK_EDEVICE; }
-        }
-        return RSK_OK;
-    }
     const bool compact = out->valid_idx || out->n_valid;
     uint64_t *masks = nullptr;
     uint32_t *counts = nullptr, *offsets = nullptr;
@@ -2054,20 +2053,15 @@ namespace {
 int parse_decode(rsk_ctx *c, uint32_t n, const uint8_t *cap_arena, const uint64_t *cap_off, uint32_t slot,
                  const uint32_t *wire_len, const uint32_t *cap_len, int datalink, int flags,
                  const rsk_tcpinfo_out *tcp, const rsk_decode_out *dec, void *stream) {
-    if (!c || !cap_arena || (!slot && !cap_off) || !wire_len || !cap_len || !tcp || !dec_out_ok(dec)) return RSK_EINVAL;
+    if (!c || !tcp || !dec) return RSK_EINVAL;
     if (datalink != RSK_DLT_EN10MB && datalink != RSK_DLT_NULL) return RSK_EINVAL;  // RawTcp.cpp:161-164
+    if (n == 0) return empty_batch(c, dec->n_valid, stream);
+    if (!cap_arena || (!slot && !cap_off) || !wire_len || !cap_len || !dec_out_ok(dec)) return RSK_EINVAL;
     if (!tcp->src || !tcp->dst || !tcp->sp || !tcp->dp || !tcp->seq || !tcp->ack || !tcp->flag ||
         !tcp->parse_status || !tcp->cap_pay_off || !tcp->cap_pay_len)
         return RSK_EINVAL;
     DeviceGuard g(c->device);
     if (!g.ok) return RSK_EDEVICE;
-    if (n == 0) {
-        if (dec->n_valid) {
-            hipError_t e = hipMemsetAsync(dec->n_valid, 0, sizeof(uint32_t), (hipStream_t)stream);
-            if (e != hipSuccess) { set_error("hipMemsetAsync", e); return RSK_EDEVICE; }
-        }
-        return RSK_OK;
-    }
     const bool compact = dec->valid_idx || dec->n_valid;
     uint64_t *masks = nullptr;
     uint32_t *counts = nullptr, *offsets = nullptr;
@@ -2122,15 +2116,9 @@ int rsk_capture_filter_batch(rsk_ctx *c, uint32_t n, const uint8_t *cap_arena, c
         for (uint32_t q = 0; q < pl->n_range; ++q)
             if (pl->range[q][0] >= pl->range[q][1]) return RSK_EINVAL;  // RPortList::AddPortRange
     }
+    if (n == 0) return empty_batch(c, n_match, stream);
     DeviceGuard g(c->device);
     if (!g.ok) return RSK_EDEVICE;
-    if (n == 0) {
-        if (n_match) {
-            hipError_t e = hipMemsetAsync(n_match, 0, sizeof(uint32_t), (hipStream_t)stream);
-            if (e != hipSuccess) { set_error("hipMemsetAsync", e); return RSK_EDEVICE; }
-        }
-        return RSK_OK;
-    }
     const bool compact = match_idx || n_match;
     uint64_t *masks = nullptr;
     uint32_t *counts = nullptr, *offsets = nullptr;
@@ -2195,8 +2183,9 @@ int rsk_filter_str(const rsk_capture_filter *f, char *buf, size_t buf_len) {
 int rsk_tcpinfo_encode_batch(rsk_ctx *c, uint32_t n, const uint32_t *src, const uint32_t *dst,
                              const uint16_t *sp, const uint16_t *dp, const uint32_t *seq,
                              const uint32_t *ack, const uint8_t *flag, uint8_t *rec, void *stream) {
-    if (!c || !src || !dst || !sp || !dp || !seq || !ack || !flag || !rec) return RSK_EINVAL;
+    if (!c) return RSK_EINVAL;
     if (n == 0) return RSK_OK;
+    if (!src || !dst || !sp || !dp || !seq || !ack || !flag || !rec) return RSK_EINVAL;
     DeviceGuard g(c->device);
     if (!g.ok) return RSK_EDEVICE;
     TcpRecArgs a{src, dst, sp, dp, seq, ack, flag, rec, n};
