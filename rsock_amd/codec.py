@@ -246,10 +246,10 @@ class Codec:
 
     def set_encode_variant(self, v: int) -> None:
         """Internal tuning knob (not in the public header) selecting k_encode's copy path: 0 hybrid
-        with the one-load DPP per-packet copy, 12 packets per iteration, nontemporal stores for sets whose
-        frames leave gaps (default); 1-12 per-packet / flat / non-temporal / interleaved variants, 13 the
-        two-load hybrid, 14-21 DPP variants; + 100 * cap holds the kernel to cap blocks per CU (list in
-        rsk_kernels.hip).  Every variant is parity-tested; used for in-process A/B."""
+        with the one-load DPP per-packet copy, 12 packets per iteration, the tag computed in the copy loop
+        for sets of long frames and nontemporal stores for sets whose frames leave gaps (default); 1-12
+        per-packet / flat / non-temporal / interleaved variants, 13 the two-load hybrid, 14-24 DPP
+        variants; + 100 * cap holds the kernel to cap blocks per CU (list in rsk_kernels.hip).  Every variant is parity-tested; used for in-process A/B."""
         fn = lib().rsk__set_encode_variant
         fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
         _check(fn(self._ctx, v), "rsk__set_encode_variant")

@@ -93,6 +93,7 @@ struct Lane1 {
     bool slow;
 };
 
+template <bool TAG = true>
 __device__ __forceinline__ Lane1 encode_phase1(const EncArgs &a, const KeySched &ks, uint64_t i) {
     Lane1 L;
     L.st = 0;
@@ -108,8 +109,8 @@ __device__ __forceinline__ Lane1 encode_phase1(const EncArgs &a, const KeySched 
         L.st = P == 0 ? RSK_SEND_RESET
                       : (P > RSK_MAX_PAYLOAD ? RSK_SEND_OVERSIZE : (int32_t)(RSK_HEAD_SIZE + P));
         if (L.st > 0) {
-            const uint32_t b0 = a.payload[L.po];
-            rsk::md5_tag(ks, b0, L.H[0], L.H[1]);
+            const uint32_t b0 = TAG ? a.payload[L.po] : 0u;
+            if (TAG) rsk::md5_tag(ks, b0, L.H[0], L.H[1]);
             uint32_t id0 = a.id_lo, id1 = a.id_hi;
             if (a.id) {
                 const uint2 v = *reinterpret_cast<const uint2 *>(a.id + 8 * i);
@@ -122,6 +123,16 @@ __device__ __forceinline__ Lane1 encode_phase1(const EncArgs &a, const KeySched 
         a.status[i] = L.st;
     }
     return L;
+}
+
+// The tag half of phase 1 for a set that skipped it (encode_phase1<false>): payload[0], MD5, and
+// payload[0] into frame byte 31 (H[7]).
+__device__ __forceinline__ void encode_tag(const EncArgs &a, const KeySched &ks, Lane1 &L) {
+    if (L.st > 0) {
+        const uint32_t b0 = a.payload[L.po];
+        rsk::md5_tag(ks, b0, L.H[0], L.H[1]);
+        L.H[7] |= b0 << 24;
+    }
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -281,6 +292,77 @@ __device__ __forceinline__ void copy_pkt_dpp(const EncArgs &a, const Lane1 &L, u
     }
 }
 
+// ---- copy_pkt_dpp with the tag computed in the copy loop (MODE 6): phase 1 skipped payload[0] and
+// the MD5, because its byte load fetches the payload's first line well before the copy reaches the
+// packet, and the line is gone from L2 by then (~128 B of extra HBM reads per packet, the excess
+// FETCH_SIZE shows).  Here lane p loads payload[0] of the iteration's packet p first, then the
+// chunks; the MD5 of the PU packets runs while the chunk loads are in flight, and the byte load
+// hits the lines those loads are fetching anyway. ------------------------------------------------
+template <int PU, int NT>
+__device__ __forceinline__ void copy_pkt_dpp_tag(const EncArgs &a, const KeySched &ks, const Lane1 &L, uint32_t lane,
+                                                 uint64_t vm) {
+    while (vm) {
+        uint32_t js[PU];
+        bool on[PU];
+#pragma unroll
+        for (int p = 0; p < PU; ++p) {
+            on[p] = vm != 0ull;
+            js[p] = on[p] ? (uint32_t)__builtin_ctzll(vm) : 0u;
+            if (on[p]) vm &= vm - 1ull;
+        }
+        // lane p: payload[0] of packet p (issued before the chunk loads)
+        uint32_t my_b0 = 0;
+#pragma unroll
+        for (int p = 0; p < PU; ++p)
+            if (on[p] && lane == (uint32_t)p) my_b0 = rsk::gptr(a.payload)[rdl64(L.po, js[p])];
+        uint4 A[PU][2];
+        uint8_t *dstp[PU];
+        uint32_t flen[PU], sh[PU];
+#pragma unroll
+        for (int p = 0; p < PU; ++p) {
+            flen[p] = on[p] ? rdl((uint32_t)L.st, js[p]) : 0u;
+            const uint8_t *src = a.payload + rdl64(L.po, js[p]);
+            dstp[p] = a.frame + rdl64(L.fo, js[p]);
+            sh[p] = (uint32_t)((reinterpret_cast<uintptr_t>(src) + 1u) & 15u);
+            const uint8_t *srcp = src + 1 - sh[p];
+            const int32_t last_rel = (int32_t)flen[p] - RSK_HEAD_SIZE + (int32_t)sh[p] - 2;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const uint32_t k = lane + 64u * q;
+                A[p][q] = make_uint4(0u, 0u, 0u, 0u);
+                if (on[p] && k >= 2u && (int32_t)(16u * (k - 2u)) <= last_rel) A[p][q] = ld16<NT>(srcp + 16u * (k - 2u));
+            }
+        }
+        uint32_t t0, t1;  // lane p: tag of packet p
+        rsk::md5_tag(ks, my_b0, t0, t1);
+#pragma unroll
+        for (int p = 0; p < PU; ++p) {
+            if (!on[p]) continue;
+            uint4 B[2];
+            B[0] = make_uint4(wave_shl1(A[p][0].x), wave_shl1(A[p][0].y), wave_shl1(A[p][0].z), wave_shl1(A[p][0].w));
+            B[1] = make_uint4(wave_shl1(A[p][1].x), wave_shl1(A[p][1].y), wave_shl1(A[p][1].z), wave_shl1(A[p][1].w));
+            if (lane == 63u)
+                B[0] = make_uint4(rdl(A[p][1].x, 0), rdl(A[p][1].y, 0), rdl(A[p][1].z, 0), rdl(A[p][1].w, 0));
+            uint32_t Hj[8];  // packet's head words, read out in uniform control flow (SGPRs)
+#pragma unroll
+            for (int t = 2; t < 8; ++t) Hj[t] = rdl(L.H[t], js[p]);
+            Hj[0] = rdl(t0, (uint32_t)p);
+            Hj[1] = rdl(t1, (uint32_t)p);
+            Hj[7] |= rdl(my_b0, (uint32_t)p) << 24;
+            const uint32_t nch = (padded_len(dstp[p], flen[p], a.pad) + 15u) >> 4;  // chunks stored
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const uint32_t k = lane + 64u * q;
+                if (k >= nch) continue;
+                uint4 v;
+                if (k >= 2u) v = rsk::funnel16(A[p][q], B[q], sh[p]);
+                else v = k == 0u ? make_uint4(Hj[0], Hj[1], Hj[2], Hj[3]) : make_uint4(Hj[4], Hj[5], Hj[6], Hj[7]);
+                store_last16<NT>(dstp[p] + 16u * k, v, (int)flen[p] - 16 * (int)k, a.pad != 0u);
+            }
+        }
+    }
+}
+
 // ---- flat copy: the payload chunks (k >= 2) of every packet in `vm` as one list of 16-B chunks;
 // lane l of iteration t takes chunk g = 64(U t + u) + l and finds its packet by a 6-step binary
 // search over the tile's prefix sums in this wave's LDS slice.  Chunks 0 and 1 (frame bytes
@@ -423,12 +505,17 @@ __device__ __forceinline__ void copy_bytes(const EncArgs &a, const Lane1 &L, uin
 // 95-B frame uses 6 of 64 lanes), the flat list costs a binary search + LDS table per chunk.
 // Measured crossover: flat wins below a tile-mean frame of ~256 B.
 constexpr uint32_t kFlatBelowMeanBytes = 256;
+// MODE 6: the tag moves into the copy loop (copy_pkt_dpp_tag) for sets of long frames only; with
+// short frames an iteration carries fewer bytes per MD5 (C4: +10 % with the tag deferred).
+constexpr uint32_t kDeferTagMeanBytes = 1024;
 
 // One 64-packet set per wave: phase 1, then the chosen copy path.
 template <int MODE, int PU, int U, int NT>
-__device__ __forceinline__ void encode_copy(const EncArgs &a, const Lane1 &L, uint32_t lane, bool vec, uint64_t vm,
-                                            bool flat, CopyRec *recs, uint32_t *cend) {
+__device__ __forceinline__ void encode_copy(const EncArgs &a, const KeySched &ks, const Lane1 &L, uint32_t lane,
+                                            bool vec, uint64_t vm, bool flat, bool defer, CopyRec *recs,
+                                            uint32_t *cend) {
     if (flat) copy_flat<U, NT>(a, L, lane, vec, recs, cend);
+    else if (MODE == 6 && defer) copy_pkt_dpp_tag<PU, NT>(a, ks, L, lane, vm);
     else if constexpr (MODE >= 3) copy_pkt_dpp<PU, NT>(a, L, lane, vm);
     else copy_pkt<PU, NT>(a, L, lane, vm);
 }
@@ -437,17 +524,21 @@ __device__ __forceinline__ void encode_copy(const EncArgs &a, const Lane1 &L, ui
 template <int MODE, int PU, int U, int NT>
 __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks, uint64_t i, uint32_t lane,
                                            CopyRec *recs, uint32_t *cend) {
-    const Lane1 L = encode_phase1(a, ks, i);
+    Lane1 L = encode_phase1<MODE != 6>(a, ks, i);
     const bool vec = L.st > 0 && !L.slow;
     const uint64_t vm = __ballot(vec);
-    bool flat = MODE == 1;
-    if constexpr (MODE == 2 || MODE == 3) {
+    bool flat = MODE == 1, defer = false;
+    if constexpr (MODE == 2 || MODE == 3 || MODE == 6) {
         // set mean frame length over framed packets (wave reduction)
         uint32_t fl = vec ? (uint32_t)L.st : 0u;
 #pragma unroll
         for (int off = 32; off; off >>= 1) fl += __shfl_xor(fl, off);
         const uint32_t cnt = (uint32_t)__popcll(vm);
         flat = fl < kFlatBelowMeanBytes * cnt;
+        if constexpr (MODE == 6) defer = !flat && fl >= kDeferTagMeanBytes * cnt;
+    }
+    if constexpr (MODE == 6) {  // the tag now, except for the frames the deferred-tag copy handles
+        if (!defer || L.slow) encode_tag(a, ks, L);
     }
     if constexpr (NT < 0) {
         // Store policy per set: frames packed back to back (each frame's padded end is the next
@@ -461,16 +552,16 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
                              ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(L.fo >> 32), 1) << 32);
         const bool nvec = __shfl_down((int)vec, 1) != 0;
         const bool gap = vec && nvec && lane != 63u && end != nfo;
-        if (!flat && __ballot(gap)) encode_copy<MODE, PU, U, 2>(a, L, lane, vec, vm, flat, recs, cend);
-        else encode_copy<MODE, PU, U, 0>(a, L, lane, vec, vm, flat, recs, cend);
+        if (!flat && __ballot(gap)) encode_copy<MODE, PU, U, 2>(a, ks, L, lane, vec, vm, flat, defer, recs, cend);
+        else encode_copy<MODE, PU, U, 0>(a, ks, L, lane, vec, vm, flat, defer, recs, cend);
     } else {
-        encode_copy<MODE, PU, U, NT>(a, L, lane, vec, vm, flat, recs, cend);
+        encode_copy<MODE, PU, U, NT>(a, ks, L, lane, vec, vm, flat, defer, recs, cend);
     }
     copy_bytes(a, L, lane, __ballot(L.st > 0 && L.slow));
 }
 
 // MODE: 0 per-packet, 1 flat, 2 hybrid (per-wave choice), 3 hybrid with the DPP per-packet copy,
-// 4 DPP per-packet only.
+// 4 DPP per-packet only, 5 (unused), 6 = 3 with the tag deferred into the copy loop for long frames.
 // Tiled mapping: wave t takes packets [64t, 64t + 64) (coalesced descriptor loads, but the 5000+
 // co-resident waves each stream their own ~92 KB region).
 template <int MODE, int PU, int U, int NT>
@@ -1801,8 +1892,8 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 // in-process A/B measurements.  k_encode<MODE, PU, U, NT>: MODE 0 per-packet, 1 flat, 2 hybrid,
 // 3 hybrid with the one-load DPP per-packet copy, 4 DPP per-packet only; PU packets per per-packet
 // iteration; U chunks per lane per flat iteration; NT bit0 nontemporal loads, bit1 nontemporal stores.
-//   0 = hybrid-DPP<12,4> with the per-set store policy (default: nontemporal stores for
-//       per-packet sets whose frames leave gaps, normal stores otherwise)
+//   0 = hybrid-DPP<12,4>, tag computed in the copy loop for sets of long frames (MODE 6), per-set
+//       store policy (default: nontemporal stores for per-packet sets whose frames leave gaps)
 //   1 = pkt PU=1   2 = flat U=2    3 = flat U=4    4 = pkt PU=2
 //   5 = pkt PU=4                6 = hybrid nt-stores           7 = pkt PU=4 nt loads+stores
 //   8 = pkt PU=4 nt stores      9 = hybrid PU=2               10 = pkt PU=2 nt stores
@@ -1811,9 +1902,11 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 //  14/15/16 = hybrid-DPP PU=4/8/12   17 = DPP per-packet only PU=16
 //  18/19 = hybrid-DPP PU=16/8 with nontemporal stores   20 = hybrid-DPP PU=16 (normal stores)
 //  21 = hybrid-DPP PU=16 with the per-set store policy (169 VGPRs: 2 waves/SIMD)
+//  22 = hybrid-DPP PU=12 with the per-set store policy, tag in phase 1 (the default before)
+//  23/24 = the default with PU=8/16
 // v + 100 * cap (cap 1..4): the same kernel held to `cap` blocks per CU by unused dynamic LDS.
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
-    if (!c || v < 0 || v % 100 > 21 || v / 100 > 4) return RSK_EINVAL;
+    if (!c || v < 0 || v % 100 > 24 || v / 100 > 4) return RSK_EINVAL;
     c->enc_variant = v;
     return RSK_OK;
 }
@@ -1900,6 +1993,9 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         case 19: hipLaunchKernelGGL((k_encode<3, 8, 4, 2>), gd, bd, lds, st, a, c->ks); break;
         case 20: hipLaunchKernelGGL((k_encode<3, 16, 4, 0>), gd, bd, lds, st, a, c->ks); break;
         case 21: hipLaunchKernelGGL((k_encode<3, 16, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 22: hipLaunchKernelGGL((k_encode<3, 12, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 23: hipLaunchKernelGGL((k_encode<6, 8, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 24: hipLaunchKernelGGL((k_encode<6, 16, 4, -1>), gd, bd, lds, st, a, c->ks); break;
         case 1: hipLaunchKernelGGL((k_encode<0, 1, 4, 0>), gd, bd, 0, st, a, c->ks); break;
         case 2: hipLaunchKernelGGL((k_encode<1, 4, 2, 0>), gd, bd, 0, st, a, c->ks); break;
         case 3: hipLaunchKernelGGL((k_encode<1, 4, 4, 0>), gd, bd, 0, st, a, c->ks); break;
@@ -1912,7 +2008,7 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         case 10: hipLaunchKernelGGL((k_encode<0, 2, 4, 2>), gd, bd, 0, st, a, c->ks); break;
         case 11: hipLaunchKernelGGL((k_encode_blk<4>), gd, bd, 0, st, a, c->ks); break;
         case 12: hipLaunchKernelGGL((k_encode_blk<2>), gd, bd, 0, st, a, c->ks); break;
-        default: hipLaunchKernelGGL((k_encode<3, 12, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        default: hipLaunchKernelGGL((k_encode<6, 12, 4, -1>), gd, bd, lds, st, a, c->ks); break;
     }
     return launch_check("k_encode");
 }
