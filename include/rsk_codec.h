@@ -25,6 +25,8 @@
  *   rsk_capture_filter_batch <- the pcap filter RCap installs: BuildFilterStr("tcp", srcIp, dstIp, srcPorts,
  *                            dstPorts, isServer) (cap/cap_util.cpp:67-144, cap/RCap.cpp:64-88) evaluated
  *                            per captured packet; rsk_filter_str renders the same string
+ *   rsk_tcp_send_seq_batch <- FakeTcp::Output's seq advance + RawTcp::Output's mIpId++      conn/FakeTcp.cpp:43-49, conn/RawTcp.cpp:111-121
+ *   rsk_tcp_recv_ack_batch <- FakeTcp::OnRecv's ack update                                  conn/FakeTcp.cpp:52-66
  *   rsk_demux_batch       <- the per-packet conn lookups of the receive path, batched:
  *                            INetGroup::Input by connKey (conn/INetGroup.cpp:57-83), IAppGroup::Input
  *                            by cmd (conn/IAppGroup.cpp:76-96), ServerGroup::OnRecv by IdBuf
@@ -284,6 +286,26 @@ int rsk_stage_capture_slots(uint32_t n, const uint8_t *arena, const uint64_t *ca
 int rsk_tcpinfo_encode_batch(rsk_ctx *ctx, uint32_t n, const uint32_t *src, const uint32_t *dst,
                              const uint16_t *sp, const uint16_t *dp, const uint32_t *seq,
                              const uint32_t *ack, const uint8_t *flag, uint8_t *rec, void *stream);
+
+/* ---- fake-TCP connection state on either side of the codec --------------------------------------- */
+/* Send: FakeTcp::Output (conn/FakeTcp.cpp:43-49) advances its connection's seq by
+ * RConn::HEAD_SIZE + nread after every frame RConn::Output produced, and RawTcp::Output
+ * (conn/RawTcp.cpp:111-121) stamps every packet it sends with mIpId++.  For a batch sent in order,
+ * packet i of connection conn[i] with rsk_encode_batch's status[i] (31 + P when framed):
+ *   framed (status > 0): ip_id[i] = *ip_id_next, then ++*ip_id_next (wraps at 2^16); and when
+ *       conn[i] < n_conn: seq[i] = conn_seq[conn[i]], then conn_seq[conn[i]] += status[i] (mod 2^32)
+ *   otherwise, or conn[i] >= n_conn: seq[i] = 0 (ip_id[i] = 0 when not framed)
+ * conn_seq [n_conn] and ip_id_next [1] are device state updated in place; seq / ip_id are what
+ * rsk_encode_wire_batch takes.  n <= 2^30; uses the demux workspace plus ~35 B per packet. */
+int rsk_tcp_send_seq_batch(rsk_ctx *ctx, uint32_t n, const uint32_t *conn, const int32_t *status,
+                           uint32_t n_conn, uint32_t *conn_seq, uint16_t *ip_id_next, uint32_t *seq,
+                           uint16_t *ip_id, void *stream);
+/* Receive: FakeTcp::OnRecv (conn/FakeTcp.cpp:52-66) raises its connection's ack to a delivered
+ * packet's TcpInfo seq (rsk_parse_decode_batch's tcp->seq) when that is larger (unsigned compare,
+ * as the reference), so over a batch conn_ack[c] = max(conn_ack[c], seq[i] of every packet i with
+ * delivered[i] != 0 and conn[i] == c) — independent of order; conn[i] >= n_conn is skipped. */
+int rsk_tcp_recv_ack_batch(rsk_ctx *ctx, uint32_t n, const uint32_t *conn, const uint8_t *delivered,
+                           const uint32_t *seq, uint32_t n_conn, uint32_t *conn_ack, void *stream);
 
 /* ---- receive demux: stable group-by of the VALID packets on decoded fields --- */
 /* The reference routes every VALID packet on its own: a map lookup per packet on the fields below,

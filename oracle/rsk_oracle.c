@@ -834,3 +834,30 @@ int orc_filter_str(const rsk_capture_filter *f, char *buf, size_t buf_len) {
     if (at + 1 > buf_len) return -1;
     return (int)at;
 }
+
+/* ---- fake-TCP connection state (restated from the reference, one packet at a time) ---------- */
+/* FakeTcp::Output (conn/FakeTcp.cpp:43-49): after INetConn::Output returns n >= 0 (the frame was
+ * sent), mInfo.UpdateSeq(nread + mInfo.seq + RConn::HEAD_SIZE); the packet carried the seq before
+ * the update.  RawTcp::Output (conn/RawTcp.cpp:111-121): SendRawTcp(..., mIpId++, ...) per sent
+ * packet.  Packets RConn::Output did not frame (status <= 0) are not sent through RawTcp. */
+void orc_tcp_send_seq_batch(uint32_t n, const uint32_t *conn, const int32_t *status, uint32_t n_conn,
+                            uint32_t *conn_seq, uint16_t *ip_id_next, uint32_t *seq, uint16_t *ip_id) {
+    for (uint32_t i = 0; i < n; ++i) {
+        seq[i] = 0;
+        ip_id[i] = 0;
+        if (status[i] <= 0) continue;
+        ip_id[i] = (*ip_id_next)++;
+        if (conn[i] >= n_conn) continue;
+        seq[i] = conn_seq[conn[i]];
+        conn_seq[conn[i]] = conn_seq[conn[i]] + (uint32_t)status[i];
+    }
+}
+
+/* FakeTcp::OnRecv (conn/FakeTcp.cpp:52-66): if (n >= 0) { if (mInfo.ack < info->seq) UpdateAck(info->seq); } */
+void orc_tcp_recv_ack_batch(uint32_t n, const uint32_t *conn, const uint8_t *delivered, const uint32_t *seq,
+                            uint32_t n_conn, uint32_t *conn_ack) {
+    for (uint32_t i = 0; i < n; ++i) {
+        if (!delivered[i] || conn[i] >= n_conn) continue;
+        if (conn_ack[conn[i]] < seq[i]) conn_ack[conn[i]] = seq[i];
+    }
+}

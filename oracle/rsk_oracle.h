@@ -108,6 +108,12 @@ int orc_capture_filter(const uint8_t *pkt, uint32_t cap_len, int datalink, const
 int orc_filter_str(const rsk_capture_filter *f, char *buf, size_t buf_len);
 
 /* KeyGenerator::KeyForTcp / KeyForUdp (src/util/KeyGenerator.cpp:16-36) */
+/* FakeTcp::Output seq advance + RawTcp::Output mIpId++ / FakeTcp::OnRecv ack (sequential loops) */
+void orc_tcp_send_seq_batch(uint32_t n, const uint32_t *conn, const int32_t *status, uint32_t n_conn,
+                            uint32_t *conn_seq, uint16_t *ip_id_next, uint32_t *seq, uint16_t *ip_id);
+void orc_tcp_recv_ack_batch(uint32_t n, const uint32_t *conn, const uint8_t *delivered, const uint32_t *seq,
+                            uint32_t n_conn, uint32_t *conn_ack);
+
 uint64_t orc_key_for_tcp(uint16_t sp, uint16_t dp);
 uint64_t orc_key_for_udp(uint16_t sp, uint16_t dp);
 

@@ -326,6 +326,20 @@ class Codec:
                                                   datalink, flags, ctypes.byref(tout), ctypes.byref(dout),
                                                   _stream(stream)), "rsk_parse_decode_slots_batch")
 
+    def tcp_send_seq_batch(self, conn, status, conn_seq, ip_id_next, seq, ip_id, stream=None) -> None:
+        """FakeTcp::Output's seq advance + RawTcp::Output's mIpId++ for a batch sent in order
+        (rsk_tcp_send_seq_batch); conn_seq / ip_id_next are device state updated in place."""
+        n = conn.numel()
+        _check(lib().rsk_tcp_send_seq_batch(self._ctx, n, _ptr(conn), _ptr(status), conn_seq.numel(), _ptr(conn_seq),
+                                            _ptr(ip_id_next), _ptr(seq), _ptr(ip_id), _stream(stream)),
+               "rsk_tcp_send_seq_batch")
+
+    def tcp_recv_ack_batch(self, conn, delivered, seq, conn_ack, stream=None) -> None:
+        """FakeTcp::OnRecv's ack update over a batch (rsk_tcp_recv_ack_batch)."""
+        n = conn.numel()
+        _check(lib().rsk_tcp_recv_ack_batch(self._ctx, n, _ptr(conn), _ptr(delivered), _ptr(seq), conn_ack.numel(),
+                                            _ptr(conn_ack), _stream(stream)), "rsk_tcp_recv_ack_batch")
+
     def tcpinfo_encode_batch(self, src, dst, sp, dp, seq, ack, flag, rec, stream=None) -> None:
         n = src.numel()
         _check(lib().rsk_tcpinfo_encode_batch(self._ctx, n, _ptr(src), _ptr(dst), _ptr(sp), _ptr(dp),

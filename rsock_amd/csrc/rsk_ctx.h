@@ -23,6 +23,9 @@ struct rsk_ctx {
     // compaction workspace
     void *ws = nullptr;
     uint32_t ws_n = 0;
+    // connection-state workspace (rsk_tcp_send_seq_batch, rsk_demux.hip)
+    void *sq_ws = nullptr;
+    size_t sq_ws_bytes = 0;
     // demux workspace (rsk_demux.hip)
     void *dm_ws = nullptr;
     size_t dm_ws_bytes = 0;

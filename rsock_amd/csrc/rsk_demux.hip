@@ -653,3 +653,168 @@ extern "C" int rsk_demux_batch(rsk_ctx *c, uint32_t n, const rsk_demux_in *in, u
                        out->perm, out->seg_off, out->n_seg, out->n_valid);
     return rsk::launch_check("k_dm_final");
 }
+
+// =============================================================================================
+// Connection state of the fake-TCP path around the codec: FakeTcp::Output's seq advance and
+// RawTcp::Output's IP id counter (send), FakeTcp::OnRecv's ack (receive).  include/rsk_codec.h.
+// =============================================================================================
+namespace {
+
+// framed packets of known connections take part in the group-by (status VALID), the rest do not
+__global__ __launch_bounds__(kBlock) void k_sq_flags(const uint32_t *conn, const int32_t *status, uint32_t n,
+                                                     uint32_t n_conn, int8_t *part, uint8_t *cmd0, uint32_t *framed) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const bool fr = status[i] > 0;                                  // RConn::Output framed it
+    part[i] = (int8_t)(fr && conn[i] < n_conn ? RSK_RECV_VALID : RSK_RECV_DROP);
+    cmd0[i] = 0;
+    framed[i] = fr ? 1u : 0u;
+}
+
+// frame lengths in segment (= connection) order, 0 past n_valid (the scan runs over n + 1 slots)
+__global__ __launch_bounds__(kBlock) void k_sq_lens(const uint32_t *perm, const uint32_t *nvp, const int32_t *status,
+                                                    uint32_t n, uint32_t *v) {
+    const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
+    if (j > n) return;
+    v[j] = j < *nvp ? (uint32_t)status[perm[j]] : 0u;
+}
+
+// one thread per segment: the connection's seq before the batch, relative to the scan, and its
+// advance over the batch (every connection is exactly one segment, so no two threads share it)
+__global__ __launch_bounds__(kBlock) void k_sq_conn(const uint32_t *nsegp, const uint32_t *seg_off,
+                                                    const uint32_t *seg_first, const uint32_t *conn,
+                                                    const uint32_t *pre, uint32_t *conn_seq, uint32_t *base) {
+    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
+    if (s >= *nsegp) return;
+    const uint32_t c = conn[seg_first[s]];
+    const uint32_t p0 = pre[seg_off[s]], p1 = pre[seg_off[s + 1]];
+    const uint32_t before = conn_seq[c];
+    base[c] = before - p0;          // mod 2^32, as TcpInfo::seq wraps
+    conn_seq[c] = before + (p1 - p0);
+}
+
+__global__ __launch_bounds__(kBlock) void k_sq_seq(const uint32_t *perm, const uint32_t *nvp, const uint32_t *conn,
+                                                   const uint32_t *base, const uint32_t *pre, uint32_t *seq) {
+    const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
+    if (j >= *nvp) return;
+    const uint32_t i = perm[j];
+    seq[i] = base[conn[i]] + pre[j];
+}
+
+__global__ __launch_bounds__(kBlock) void k_sq_ipid(const uint32_t *framed, const uint32_t *rank, uint32_t n,
+                                                    const uint16_t *ip_next, uint16_t *ip_id) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    ip_id[i] = framed[i] ? (uint16_t)(*ip_next + rank[i]) : (uint16_t)0;  // mIpId++ wraps at 2^16
+}
+
+__global__ void k_sq_ipid_advance(uint16_t *ip_next, const uint32_t *nfr) { *ip_next = (uint16_t)(*ip_next + *nfr); }
+
+__global__ __launch_bounds__(kBlock) void k_ack(const uint32_t *conn, const uint8_t *delivered, const uint32_t *seq,
+                                                uint32_t n, uint32_t n_conn, uint32_t *conn_ack) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n || !delivered[i] || conn[i] >= n_conn) return;
+    atomicMax(conn_ack + conn[i], seq[i]);  // FakeTcp.cpp:60-64: ack = seq when mInfo.ack < seq
+}
+
+struct SqWs {
+    int8_t *part;
+    uint8_t *cmd0;
+    uint32_t *framed, *rank, *perm, *seg_off, *seg_first, *v, *pre, *base, *nseg, *nvalid, *nfr;
+    ScanWs scan;
+};
+
+size_t sq_layout(uint32_t n, uint32_t n_conn, uint8_t *b, SqWs *w) {
+    size_t off = 0;
+    auto take = [&](size_t bytes) -> uint8_t * {
+        uint8_t *p = b ? b + off : nullptr;
+        off += (bytes + 255) & ~size_t(255);
+        return p;
+    };
+    SqWs d;
+    const size_t nc = (n + 1 + kScanChunk - 1) / kScanChunk + 1;
+    d.part = (int8_t *)take(n);
+    d.cmd0 = take(n);
+    d.framed = (uint32_t *)take(4ull * n);
+    d.rank = (uint32_t *)take(4ull * n);
+    d.perm = (uint32_t *)take(4ull * n);
+    d.seg_off = (uint32_t *)take(4ull * (n + 1));
+    d.seg_first = (uint32_t *)take(4ull * n);
+    d.v = (uint32_t *)take(4ull * (n + 1));
+    d.pre = (uint32_t *)take(4ull * (n + 1));
+    d.base = (uint32_t *)take(4ull * n_conn);
+    d.nseg = (uint32_t *)take(4);
+    d.nvalid = (uint32_t *)take(4);
+    d.nfr = (uint32_t *)take(4);
+    d.scan.sums = (uint32_t *)take(4ull * nc);
+    d.scan.sum_off = (uint32_t *)take(4ull * nc);
+    if (w) *w = d;
+    return off;
+}
+
+}  // namespace
+
+extern "C" int rsk_tcp_send_seq_batch(rsk_ctx *c, uint32_t n, const uint32_t *conn, const int32_t *status,
+                                      uint32_t n_conn, uint32_t *conn_seq, uint16_t *ip_id_next, uint32_t *seq,
+                                      uint16_t *ip_id, void *stream) {
+    if (!c) return RSK_EINVAL;
+    if (n == 0) return RSK_OK;
+    if (!conn || !status || !ip_id_next || !seq || !ip_id || (n_conn && !conn_seq)) return RSK_EINVAL;
+    if (n > (1u << 30)) return RSK_EINVAL;
+    rsk::DeviceGuard g(c->device);
+    if (!g.ok) return RSK_EDEVICE;
+    hipStream_t s = (hipStream_t)stream;
+    const size_t need = sq_layout(n, n_conn, nullptr, nullptr);
+    if (!c->sq_ws || c->sq_ws_bytes < need) {
+        if (c->sq_ws) {
+            hipError_t e = hipDeviceSynchronize();
+            if (e != hipSuccess) { rsk::set_error("hipDeviceSynchronize", e); return RSK_EDEVICE; }
+            (void)hipFree(c->sq_ws);
+            c->sq_ws = nullptr;
+            c->sq_ws_bytes = 0;
+        }
+        hipError_t e = hipMalloc(&c->sq_ws, need);
+        if (e != hipSuccess) { rsk::set_error("hipMalloc(seq workspace)", e); return RSK_ENOMEM; }
+        c->sq_ws_bytes = need;
+    }
+    SqWs w;
+    sq_layout(n, n_conn, static_cast<uint8_t *>(c->sq_ws), &w);
+    const unsigned nb = (n + kBlock - 1) / kBlock, nb1 = (n + 1 + kBlock - 1) / kBlock;
+    int r;
+    hipError_t e = hipMemsetAsync(seq, 0, 4ull * n, s);
+    if (e != hipSuccess) { rsk::set_error("hipMemsetAsync(seq)", e); return RSK_EDEVICE; }
+    hipLaunchKernelGGL(k_sq_flags, dim3(nb), dim3(kBlock), 0, s, conn, status, n, n_conn, w.part, w.cmd0, w.framed);
+    if ((r = rsk::launch_check("k_sq_flags"))) return r;
+    // IP ids: RawTcp::Output's mIpId++ over the framed packets in batch order (conn/RawTcp.cpp:119)
+    if ((r = scan_u32(w.framed, w.rank, n, w.nfr, w.scan, s))) return r;
+    hipLaunchKernelGGL(k_sq_ipid, dim3(nb), dim3(kBlock), 0, s, w.framed, w.rank, n, ip_id_next, ip_id);
+    hipLaunchKernelGGL(k_sq_ipid_advance, dim3(1), dim3(1), 0, s, ip_id_next, w.nfr);
+    if ((r = rsk::launch_check("k_sq_ipid"))) return r;
+    // seq: FakeTcp::Output's UpdateSeq(seq + 31 + nread) per connection, in batch order (FakeTcp.cpp:43-49):
+    // group the framed packets by connection (stable), one scan of their frame lengths in that order
+    rsk_demux_in din{};
+    din.status = w.part;
+    din.cmd = w.cmd0;
+    din.conv = conn;
+    rsk_demux_out dout{w.perm, w.seg_off, w.seg_first, w.nseg, w.nvalid};
+    if ((r = rsk_demux_batch(c, n, &din, RSK_DEMUX_CONV, &dout, stream))) return r;
+    hipLaunchKernelGGL(k_sq_lens, dim3(nb1), dim3(kBlock), 0, s, w.perm, w.nvalid, status, n, w.v);
+    if ((r = rsk::launch_check("k_sq_lens"))) return r;
+    if ((r = scan_u32(w.v, w.pre, n + 1, nullptr, w.scan, s))) return r;
+    hipLaunchKernelGGL(k_sq_conn, dim3(nb), dim3(kBlock), 0, s, w.nseg, w.seg_off, w.seg_first, conn, w.pre, conn_seq,
+                       w.base);
+    hipLaunchKernelGGL(k_sq_seq, dim3(nb), dim3(kBlock), 0, s, w.perm, w.nvalid, conn, w.base, w.pre, seq);
+    return rsk::launch_check("k_sq_seq");
+}
+
+extern "C" int rsk_tcp_recv_ack_batch(rsk_ctx *c, uint32_t n, const uint32_t *conn, const uint8_t *delivered,
+                                      const uint32_t *seq, uint32_t n_conn, uint32_t *conn_ack, void *stream) {
+    if (!c) return RSK_EINVAL;
+    if (n == 0) return RSK_OK;
+    if (!conn || !delivered || !seq || (n_conn && !conn_ack)) return RSK_EINVAL;
+    rsk::DeviceGuard g(c->device);
+    if (!g.ok) return RSK_EDEVICE;
+    hipLaunchKernelGGL(k_ack, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, (hipStream_t)stream, conn, delivered,
+                       seq, n, n_conn, conn_ack);
+    return rsk::launch_check("k_ack");
+}

@@ -1945,6 +1945,7 @@ void rsk_destroy(rsk_ctx *c) {
     DeviceGuard g(c->device);
     if (c->ws) (void)hipFree(c->ws);
     if (c->dm_ws) (void)hipFree(c->dm_ws);
+    if (c->sq_ws) (void)hipFree(c->sq_ws);
     if (c->shim_dev) (void)hipFree(c->shim_dev);
     if (c->shim_host) (void)hipHostFree(c->shim_host);
     if (c->shim_stream) (void)hipStreamDestroy(c->shim_stream);

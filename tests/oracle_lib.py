@@ -75,6 +75,8 @@ class Oracle:
         L.orc_decode_batch.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32] + [_vp] * 14 + [ctypes.c_int]
         L.orc_parse_decode_batch.argtypes = ([ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, _vp, _vp, _vp,
                                               _vp, ctypes.c_int, ctypes.c_int] + [_vp] * 20)
+        L.orc_tcp_send_seq_batch.argtypes = [ctypes.c_uint32, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp, _vp]
+        L.orc_tcp_recv_ack_batch.argtypes = [ctypes.c_uint32, _vp, _vp, _vp, ctypes.c_uint32, _vp]
 
     # ---- scalar ----
     def md5(self, msg: bytes) -> bytes:
@@ -163,6 +165,27 @@ class Oracle:
         assert r == 0
         S = int(ns[0])
         return [(int(first[s]), perm[seg_off[s]:seg_off[s + 1]].tolist()) for s in range(S)], int(nv[0])
+
+    def tcp_send_seq_batch(self, conn, status, conn_seq, ip_id_next: int):
+        """-> (seq, ip_id, conn_seq after, ip_id_next after) (orc_tcp_send_seq_batch)."""
+        n = len(conn)
+        c = np.ascontiguousarray(conn, np.uint32)
+        st = np.ascontiguousarray(status, np.int32)
+        cs = np.array(conn_seq, np.uint32)
+        ipn = np.array([ip_id_next], np.uint16)
+        seq = np.zeros(max(n, 1), np.uint32)
+        ipid = np.zeros(max(n, 1), np.uint16)
+        self.L.orc_tcp_send_seq_batch(n, _p(c), _p(st), len(cs), _p(cs), _p(ipn), _p(seq), _p(ipid))
+        return seq[:n], ipid[:n], cs, int(ipn[0])
+
+    def tcp_recv_ack_batch(self, conn, delivered, seq, conn_ack):
+        n = len(conn)
+        c = np.ascontiguousarray(conn, np.uint32)
+        dl = np.ascontiguousarray(delivered, np.uint8)
+        sq = np.ascontiguousarray(seq, np.uint32)
+        ca = np.array(conn_ack, np.uint32)
+        self.L.orc_tcp_recv_ack_batch(n, _p(c), _p(dl), _p(sq), len(ca), _p(ca))
+        return ca
 
     def splitmix_bytes(self, seed: int, n: int) -> np.ndarray:
         out = np.empty(n, np.uint8)

@@ -80,6 +80,14 @@ def main():
         ops[f"encode_wire_eth_v{v}"] = (lambda v=v: (cx.set_wire_variant(v), cx.output_wire_batch(
             *common, src, dst, sp, dp, seq, ack, flag, ipid, wiree, offe, ste, eth=eth, id_uniform=workload.ID_UNIFORM,
             pad16=True, stream=s), cx.set_wire_variant(0)))
+    # fake-TCP connection state: seq / IP id of a send batch over 64 connections, ack of a receive batch
+    conn64 = (torch.arange(n, device=dev, dtype=torch.int64) % 64).to(torch.int32)
+    cseq, cack = torch.zeros(64, dtype=torch.int32, device=dev), torch.zeros(64, dtype=torch.int32, device=dev)
+    ipn = torch.zeros(1, dtype=torch.int16, device=dev)
+    sq_seq, sq_ip = torch.empty(n, dtype=torch.int32, device=dev), torch.empty(n, dtype=torch.int16, device=dev)
+    deliv = torch.ones(n, dtype=torch.uint8, device=dev)
+    ops["tcp_send_seq"] = lambda: cx.tcp_send_seq_batch(conn64, w.status, cseq, ipn, sq_seq, sq_ip, stream=s)
+    ops["tcp_recv_ack"] = lambda: cx.tcp_recv_ack_batch(conn64, deliv, sq_seq, cack, stream=s)
     # receive demux on the decoded fields (frames of this config; C4 marks 1/16 corrupted, 5% control)
     w.corrupt_frames()
     dmx = rc.DemuxBuffers.alloc(n, dev)
@@ -144,6 +152,8 @@ def main():
         "capture_filter": 8 + 4 + 64 + 16 + 1 + 4,  # cap_off, cap_len, header windows, match, match_idx
         "decode_hdr": 32 + 2 + 27 + 4,
         "encode_hdr": 1 + 2 + 1 + 4 + 8 + 32 + 4,
+        "tcp_send_seq": 4 + 4 + 4 + 2,  # conn, status in; seq, ip_id out
+        "tcp_recv_ack": 4 + 1 + 4,      # conn, delivered, seq in
     }
     out = {}
     for k, t in times.items():
