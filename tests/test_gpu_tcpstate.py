@@ -48,7 +48,7 @@ def test_recv_ack_matches_oracle(codec, gpu, oracle):
     import torch
 
     rng = np.random.default_rng(9)
-    for n, n_conn in ((1000, 3), (200_000, 5000)):
+    for n, n_conn in ((1000, 3), (200_000, 5000), (300_000, 8192), (300_000, 8193), (100_000, 50_000)):
         conn = rng.integers(0, n_conn + 1, n).astype(np.uint32)
         dl = (rng.random(n) < 0.8).astype(np.uint8)
         seq = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
