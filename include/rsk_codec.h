@@ -378,6 +378,15 @@ typedef struct rsk_capture_filter {
 int rsk_capture_filter_batch(rsk_ctx *ctx, uint32_t n, const uint8_t *cap_arena, const uint64_t *cap_off,
                              const uint32_t *cap_len, int datalink, const rsk_capture_filter *filter,
                              uint8_t *match, uint32_t *match_idx, uint32_t *n_match, void *stream);
+/* The filter and rsk_parse_decode_batch in one pass over a capture batch (the parse reuses the
+ * filter's header window): match[i] as above; a packet the filter passes gets exactly
+ * rsk_parse_decode_batch's outputs, one it rejects (pcap never hands it to RawTcp::RawInput) gets
+ * parse_status RSK_PARSE_DROP, zero TcpInfo and dec->status RSK_RECV_DROP; dec->valid_idx lists the
+ * VALID packets in order. */
+int rsk_filter_parse_decode_batch(rsk_ctx *ctx, uint32_t n, const uint8_t *cap_arena, const uint64_t *cap_off,
+                                  const uint32_t *wire_len, const uint32_t *cap_len, int datalink, int flags,
+                                  const rsk_capture_filter *filter, uint8_t *match, const rsk_tcpinfo_out *tcp,
+                                  const rsk_decode_out *dec, void *stream);
 /* Host: the exact string BuildFilterStr returns for this filter (proto "tcp", addresses dotted),
  * NUL-terminated into buf.  Returns its length, or -1 if buf_len is too small. */
 int rsk_filter_str(const rsk_capture_filter *filter, char *buf, size_t buf_len);

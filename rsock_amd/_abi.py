@@ -152,6 +152,9 @@ SIGNATURES = [
     ("rsk_capture_filter_batch", ctypes.c_int,
      [_vp, ctypes.c_uint32, _vp, _vp, _vp, ctypes.c_int, ctypes.POINTER(CaptureFilter), _vp, _vp, _vp, _vp]),
     ("rsk_filter_str", ctypes.c_int, [ctypes.POINTER(CaptureFilter), ctypes.c_char_p, ctypes.c_size_t]),
+    ("rsk_filter_parse_decode_batch", ctypes.c_int,
+     [_vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(CaptureFilter), _vp,
+      ctypes.POINTER(TcpInfoOut), ctypes.POINTER(DecodeOut), _vp]),
     ("rsk_tcp_send_seq_batch", ctypes.c_int,
      [_vp, ctypes.c_uint32, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp]),
     ("rsk_tcp_recv_ack_batch", ctypes.c_int, [_vp, ctypes.c_uint32, _vp, _vp, _vp, ctypes.c_uint32, _vp, _vp]),

@@ -362,6 +362,18 @@ class Codec:
                                               ctypes.byref(out.abi()), _stream(stream)),
                "rsk_decode_headers_batch")
 
+    def filter_rawinput_batch(self, cap, cap_off, wire_len, cap_len, datalink: int, flags: int,
+                              filt: "_abi.CaptureFilter", match, tcp: TcpInfoBuffers, out: DecodeBuffers,
+                              compact: bool = True, stream=None) -> None:
+        """Capture filter + RawTcp::RawInput + RConn::OnRecv in one pass (rsk_filter_parse_decode_batch)."""
+        n = wire_len.numel()
+        tout = tcp.abi()
+        dout = out.abi(compact)
+        _check(lib().rsk_filter_parse_decode_batch(self._ctx, n, _ptr(cap), _ptr(cap_off), _ptr(wire_len),
+                                                   _ptr(cap_len), datalink, flags, ctypes.byref(filt), _ptr(match),
+                                                   ctypes.byref(tout), ctypes.byref(dout), _stream(stream)),
+               "rsk_filter_parse_decode_batch")
+
     def capture_filter_batch(self, cap, cap_off, cap_len, datalink: int, filt: "_abi.CaptureFilter", match,
                              match_idx=None, n_match=None, stream=None) -> None:
         """The capture filter RCap installs (rsk_capture_filter_batch) over a batch."""

@@ -1352,6 +1352,104 @@ struct ParseArgs {
 // SLOT: host-resident capture, only the first min(cap_len, slot) bytes of each packet were staged
 // (slot >= 64); every decision still uses the real cap_len, and a packet whose parse or decode needs
 // a byte past its slot gets RSK_PARSE_SLOT_SHORT (zero outputs) instead, for a whole resubmission.
+// HWIN: hw already holds the packet's first 64 bytes, loaded as below (the fused capture filter).
+struct ParseRes {
+    int ps;
+    uint32_t src, dst, sp, dp, seq, ack, fl, payo, plen;
+    Dec o;
+};
+
+template <int L, bool SLOT, bool HWIN>
+__device__ __forceinline__ ParseRes parse_one(const ParseArgs &a, const uint8_t *pkt, uint32_t wl, uint32_t cl,
+                                              uint32_t av, uint32_t (&hw)[16], const KeySched &ks) {
+    int ps = RSK_PARSE_DROP;
+    uint32_t src = 0, dst = 0, sp = 0, dp = 0, seq = 0, ack = 0, fl = 0, payo = 0, plen = 0;
+    Dec o = {0, 0, 0, 0, 0, 0, 0, 0, RSK_RECV_DROP};
+    do {
+        if (wl < 44u) break;                                   // :139
+        const uint8_t *last = pkt + (av ? av - 1u : 0u);
+        if (cl < (uint32_t)L) { ps = RSK_PARSE_MALFORMED; break; }
+        if (!HWIN) rsk::load_window16<16>(pkt, last, hw);  // HWIN: the caller loaded it
+        if (L == 14) {                                          // :144-151
+            if ((hw[3] & 0xffffu) != 0x0008u) break;           // OM_PROTO_IP read LE
+        } else {                                                // DLT_NULL :152-160
+            if (hw[0] != 2u) break;
+        }
+        constexpr uint32_t ipo = L;
+        if (cl < ipo + 20u) { ps = RSK_PARSE_MALFORMED; break; }
+        uint32_t ip[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) ip[k] = rsk::funnel(hw[L / 4 + k + 1], hw[L / 4 + k], L & 3);
+        if (((ip[2] >> 8) & 0xffu) != 6u) break;               // ip_p :167-172
+        const uint32_t ihl = (ip[0] & 15u) * 4u;
+        const uint32_t tcpo = ipo + ihl;
+        if (cl < tcpo + 20u) { ps = RSK_PARSE_MALFORMED; break; }
+        uint32_t th[4];
+        if (ihl == 20u) {
+            constexpr int T = L + 20;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) th[k] = rsk::funnel(hw[T / 4 + k + 1], hw[T / 4 + k], T & 3);
+        } else {
+            if (SLOT && tcpo + 16u > av) { ps = RSK_PARSE_SLOT_SHORT; break; }
+            rsk::load_window16<4>(pkt + tcpo, last, th);
+        }
+        const uint32_t thl = ((th[3] & 0xffu) >> 4) * 4u;
+        payo = tcpo + thl;
+        const int payload_len = (int)rsk::bswap16(ip[0] >> 16) - (int)(ihl + thl);  // :177
+        fl = (th[3] >> 8) & 0xffu;
+        src = ip[4];                                            // ip_dst.s_addr :213
+        dst = ip[3];                                            // ip_src.s_addr :215
+        sp = rsk::bswap16(th[0] >> 16);                         // ntohs(th_dport)
+        dp = rsk::bswap16(th[0] & 0xffffu);                     // ntohs(th_sport)
+        seq = rsk::bswap32(th[1]);
+        ack = rsk::bswap32(th[2]);
+        if ((fl & RSK_TH_SYN) && (a.flags & RSK_PARSE_HAS_ACK_POOL)) {  // :221-228
+            if (a.flags & RSK_PARSE_IS_SERVER) {
+                uint32_t t = src; src = dst; dst = t;
+                t = sp; sp = dp; dp = t;
+                t = seq; seq = ack; ack = t;
+            }
+            ps = RSK_PARSE_SYN;
+            break;
+        }
+        const bool close = (fl & (RSK_TH_FIN | RSK_TH_RST)) != 0;
+        if (payload_len < RSK_HASH_BUF_SIZE + 1 && !close) break;            // :232-234
+        if (payload_len < -32) break;                          // cap2uv size_t wrap :240
+        if (payload_len < 0) { ps = RSK_PARSE_MALFORMED; break; }
+        if (payload_len + 32 > RSK_MAX_PKT_SIZE) break;        // cap2uv :240-244
+        if ((uint64_t)payo + (uint64_t)payload_len > cl) { ps = RSK_PARSE_MALFORMED; break; }
+        if (SLOT && payload_len > RSK_HEAD_SIZE) {  // decode reads frame [0, 32) and frame[8 + len]
+            if (payo + 32u > av) { ps = RSK_PARSE_SLOT_SHORT; break; }
+            const uint32_t len = pkt[payo + 8u];
+            if (len != (uint32_t)RSK_ENC_HEAD_SIZE && (int)len < payload_len - 8 && payo + 9u + len > av) {
+                ps = RSK_PARSE_SLOT_SHORT;
+                break;
+            }
+        }
+        seq += (uint32_t)payload_len;                           // :235
+        plen = (uint32_t)payload_len;
+        ps = RSK_PARSE_DELIVER;
+        o = decode_frame(pkt + payo, payload_len, close, ks);
+    } while (false);
+    return ParseRes{ps, src, dst, sp, dp, seq, ack, fl, payo, plen, o};
+}
+
+__device__ __forceinline__ bool store_parse(const ParseArgs &a, const DecOut &d, uint64_t i, const ParseRes &r) {
+    const bool keep = r.ps == RSK_PARSE_DELIVER || r.ps == RSK_PARSE_SYN;
+    a.src[i] = keep ? r.src : 0u;
+    a.dst[i] = keep ? r.dst : 0u;
+    a.sp[i] = (uint16_t)(keep ? r.sp : 0u);
+    a.dp[i] = (uint16_t)(keep ? r.dp : 0u);
+    a.seq[i] = keep ? r.seq : 0u;
+    a.ack[i] = keep ? r.ack : 0u;
+    a.flag[i] = (uint8_t)(keep ? r.fl : 0u);
+    a.pst[i] = (int8_t)r.ps;
+    a.cpo[i] = (uint16_t)(keep ? r.payo : 0u);
+    a.cpl[i] = (uint16_t)r.plen;
+    store_dec(d, i, r.o);
+    return r.o.st == RSK_RECV_VALID;
+}
+
 template <int L, bool SLOT>
 __global__ __launch_bounds__(kBlock) void k_parse_decode(ParseArgs a, DecOut d, KeySched ks) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -1360,89 +1458,8 @@ __global__ __launch_bounds__(kBlock) void k_parse_decode(ParseArgs a, DecOut d, 
         const uint8_t *pkt = SLOT ? a.cap + (uint64_t)a.slot * i : a.cap + a.cap_off[i];
         const uint32_t wl = a.wire_len[i], cl = a.cap_len[i];
         const uint32_t av = SLOT ? (cl < a.slot ? cl : a.slot) : cl;  // bytes present at pkt
-        int ps = RSK_PARSE_DROP;
-        uint32_t src = 0, dst = 0, sp = 0, dp = 0, seq = 0, ack = 0, fl = 0, payo = 0, plen = 0;
-        Dec o = {0, 0, 0, 0, 0, 0, 0, 0, RSK_RECV_DROP};
-        do {
-            if (wl < 44u) break;                                   // :139
-            const uint8_t *last = pkt + (av ? av - 1u : 0u);
-            if (cl < (uint32_t)L) { ps = RSK_PARSE_MALFORMED; break; }
-            uint32_t hw[16];
-            rsk::load_window16<16>(pkt, last, hw);
-            if (L == 14) {                                          // :144-151
-                if ((hw[3] & 0xffffu) != 0x0008u) break;           // OM_PROTO_IP read LE
-            } else {                                                // DLT_NULL :152-160
-                if (hw[0] != 2u) break;
-            }
-            constexpr uint32_t ipo = L;
-            if (cl < ipo + 20u) { ps = RSK_PARSE_MALFORMED; break; }
-            uint32_t ip[5];
-#pragma unroll
-            for (int k = 0; k < 5; ++k) ip[k] = rsk::funnel(hw[L / 4 + k + 1], hw[L / 4 + k], L & 3);
-            if (((ip[2] >> 8) & 0xffu) != 6u) break;               // ip_p :167-172
-            const uint32_t ihl = (ip[0] & 15u) * 4u;
-            const uint32_t tcpo = ipo + ihl;
-            if (cl < tcpo + 20u) { ps = RSK_PARSE_MALFORMED; break; }
-            uint32_t th[4];
-            if (ihl == 20u) {
-                constexpr int T = L + 20;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) th[k] = rsk::funnel(hw[T / 4 + k + 1], hw[T / 4 + k], T & 3);
-            } else {
-                if (SLOT && tcpo + 16u > av) { ps = RSK_PARSE_SLOT_SHORT; break; }
-                rsk::load_window16<4>(pkt + tcpo, last, th);
-            }
-            const uint32_t thl = ((th[3] & 0xffu) >> 4) * 4u;
-            payo = tcpo + thl;
-            const int payload_len = (int)rsk::bswap16(ip[0] >> 16) - (int)(ihl + thl);  // :177
-            fl = (th[3] >> 8) & 0xffu;
-            src = ip[4];                                            // ip_dst.s_addr :213
-            dst = ip[3];                                            // ip_src.s_addr :215
-            sp = rsk::bswap16(th[0] >> 16);                         // ntohs(th_dport)
-            dp = rsk::bswap16(th[0] & 0xffffu);                     // ntohs(th_sport)
-            seq = rsk::bswap32(th[1]);
-            ack = rsk::bswap32(th[2]);
-            if ((fl & RSK_TH_SYN) && (a.flags & RSK_PARSE_HAS_ACK_POOL)) {  // :221-228
-                if (a.flags & RSK_PARSE_IS_SERVER) {
-                    uint32_t t = src; src = dst; dst = t;
-                    t = sp; sp = dp; dp = t;
-                    t = seq; seq = ack; ack = t;
-                }
-                ps = RSK_PARSE_SYN;
-                break;
-            }
-            const bool close = (fl & (RSK_TH_FIN | RSK_TH_RST)) != 0;
-            if (payload_len < RSK_HASH_BUF_SIZE + 1 && !close) break;            // :232-234
-            if (payload_len < -32) break;                          // cap2uv size_t wrap :240
-            if (payload_len < 0) { ps = RSK_PARSE_MALFORMED; break; }
-            if (payload_len + 32 > RSK_MAX_PKT_SIZE) break;        // cap2uv :240-244
-            if ((uint64_t)payo + (uint64_t)payload_len > cl) { ps = RSK_PARSE_MALFORMED; break; }
-            if (SLOT && payload_len > RSK_HEAD_SIZE) {  // decode reads frame [0, 32) and frame[8 + len]
-                if (payo + 32u > av) { ps = RSK_PARSE_SLOT_SHORT; break; }
-                const uint32_t len = pkt[payo + 8u];
-                if (len != (uint32_t)RSK_ENC_HEAD_SIZE && (int)len < payload_len - 8 && payo + 9u + len > av) {
-                    ps = RSK_PARSE_SLOT_SHORT;
-                    break;
-                }
-            }
-            seq += (uint32_t)payload_len;                           // :235
-            plen = (uint32_t)payload_len;
-            ps = RSK_PARSE_DELIVER;
-            o = decode_frame(pkt + payo, payload_len, close, ks);
-        } while (false);
-        const bool keep = ps == RSK_PARSE_DELIVER || ps == RSK_PARSE_SYN;
-        a.src[i] = keep ? src : 0u;
-        a.dst[i] = keep ? dst : 0u;
-        a.sp[i] = (uint16_t)(keep ? sp : 0u);
-        a.dp[i] = (uint16_t)(keep ? dp : 0u);
-        a.seq[i] = keep ? seq : 0u;
-        a.ack[i] = keep ? ack : 0u;
-        a.flag[i] = (uint8_t)(keep ? fl : 0u);
-        a.pst[i] = (int8_t)ps;
-        a.cpo[i] = (uint16_t)(keep ? payo : 0u);
-        a.cpl[i] = (uint16_t)plen;
-        store_dec(d, i, o);
-        valid = o.st == RSK_RECV_VALID;
+        uint32_t hw[16];
+        valid = store_parse(a, d, i, parse_one<L, SLOT, false>(a, pkt, wl, cl, av, hw, ks));
     }
     if (d.masks) compact_epilogue(d, valid);
 }
@@ -1546,43 +1563,76 @@ __device__ __forceinline__ int fp_main(const FPkt<L> &k, const rsk_capture_filte
     return fp_ports(k, f.dst_ports, primed ? 0u : 2u);
 }
 
+// the filter's view of one captured packet: the 64-B window at the link header and the 16-B window
+// at the transport header, both bounded by cap_len
+template <int L>
+__device__ __forceinline__ void filter_load(const uint8_t *p, uint32_t cl, FPkt<L> &k) {
+    k.cl = cl;
+    const uint8_t *last = p + (cl ? cl - 1u : 0u);
+    if (cl) rsk::load_window16<16>(p, last, k.w);
+    else
+#pragma unroll
+        for (int q = 0; q < 16; ++q) k.w[q] = 0;
+    if (L == 14) {
+        k.lt = cl < 14u ? -1 : ({ const uint32_t et = (k.b(12) << 8) | k.b(13); et == 0x0800u ? 4 : et == 0x86ddu ? 6 : 0; });
+    } else {
+        k.lt = cl < 4u ? -1 : (k.w[0] == 2u ? 4 : (k.w[0] == 24u || k.w[0] == 28u || k.w[0] == 30u) ? 6 : 0);
+    }
+    const uint32_t th = L + (k.lt == 6 ? 40u : k.ihl4());
+#pragma unroll
+    for (int q = 0; q < 4; ++q) k.t[q] = 0;
+    if (k.lt > 0 && th < cl) rsk::load_window16<4>(p + th, last, k.t);
+}
+
+template <int L>
+__device__ __forceinline__ bool filter_eval(const FPkt<L> &k, const rsk_capture_filter &f) {
+    int r;
+    if (!f.is_server) {
+        r = fp_main(k, f, false);
+    } else {  // ((syn) and F') or (F and (no syn))
+        r = fp_syn(k, true);
+        if (r == 1) r = fp_main(k, f, true);
+        if (r == 0) {
+            r = fp_main(k, f, false);
+            if (r == 1) r = fp_syn(k, false);
+        }
+    }
+    return r == 1;
+}
+
 template <int L>
 __global__ __launch_bounds__(kBlock) void k_capture_filter(FiltArgs a, DecOut d, rsk_capture_filter f) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     bool m = false;
     if (i < a.n) {
         FPkt<L> k;
-        const uint8_t *p = a.cap + a.cap_off[i];
-        k.cl = a.cap_len[i];
-        const uint8_t *last = p + (k.cl ? k.cl - 1u : 0u);
-        if (k.cl) rsk::load_window16<16>(p, last, k.w);
-        else
-#pragma unroll
-            for (int q = 0; q < 16; ++q) k.w[q] = 0;
-        if (L == 14) {
-            k.lt = k.cl < 14u ? -1 : ({ const uint32_t et = (k.b(12) << 8) | k.b(13); et == 0x0800u ? 4 : et == 0x86ddu ? 6 : 0; });
-        } else {
-            k.lt = k.cl < 4u ? -1 : (k.w[0] == 2u ? 4 : (k.w[0] == 24u || k.w[0] == 28u || k.w[0] == 30u) ? 6 : 0);
-        }
-        const uint32_t th = L + (k.lt == 6 ? 40u : k.ihl4());
-#pragma unroll
-        for (int q = 0; q < 4; ++q) k.t[q] = 0;
-        if (k.lt > 0 && th < k.cl) rsk::load_window16<4>(p + th, last, k.t);
-        int r;
-        if (!f.is_server) {
-            r = fp_main(k, f, false);
-        } else {  // ((syn) and F') or (F and (no syn))
-            r = fp_syn(k, true);
-            if (r == 1) r = fp_main(k, f, true);
-            if (r == 0) {
-                r = fp_main(k, f, false);
-                if (r == 1) r = fp_syn(k, false);
-            }
-        }
-        m = r == 1;
+        filter_load<L>(a.cap + a.cap_off[i], a.cap_len[i], k);
+        m = filter_eval(k, f);
         a.match[i] = m ? 1 : 0;
     }
     if (d.masks) compact_epilogue(d, m);
+}
+
+// Capture filter, then RawTcp::RawInput + RConn::OnRecv on the packets it passes, in one pass: the
+// parse reuses the filter's 64-B header window.  A packet the filter rejects never reached RawInput
+// in the reference (pcap drops it), so it gets match 0, RSK_PARSE_DROP and zero outputs.
+template <int L>
+__global__ __launch_bounds__(kBlock) void k_filter_parse_decode(ParseArgs a, DecOut d, KeySched ks, uint8_t *match,
+                                                                rsk_capture_filter f) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    bool valid = false;
+    if (i < a.n) {
+        const uint8_t *pkt = a.cap + a.cap_off[i];
+        const uint32_t wl = a.wire_len[i], cl = a.cap_len[i];
+        FPkt<L> k;
+        filter_load<L>(pkt, cl, k);
+        const bool m = filter_eval(k, f);
+        match[i] = m ? 1 : 0;
+        ParseRes r = {RSK_PARSE_DROP, 0, 0, 0, 0, 0, 0, 0, 0, 0, {0, 0, 0, 0, 0, 0, 0, 0, RSK_RECV_DROP}};
+        if (m) r = parse_one<L, false, true>(a, pkt, wl, cl, cl, k.w, ks);
+        valid = store_parse(a, d, i, r);
+    }
+    if (d.masks) compact_epilogue(d, valid);
 }
 
 __global__ __launch_bounds__(1024) void k_scan(const uint32_t *counts, uint32_t *offsets, uint32_t nb,
@@ -1852,6 +1902,15 @@ int run_compaction(rsk_ctx *c, uint32_t n, uint64_t *masks, uint32_t *counts, ui
         r = launch_check("k_scatter");
     }
     return r;
+}
+
+bool filter_ports_bad(const rsk_capture_filter *f) {
+    for (const rsk_port_list *pl : {&f->src_ports, &f->dst_ports}) {
+        if (pl->n_single > RSK_FILTER_MAX_PORTS || pl->n_range > RSK_FILTER_MAX_PORTS) return true;
+        for (uint32_t q = 0; q < pl->n_range; ++q)
+            if (pl->range[q][0] >= pl->range[q][1]) return true;  // RPortList::AddPortRange
+    }
+    return false;
 }
 
 // An empty batch (n == 0) is a no-op that may pass null arrays; it still zeroes a given n_valid.
@@ -2203,16 +2262,50 @@ int rsk_parse_decode_slots_batch(rsk_ctx *c, uint32_t n, const uint8_t *slots, u
     return parse_decode(c, n, slots, nullptr, slot, wire_len, cap_len, datalink, flags, tcp, dec, stream);
 }
 
+int rsk_filter_parse_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *cap_arena, const uint64_t *cap_off,
+                                  const uint32_t *wire_len, const uint32_t *cap_len, int datalink, int flags,
+                                  const rsk_capture_filter *f, uint8_t *match, const rsk_tcpinfo_out *tcp,
+                                  const rsk_decode_out *dec, void *stream) {
+    if (!c || !f || !tcp || !dec) return RSK_EINVAL;
+    if (datalink != RSK_DLT_EN10MB && datalink != RSK_DLT_NULL) return RSK_EINVAL;
+    if (filter_ports_bad(f)) return RSK_EINVAL;
+    if (n == 0) return empty_batch(c, dec->n_valid, stream);
+    if (!cap_arena || !cap_off || !wire_len || !cap_len || !match || !dec_out_ok(dec)) return RSK_EINVAL;
+    if (!tcp->src || !tcp->dst || !tcp->sp || !tcp->dp || !tcp->seq || !tcp->ack || !tcp->flag ||
+        !tcp->parse_status || !tcp->cap_pay_off || !tcp->cap_pay_len)
+        return RSK_EINVAL;
+    DeviceGuard g(c->device);
+    if (!g.ok) return RSK_EDEVICE;
+    const bool compact = dec->valid_idx || dec->n_valid;
+    uint64_t *masks = nullptr;
+    uint32_t *counts = nullptr, *offsets = nullptr;
+    if (compact) {
+        int r = ensure_ws(c, n);
+        if (r) return r;
+        ws_split(c, n, masks, counts, offsets);
+    }
+    ParseArgs a;
+    a.cap = cap_arena; a.cap_off = cap_off; a.wire_len = wire_len; a.cap_len = cap_len;
+    a.src = tcp->src; a.dst = tcp->dst; a.sp = tcp->sp; a.dp = tcp->dp; a.seq = tcp->seq; a.ack = tcp->ack;
+    a.flag = tcp->flag; a.pst = tcp->parse_status; a.cpo = tcp->cap_pay_off; a.cpl = tcp->cap_pay_len;
+    a.datalink = datalink; a.flags = flags; a.n = n; a.slot = 0;
+    DecOut d = make_dec_out(dec, masks, counts);
+    const hipStream_t st = (hipStream_t)stream;
+    if (datalink == RSK_DLT_EN10MB)
+        hipLaunchKernelGGL(k_filter_parse_decode<14>, dim3(grid_for(n)), dim3(kBlock), 0, st, a, d, c->ks, match, *f);
+    else
+        hipLaunchKernelGGL(k_filter_parse_decode<4>, dim3(grid_for(n)), dim3(kBlock), 0, st, a, d, c->ks, match, *f);
+    int r = launch_check("k_filter_parse_decode");
+    if (r || !compact) return r;
+    return run_compaction(c, n, masks, counts, offsets, dec, st);
+}
+
 int rsk_capture_filter_batch(rsk_ctx *c, uint32_t n, const uint8_t *cap_arena, const uint64_t *cap_off,
                              const uint32_t *cap_len, int datalink, const rsk_capture_filter *f, uint8_t *match,
                              uint32_t *match_idx, uint32_t *n_match, void *stream) {
     if (!c || !f || (n && (!cap_arena || !cap_off || !cap_len || !match))) return RSK_EINVAL;
     if (datalink != RSK_DLT_EN10MB && datalink != RSK_DLT_NULL) return RSK_EINVAL;
-    for (const rsk_port_list *pl : {&f->src_ports, &f->dst_ports}) {
-        if (pl->n_single > RSK_FILTER_MAX_PORTS || pl->n_range > RSK_FILTER_MAX_PORTS) return RSK_EINVAL;
-        for (uint32_t q = 0; q < pl->n_range; ++q)
-            if (pl->range[q][0] >= pl->range[q][1]) return RSK_EINVAL;  // RPortList::AddPortRange
-    }
+    if (filter_ports_bad(f)) return RSK_EINVAL;
     if (n == 0) return empty_batch(c, n_match, stream);
     DeviceGuard g(c->device);
     if (!g.ok) return RSK_EDEVICE;

@@ -100,6 +100,9 @@ def main():
     fnm = torch.empty(1, dtype=torch.int32, device=dev)
     filt = rc.make_filter(dst_singles=[10001, 10002], dst_ranges=[(20000, 30000)], is_server=True)
     ops["capture_filter"] = lambda: cx.capture_filter_batch(wiree, offe, ste, 1, filt, fmatch, fidx, fnm, stream=s)
+    tcp2, pdec2 = rc.TcpInfoBuffers.alloc(n, dev), rc.DecodeBuffers.alloc(n, dev)
+    ops["filter_parse_decode"] = lambda: cx.filter_rawinput_batch(wiree, offe, ste, ste, 1, 0, filt, fmatch, tcp2,
+                                                                  pdec2, stream=s)
     # header-only kernels: contiguous 32-B slots (no dependent offset load, no scattered headers)
     slots = w.frame[w.frame_off.view(-1, 1) + torch.arange(32, device=dev).view(1, -1)].reshape(-1).contiguous()
     hdec = rc.DecodeBuffers.alloc(n, dev)
@@ -150,6 +153,7 @@ def main():
         "demux": 1 + 1 + 8 + 8 + 4,  # status, cmd, id, conn_key in; perm out (+ per-segment words)
         "demux_64conn": 1 + 1 + 8 + 8 + 4,
         "capture_filter": 8 + 4 + 64 + 16 + 1 + 4,  # cap_off, cap_len, header windows, match, match_idx
+        "filter_parse_decode": 8 + 4 + 64 + 16 + 1 + 54 + 32 + 16 + 21 + 4 + 73 - 42,
         "decode_hdr": 32 + 2 + 27 + 4,
         "encode_hdr": 1 + 2 + 1 + 4 + 8 + 32 + 4,
         "tcp_send_seq": 4 + 4 + 4 + 2,  # conn, status in; seq, ip_id out
