@@ -25,6 +25,7 @@
  *   rsk_capture_filter_batch <- the pcap filter RCap installs: BuildFilterStr("tcp", srcIp, dstIp, srcPorts,
  *                            dstPorts, isServer) (cap/cap_util.cpp:67-144, cap/RCap.cpp:64-88) evaluated
  *                            per captured packet; rsk_filter_str renders the same string
+ *   rsk_filter_parse_decode_batch <- that filter fused with RawTcp::RawInput + RConn::OnRecv (one pass)
  *   rsk_tcp_send_seq_batch <- FakeTcp::Output's seq advance + RawTcp::Output's mIpId++      conn/FakeTcp.cpp:43-49, conn/RawTcp.cpp:111-121
  *   rsk_tcp_recv_ack_batch <- FakeTcp::OnRecv's ack update                                  conn/FakeTcp.cpp:52-66
  *   rsk_demux_batch       <- the per-packet conn lookups of the receive path, batched:
