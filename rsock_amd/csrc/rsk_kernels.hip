@@ -564,12 +564,20 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
 // 4 DPP per-packet only, 5 (unused), 6 = 3 with the tag deferred into the copy loop for long frames.
 // Tiled mapping: wave t takes packets [64t, 64t + 64) (coalesced descriptor loads, but the 5000+
 // co-resident waves each stream their own ~92 KB region).
-template <int MODE, int PU, int U, int NT>
+// MAP 1 (A/B): workgroups are dispatched round-robin over the 8 XCDs, so by default XCD x runs
+// blocks x, x + 8, ...; MAP 1 renumbers them so that XCD x owns one contiguous eighth of the batch.
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
+    const uint32_t x = b & 7u, k = b >> 3, q = nb >> 3, r = nb & 7u;
+    return x < r ? x * (q + 1u) + k : r * (q + 1u) + (x - r) * q + k;
+}
+
+template <int MODE, int PU, int U, int NT, int MAP = 0>
 __global__ __launch_bounds__(kBlock) void k_encode(EncArgs a, KeySched ks) {
     __shared__ CopyRec recs[kWavesPerBlock][64];
     __shared__ uint32_t cend[kWavesPerBlock][64];
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    const uint64_t base = ((uint64_t)blockIdx.x * kWavesPerBlock + w) * 64u;
+    const uint32_t blk = MAP == 1 ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint64_t base = ((uint64_t)blk * kWavesPerBlock + w) * 64u;
     if (base >= a.n) return;  // wave-uniform; no block barriers below
     encode_set<MODE, PU, U, NT>(a, ks, base + lane, lane, recs[w], cend[w]);
 }
@@ -706,13 +714,36 @@ struct WireGeom {
     static constexpr int IPC = E + 10;                // IPv4 checksum byte offset
 };
 
+// payload bytes [0, 16) of a P-byte payload as 4 LE words (bytes past P zero)
+__device__ __forceinline__ void wire_payload_prefix(const uint8_t *pay, uint32_t P, uint32_t (&pw)[4]) {
+    rsk::load_window<4>(pay, pay + P - 1, pw);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int k = (int)P - 4 * q;
+        pw[q] &= k >= 4 ? 0xffffffffu : (k <= 0 ? 0u : ((1u << (8 * k)) - 1u));
+    }
+}
+
+// those words into the prefix image at wire offset HB (the part that falls inside the NPRE chunks)
+template <int E>
+__device__ __forceinline__ void wire_put_prefix(uint32_t (&PW)[WireGeom<E>::NPW], const uint32_t (&pw)[4]) {
+    using G = WireGeom<E>;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int off = G::HB + 4 * q;
+        const int nb = (off + 4 <= 4 * G::NPW) ? 4 : 4 * G::NPW - off;
+        if (nb > 0) put_bytes(PW, off, pw[q], nb);
+    }
+}
+
 // ---- phase 1 (one lane per packet): the wire prefix image PW = link header, IPv4 header (with its
 // checksum), TCP header (checksum 0), frame bytes [0, 31) and payload bytes [0, D0) (masked to P);
 // sum_pre = TCP checksum contribution of the pseudo-header and PW from the TCP header on; the
 // packet status becomes the wire length.
 template <int E>
 __device__ __forceinline__ void wire_phase1(const EncArgs &a, const WireArgs &wa, const Lane1 &L, uint64_t i,
-                                            uint32_t (&PW)[WireGeom<E>::NPW], uint32_t &sum_pre, int32_t &wst) {
+                                            uint32_t (&PW)[WireGeom<E>::NPW], uint32_t &sum_pre, int32_t &wst,
+                                            bool pre = true) {
     using G = WireGeom<E>;
 #pragma unroll
     for (int q = 0; q < G::NPW; ++q) PW[q] = 0;
@@ -749,20 +780,12 @@ __device__ __forceinline__ void wire_phase1(const EncArgs &a, const WireArgs &wa
     // frame bytes [0, 31) = tag + EncHead (H[7]'s top byte is payload[0], written below)
 #pragma unroll
     for (int q = 0; q < 8; ++q) put_bytes(PW, G::HL + 4 * q, L.H[q], q == 7 ? 3 : 4);
-    // payload bytes [0, 16) (bounded by P; bytes past P stay zero)
-    const uint8_t *pay = a.payload + L.po;
-    uint32_t pw[4];
-    rsk::load_window<4>(pay, pay + P - 1, pw);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int k = (int)P - 4 * q;
-        pw[q] &= k >= 4 ? 0xffffffffu : (k <= 0 ? 0u : ((1u << (8 * k)) - 1u));
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int off = G::HB + 4 * q;
-        const int nb = (off + 4 <= 4 * G::NPW) ? 4 : 4 * G::NPW - off;
-        if (nb > 0) put_bytes(PW, off, pw[q], nb);
+    // payload bytes [0, 16) (bounded by P; bytes past P stay zero); !pre: left to the copy loop
+    // (copy_wire_pkt_dpp<..., TAG = true>), which adds them with the tag
+    if (pre) {
+        uint32_t pw[4];
+        wire_payload_prefix(a.payload + L.po, P, pw);
+        wire_put_prefix<E>(PW, pw);
     }
     // pseudo-header (src, dst, 0, 6, tcp_len) + TCP header + prefix frame/payload bytes, from the
     // TCP header start (even offset E + 20) to the end of the prefix chunks
@@ -855,9 +878,15 @@ __device__ __forceinline__ void copy_wire_pkt(const EncArgs &a, const Lane1 &L, 
 
 // ---- the same with one aligned load per chunk: the funnel partner comes from lane + 1 by DPP (as
 // copy_pkt_dpp), all PU packets' loads issued before the first shift. ------------------------------
-template <int E, int PU, int NT>
-__device__ __forceinline__ void copy_wire_pkt_dpp(const EncArgs &a, const Lane1 &L, const uint32_t *stage,
-                                                  uint32_t sum_pre, int32_t wst, uint32_t lane, uint64_t vm) {
+// TAG (sets of long frames, as copy_pkt_dpp_tag): phase 1 left the tag, payload[0] at frame byte
+// 31 and the payload prefix bytes out of the prefix images, so that each payload's first line is read
+// once, here, next to the chunk loads that fetch it anyway.  Lane p loads packet p's first 16 payload
+// bytes before the chunk loads, runs the MD5 while they are in flight, ORs the missing bytes into
+// the packet's LDS prefix image and hands their checksum share to the packet's checksum.
+template <int E, int PU, int NT, bool TAG = false>
+__device__ __forceinline__ void copy_wire_pkt_dpp(const EncArgs &a, const KeySched &ks, const Lane1 &L,
+                                                  uint32_t *stage, uint32_t sum_pre, int32_t wst, uint32_t lane,
+                                                  uint64_t vm) {
     using G = WireGeom<E>;
     while (vm) {
         uint32_t js[PU];
@@ -867,6 +896,21 @@ __device__ __forceinline__ void copy_wire_pkt_dpp(const EncArgs &a, const Lane1 
             on[p] = vm != 0ull;
             js[p] = on[p] ? (uint32_t)__builtin_ctzll(vm) : 0u;
             if (on[p]) vm &= vm - 1ull;
+        }
+        uint32_t pw[4] = {0u, 0u, 0u, 0u}, myP = 0, myj = 0;  // TAG: lane p's packet
+        if constexpr (TAG) {
+            uint64_t mypo = 0;
+#pragma unroll
+            for (int p = 0; p < PU; ++p) {  // uniform readlanes, per-lane selects
+                const uint32_t wl = on[p] ? rdl((uint32_t)wst, js[p]) : 0u;
+                const uint64_t po = rdl64(L.po, js[p]);
+                if (lane == (uint32_t)p) {
+                    myP = on[p] ? wl - G::HB : 0u;
+                    mypo = po;
+                    myj = js[p];
+                }
+            }
+            if (myP) wire_payload_prefix(a.payload + mypo, myP, pw);
         }
         uint4 A[PU][2];
         uint32_t wlen[PU], shp[PU];
@@ -886,6 +930,26 @@ __device__ __forceinline__ void copy_wire_pkt_dpp(const EncArgs &a, const Lane1 
                 A[p][q] = make_uint4(0u, 0u, 0u, 0u);
                 if (on[p] && (int32_t)(16u * m) <= last_rel) A[p][q] = ld16<0>(src_al + 16u * m);
             }
+        }
+        uint32_t dsum = 0;  // TAG: lane p, checksum share of the bytes it adds to packet p's prefix image
+        if constexpr (TAG) {
+            uint32_t t0, t1;
+            rsk::md5_tag(ks, pw[0] & 0xffu, t0, t1);
+            uint32_t D[G::NPW];
+#pragma unroll
+            for (int q = 0; q < G::NPW; ++q) D[q] = 0;
+            put_bytes(D, G::HL, t0, 4);
+            put_bytes(D, G::HL + 4, t1, 4);
+            put_bytes(D, G::HL + RSK_HEAD_SIZE - 1, pw[0] & 0xffu, 1);  // frame byte 31 = payload[0]
+            wire_put_prefix<E>(D, pw);
+            if (myP) {
+#pragma unroll
+                for (int q = G::HL / 4; q < G::NPW; ++q) {
+                    stage[myj * G::NPW + q] |= D[q];
+                    dsum += hsum(D[q]);
+                }
+            }
+            wave_lds_sync();
         }
         uint4 v[PU][2];
         uint32_t ck[PU];
@@ -911,7 +975,8 @@ __device__ __forceinline__ void copy_wire_pkt_dpp(const EncArgs &a, const Lane1 
             ck[p] = part;
         }
 #pragma unroll
-        for (int p = 0; p < PU; ++p) ck[p] = ~fold16(wave_sum(ck[p]) + rdl(sum_pre, js[p])) & 0xffffu;
+        for (int p = 0; p < PU; ++p)
+            ck[p] = ~fold16(wave_sum(ck[p]) + rdl(sum_pre, js[p]) + (TAG ? rdl(dsum, (uint32_t)p) : 0u)) & 0xffffu;
 #pragma unroll
         for (int p = 0; p < PU; ++p) {
             if (!on[p]) continue;
@@ -1081,7 +1146,8 @@ __device__ __forceinline__ void copy_wire_bytes(const EncArgs &a, const Lane1 &L
 // MODE: 0 per-packet, 1 flat, 2 hybrid (per-wave choice on the set's mean wire length, one launch),
 // 3 / 4 = the per-packet / flat halves of the two-launch hybrid: each wave re-derives the same
 // choice from pay_len and frame_off alone and returns unless it is its launch's path, so every set
-// is handled exactly once and each launch sizes LDS (hence occupancy) for its own path only.
+// is handled exactly once and each launch sizes LDS (hence occupancy) for its own path only;
+// 5 = 3 with the tag and payload prefix deferred into the copy loop for sets of long frames.
 template <int E, int MODE>
 struct WireLds {
     static constexpr int kStage = 64 * WireGeom<E>::NPW * 4;  // prefix images (both paths)
@@ -1117,11 +1183,20 @@ __global__ __launch_bounds__(kBlock) void k_encode_wire(EncArgs a, WireArgs wa, 
         }
         if (wire_flat_choice<E>(v0, wl) != (MODE == 4)) return;
     }
-    const Lane1 L = encode_phase1(a, ks, i);
+    Lane1 L = encode_phase1<MODE != 5>(a, ks, i);
+    bool defer = false;
+    if constexpr (MODE == 5) {  // as k_encode MODE 6: set mean frame length decides
+        const bool v = L.st > 0 && !L.slow;
+        uint32_t fl = v ? (uint32_t)L.st : 0u;
+#pragma unroll
+        for (int off = 32; off; off >>= 1) fl += __shfl_xor(fl, off);
+        defer = fl >= kDeferTagMeanBytes * (uint32_t)__popcll(__ballot(v));
+        if (!defer || L.slow) encode_tag(a, ks, L);
+    }
     uint32_t PW[G::NPW];
     uint32_t sum_pre;
     int32_t wst;
-    wire_phase1<E>(a, wa, L, i, PW, sum_pre, wst);
+    wire_phase1<E>(a, wa, L, i, PW, sum_pre, wst, !defer || L.slow);
     const bool vec = L.st > 0 && !L.slow;
     const uint64_t vm = __ballot(vec);
     bool flat = MODE == 1 || MODE == 4;
@@ -1150,10 +1225,14 @@ __global__ __launch_bounds__(kBlock) void k_encode_wire(EncArgs a, WireArgs wa, 
             const uint64_t nfo = (uint64_t)(uint32_t)__shfl_down((int)(uint32_t)L.fo, 1) |
                                  ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(L.fo >> 32), 1) << 32);
             const bool nvec = __shfl_down((int)vec, 1) != 0;
-            if (__ballot(vec && nvec && lane != 63u && end != nfo))
-                copy_wire_pkt_dpp<E, PU - 100, 2>(a, L, stage, sum_pre, wst, lane, vm);
-            else
-                copy_wire_pkt_dpp<E, PU - 100, 0>(a, L, stage, sum_pre, wst, lane, vm);
+            const bool gaps = __ballot(vec && nvec && lane != 63u && end != nfo) != 0ull;
+            if (MODE == 5 && defer) {
+                if (gaps) copy_wire_pkt_dpp<E, PU - 100, 2, true>(a, ks, L, stage, sum_pre, wst, lane, vm);
+                else copy_wire_pkt_dpp<E, PU - 100, 0, true>(a, ks, L, stage, sum_pre, wst, lane, vm);
+            } else {
+                if (gaps) copy_wire_pkt_dpp<E, PU - 100, 2>(a, ks, L, stage, sum_pre, wst, lane, vm);
+                else copy_wire_pkt_dpp<E, PU - 100, 0>(a, ks, L, stage, sum_pre, wst, lane, vm);
+            }
         }
         else copy_wire_pkt<E, PU>(a, L, stage, sum_pre, wst, lane, vm);
     }
@@ -1965,17 +2044,17 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 //  23/24 = the default with PU=8/16
 // v + 100 * cap (cap 1..4): the same kernel held to `cap` blocks per CU by unused dynamic LDS.
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
-    if (!c || v < 0 || v % 100 > 24 || v / 100 > 4) return RSK_EINVAL;
+    if (!c || v < 0 || v % 100 > 25 || v / 100 > 4) return RSK_EINVAL;
     c->enc_variant = v;
     return RSK_OK;
 }
 
 // Internal (A/B and tests): wire-build copy path.  0 = two-launch hybrid whose per-packet half uses the
-// one-load DPP copy, 8 packets per iteration (default), 1 = per-packet, 2 = flat, 3 = one-launch
-// hybrid, 4 = two-launch hybrid with the two-load copy PU=2 (the default before), 5 = the same PU=4,
-// 6 / 7 = DPP copy PU=4 / 16.
+// one-load DPP copy, 8 packets per iteration, tag + payload prefix in the copy loop for sets of long
+// frames (default), 1 = per-packet, 2 = flat, 3 = one-launch hybrid, 4 = two-launch hybrid with the
+// two-load copy PU=2, 5 = the same PU=4, 6 / 7 = DPP copy PU=4 / 16, 8 = 0 with the tag in phase 1.
 int rsk__set_wire_variant(rsk_ctx *c, int v) {
-    if (!c || v < 0 || v > 7) return RSK_EINVAL;
+    if (!c || v < 0 || v > 8) return RSK_EINVAL;
     c->wire_variant = v;
     return RSK_OK;
 }
@@ -2056,6 +2135,7 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         case 22: hipLaunchKernelGGL((k_encode<3, 12, 4, -1>), gd, bd, lds, st, a, c->ks); break;
         case 23: hipLaunchKernelGGL((k_encode<6, 8, 4, -1>), gd, bd, lds, st, a, c->ks); break;
         case 24: hipLaunchKernelGGL((k_encode<6, 16, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 25: hipLaunchKernelGGL((k_encode<6, 12, 4, -1, 1>), gd, bd, lds, st, a, c->ks); break;
         case 1: hipLaunchKernelGGL((k_encode<0, 1, 4, 0>), gd, bd, 0, st, a, c->ks); break;
         case 2: hipLaunchKernelGGL((k_encode<1, 4, 2, 0>), gd, bd, 0, st, a, c->ks); break;
         case 3: hipLaunchKernelGGL((k_encode<1, 4, 4, 0>), gd, bd, 0, st, a, c->ks); break;
@@ -2111,7 +2191,8 @@ int rsk_encode_wire_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const
         else if (v == 5) { RSK_WIRE(14, 3, 4, 2); RSK_WIRE(14, 4, 2, 2); }
         else if (v == 6) { RSK_WIRE(14, 3, 104, 2); RSK_WIRE(14, 4, 2, 2); }
         else if (v == 7) { RSK_WIRE(14, 3, 116, 2); RSK_WIRE(14, 4, 2, 2); }
-        else { RSK_WIRE(14, 3, 108, 2); RSK_WIRE(14, 4, 2, 2); }
+        else if (v == 8) { RSK_WIRE(14, 3, 108, 2); RSK_WIRE(14, 4, 2, 2); }
+        else { RSK_WIRE(14, 5, 108, 2); RSK_WIRE(14, 4, 2, 2); }
     } else {
         if (v == 1) RSK_WIRE(0, 0, 2, 4);
         else if (v == 2) RSK_WIRE(0, 1, 2, 2);
@@ -2120,7 +2201,8 @@ int rsk_encode_wire_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const
         else if (v == 5) { RSK_WIRE(0, 3, 4, 2); RSK_WIRE(0, 4, 2, 2); }
         else if (v == 6) { RSK_WIRE(0, 3, 104, 2); RSK_WIRE(0, 4, 2, 2); }
         else if (v == 7) { RSK_WIRE(0, 3, 116, 2); RSK_WIRE(0, 4, 2, 2); }
-        else { RSK_WIRE(0, 3, 108, 2); RSK_WIRE(0, 4, 2, 2); }
+        else if (v == 8) { RSK_WIRE(0, 3, 108, 2); RSK_WIRE(0, 4, 2, 2); }
+        else { RSK_WIRE(0, 5, 108, 2); RSK_WIRE(0, 4, 2, 2); }
     }
 #undef RSK_WIRE
     return launch_check("k_encode_wire");

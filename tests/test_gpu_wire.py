@@ -19,14 +19,15 @@ KEY = b"hello135"
 @pytest.mark.parametrize("eth", [False, True])
 @pytest.mark.parametrize("layout", ["aligned", "odd_payload", "odd_wire"])
 @pytest.mark.parametrize("pad16", [False, True])
-@pytest.mark.parametrize("mix", ["mixed", "short", "bimodal"])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])  # see rsk__set_wire_variant
+@pytest.mark.parametrize("mix", ["mixed", "short", "bimodal", "long"])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8])  # see rsk__set_wire_variant
 def test_wire_batch(codec, gpu, oracle, eth, layout, pad16, mix, variant):
     import torch
 
     rng = np.random.default_rng(hash((eth, layout, pad16, mix)) & 0xFFFF)
     lens = [0, 1, 2, 8, 9, 10, 11, 12, 15, 16, 17, 31, 32, 33, 100, 1000, 1400, 1468, 1469, 1470] + \
-        list(rng.integers(1, 1470 if mix == "mixed" else 160, 400))
+        list(rng.integers(1200 if mix == "long" else 1, 1470 if mix in ("mixed", "long") else 160, 400))
+    # "long": every set's mean frame >= 1024 B, so the deferred-tag copy also meets the 20 edge lengths
     if mix == "bimodal":  # short sets then long sets: both launches of the split hybrid in one batch
         lens = lens[:20] + list(rng.integers(1, 160, 236)) + list(rng.integers(1000, 1470, 200))
     n = len(lens)
