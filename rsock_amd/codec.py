@@ -249,7 +249,8 @@ class Codec:
         with the one-load DPP per-packet copy, 12 packets per iteration, the tag computed in the copy loop
         for sets of long frames and nontemporal stores for sets whose frames leave gaps (default); 1-12
         per-packet / flat / non-temporal / interleaved variants, 13 the two-load hybrid, 14-24 DPP
-        variants, 25 the default with XCD-contiguous block numbering; + 100 * cap holds the kernel to cap blocks per CU (list in rsk_kernels.hip).  Every variant is parity-tested; used for in-process A/B."""
+        variants, 25 the default with XCD-contiguous block numbering,
+        26-28 the default with 2 / 4 / 8 sets per wave; + 100 * cap holds the kernel to cap blocks per CU (list in rsk_kernels.hip).  Every variant is parity-tested; used for in-process A/B."""
         fn = lib().rsk__set_encode_variant
         fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
         _check(fn(self._ctx, v), "rsk__set_encode_variant")
@@ -257,7 +258,7 @@ class Codec:
     def set_wire_variant(self, v: int) -> None:
         """Internal tuning knob for k_encode_wire: 0 two-launch hybrid with the DPP per-packet copy
         and the tag deferred into the copy loop for long frames (default), 1 per-packet, 2 flat, 3 one-launch
-        hybrid, 4-8 A/B variants (8 = the default with the tag in phase 1; list in rsk_kernels.hip)."""
+        hybrid, 4-9 A/B variants (8 = the default with the tag in phase 1; list in rsk_kernels.hip)."""
         fn = lib().rsk__set_wire_variant
         fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
         _check(fn(self._ctx, v), "rsk__set_wire_variant")

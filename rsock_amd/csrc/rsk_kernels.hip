@@ -273,8 +273,9 @@ __device__ __forceinline__ void copy_pkt_dpp(const EncArgs &a, const Lane1 &L, u
             uint4 B[2];
             B[0] = make_uint4(wave_shl1(A[p][0].x), wave_shl1(A[p][0].y), wave_shl1(A[p][0].z), wave_shl1(A[p][0].w));
             B[1] = make_uint4(wave_shl1(A[p][1].x), wave_shl1(A[p][1].y), wave_shl1(A[p][1].z), wave_shl1(A[p][1].w));
-            if (lane == 63u)
-                B[0] = make_uint4(rdl(A[p][1].x, 0), rdl(A[p][1].y, 0), rdl(A[p][1].z, 0), rdl(A[p][1].w, 0));
+            const uint4 l0 = make_uint4(rdl(A[p][1].x, 0), rdl(A[p][1].y, 0), rdl(A[p][1].z, 0),
+                                        rdl(A[p][1].w, 0));  // read in uniform flow (see k_encode)
+            if (lane == 63u) B[0] = l0;
             uint32_t Hj[8];  // packet's head words, read out in uniform control flow (SGPRs)
 #pragma unroll
             for (int t = 0; t < 8; ++t) Hj[t] = rdl(L.H[t], js[p]);
@@ -341,8 +342,9 @@ __device__ __forceinline__ void copy_pkt_dpp_tag(const EncArgs &a, const KeySche
             uint4 B[2];
             B[0] = make_uint4(wave_shl1(A[p][0].x), wave_shl1(A[p][0].y), wave_shl1(A[p][0].z), wave_shl1(A[p][0].w));
             B[1] = make_uint4(wave_shl1(A[p][1].x), wave_shl1(A[p][1].y), wave_shl1(A[p][1].z), wave_shl1(A[p][1].w));
-            if (lane == 63u)
-                B[0] = make_uint4(rdl(A[p][1].x, 0), rdl(A[p][1].y, 0), rdl(A[p][1].z, 0), rdl(A[p][1].w, 0));
+            const uint4 l0 = make_uint4(rdl(A[p][1].x, 0), rdl(A[p][1].y, 0), rdl(A[p][1].z, 0),
+                                        rdl(A[p][1].w, 0));  // read in uniform flow (see k_encode)
+            if (lane == 63u) B[0] = l0;
             uint32_t Hj[8];  // packet's head words, read out in uniform control flow (SGPRs)
 #pragma unroll
             for (int t = 2; t < 8; ++t) Hj[t] = rdl(L.H[t], js[p]);
@@ -571,15 +573,20 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
     return x < r ? x * (q + 1u) + k : r * (q + 1u) + (x - r) * q + k;
 }
 
+// MAP >= 2 (A/B): each wave takes MAP consecutive sets (a MAP x 92-KB tile for C3), the grid MAP
+// times smaller.
 template <int MODE, int PU, int U, int NT, int MAP = 0>
 __global__ __launch_bounds__(kBlock) void k_encode(EncArgs a, KeySched ks) {
     __shared__ CopyRec recs[kWavesPerBlock][64];
     __shared__ uint32_t cend[kWavesPerBlock][64];
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     const uint32_t blk = MAP == 1 ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    const uint64_t base = ((uint64_t)blk * kWavesPerBlock + w) * 64u;
-    if (base >= a.n) return;  // wave-uniform; no block barriers below
-    encode_set<MODE, PU, U, NT>(a, ks, base + lane, lane, recs[w], cend[w]);
+    constexpr uint32_t S = MAP >= 2 ? MAP : 1;
+    for (uint32_t k = 0; k < S; ++k) {
+        const uint64_t base = (((uint64_t)blk * kWavesPerBlock + w) * S + k) * 64u;
+        if (base >= a.n) return;  // wave-uniform; no block barriers below
+        encode_set<MODE, PU, U, NT>(a, ks, base + lane, lane, recs[w], cend[w]);
+    }
 }
 
 
@@ -940,8 +947,7 @@ __device__ __forceinline__ void copy_wire_pkt_dpp(const EncArgs &a, const KeySch
             for (int q = 0; q < G::NPW; ++q) D[q] = 0;
             put_bytes(D, G::HL, t0, 4);
             put_bytes(D, G::HL + 4, t1, 4);
-            put_bytes(D, G::HL + RSK_HEAD_SIZE - 1, pw[0] & 0xffu, 1);  // frame byte 31 = payload[0]
-            wire_put_prefix<E>(D, pw);
+            wire_put_prefix<E>(D, pw);  // payload bytes from wire offset HB (frame byte 31 = payload[0])
             if (myP) {
 #pragma unroll
                 for (int q = G::HL / 4; q < G::NPW; ++q) {
@@ -958,8 +964,9 @@ __device__ __forceinline__ void copy_wire_pkt_dpp(const EncArgs &a, const KeySch
             uint4 B[2];
             B[0] = make_uint4(wave_shl1(A[p][0].x), wave_shl1(A[p][0].y), wave_shl1(A[p][0].z), wave_shl1(A[p][0].w));
             B[1] = make_uint4(wave_shl1(A[p][1].x), wave_shl1(A[p][1].y), wave_shl1(A[p][1].z), wave_shl1(A[p][1].w));
-            if (lane == 63u)
-                B[0] = make_uint4(rdl(A[p][1].x, 0), rdl(A[p][1].y, 0), rdl(A[p][1].z, 0), rdl(A[p][1].w, 0));
+            const uint4 l0 = make_uint4(rdl(A[p][1].x, 0), rdl(A[p][1].y, 0), rdl(A[p][1].z, 0),
+                                        rdl(A[p][1].w, 0));  // read in uniform flow (see k_encode)
+            if (lane == 63u) B[0] = l0;
             const uint32_t nch = (wlen[p] + 15u) >> 4;
             uint32_t part = 0;
 #pragma unroll
@@ -1165,7 +1172,7 @@ __device__ __forceinline__ bool wire_flat_choice(bool vec, uint32_t wlen) {
 }
 
 template <int E, int MODE, int PU, int U>
-__global__ __launch_bounds__(kBlock) void k_encode_wire(EncArgs a, WireArgs wa, KeySched ks) {
+__device__ __forceinline__ void encode_wire_set(const EncArgs &a, const WireArgs &wa, const KeySched &ks) {
     using G = WireGeom<E>;
     __shared__ uint4 lds[kWavesPerBlock][WireLds<E, MODE>::kBytes / 16];
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
@@ -1241,6 +1248,19 @@ __global__ __launch_bounds__(kBlock) void k_encode_wire(EncArgs a, WireArgs wa, 
         wave_lds_sync();
         copy_wire_bytes<E>(a, L, stage, sum_pre, wst, lane, sm);
     }
+}
+
+template <int E, int MODE, int PU, int U>
+__global__ __launch_bounds__(kBlock) void k_encode_wire(EncArgs a, WireArgs wa, KeySched ks) {
+    encode_wire_set<E, MODE, PU, U>(a, wa, ks);
+}
+
+// The same held to 4 waves per SIMD (<= 128 VGPRs): the deferred-tag build (MODE 5) needs 131 and
+// would otherwise drop to 3, which costs the sets that keep the tag in phase 1 (C4 +9 %).
+template <int E, int MODE, int PU, int U>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_encode_wire_w4(
+    EncArgs a, WireArgs wa, KeySched ks) {
+    encode_wire_set<E, MODE, PU, U>(a, wa, ks);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2044,7 +2064,7 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 //  23/24 = the default with PU=8/16
 // v + 100 * cap (cap 1..4): the same kernel held to `cap` blocks per CU by unused dynamic LDS.
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
-    if (!c || v < 0 || v % 100 > 25 || v / 100 > 4) return RSK_EINVAL;
+    if (!c || v < 0 || v % 100 > 28 || v / 100 > 4) return RSK_EINVAL;
     c->enc_variant = v;
     return RSK_OK;
 }
@@ -2052,9 +2072,10 @@ int rsk__set_encode_variant(rsk_ctx *c, int v) {
 // Internal (A/B and tests): wire-build copy path.  0 = two-launch hybrid whose per-packet half uses the
 // one-load DPP copy, 8 packets per iteration, tag + payload prefix in the copy loop for sets of long
 // frames (default), 1 = per-packet, 2 = flat, 3 = one-launch hybrid, 4 = two-launch hybrid with the
-// two-load copy PU=2, 5 = the same PU=4, 6 / 7 = DPP copy PU=4 / 16, 8 = 0 with the tag in phase 1.
+// two-load copy PU=2, 5 = the same PU=4, 6 / 7 = DPP copy PU=4 / 16, 8 = 0 with the tag in phase 1,
+// 9 = 0 without the 4-waves-per-SIMD bound.
 int rsk__set_wire_variant(rsk_ctx *c, int v) {
-    if (!c || v < 0 || v > 8) return RSK_EINVAL;
+    if (!c || v < 0 || v > 9) return RSK_EINVAL;
     c->wire_variant = v;
     return RSK_OK;
 }
@@ -2136,6 +2157,9 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         case 23: hipLaunchKernelGGL((k_encode<6, 8, 4, -1>), gd, bd, lds, st, a, c->ks); break;
         case 24: hipLaunchKernelGGL((k_encode<6, 16, 4, -1>), gd, bd, lds, st, a, c->ks); break;
         case 25: hipLaunchKernelGGL((k_encode<6, 12, 4, -1, 1>), gd, bd, lds, st, a, c->ks); break;
+        case 26: hipLaunchKernelGGL((k_encode<6, 12, 4, -1, 2>), dim3((grid + 1) / 2), bd, lds, st, a, c->ks); break;
+        case 27: hipLaunchKernelGGL((k_encode<6, 12, 4, -1, 4>), dim3((grid + 3) / 4), bd, lds, st, a, c->ks); break;
+        case 28: hipLaunchKernelGGL((k_encode<6, 12, 4, -1, 8>), dim3((grid + 7) / 8), bd, lds, st, a, c->ks); break;
         case 1: hipLaunchKernelGGL((k_encode<0, 1, 4, 0>), gd, bd, 0, st, a, c->ks); break;
         case 2: hipLaunchKernelGGL((k_encode<1, 4, 2, 0>), gd, bd, 0, st, a, c->ks); break;
         case 3: hipLaunchKernelGGL((k_encode<1, 4, 4, 0>), gd, bd, 0, st, a, c->ks); break;
@@ -2182,6 +2206,7 @@ int rsk_encode_wire_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const
     const unsigned grid = (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
     const hipStream_t st = (hipStream_t)stream;
 #define RSK_WIRE(E, M, PU, U) hipLaunchKernelGGL((k_encode_wire<E, M, PU, U>), dim3(grid), dim3(kBlock), 0, st, a, w, c->ks)
+#define RSK_WIRE4(E, M, PU, U) hipLaunchKernelGGL((k_encode_wire_w4<E, M, PU, U>), dim3(grid), dim3(kBlock), 0, st, a, w, c->ks)
     const int v = c->wire_variant;
     if (wire->with_eth) {
         if (v == 1) RSK_WIRE(14, 0, 2, 4);
@@ -2192,7 +2217,8 @@ int rsk_encode_wire_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const
         else if (v == 6) { RSK_WIRE(14, 3, 104, 2); RSK_WIRE(14, 4, 2, 2); }
         else if (v == 7) { RSK_WIRE(14, 3, 116, 2); RSK_WIRE(14, 4, 2, 2); }
         else if (v == 8) { RSK_WIRE(14, 3, 108, 2); RSK_WIRE(14, 4, 2, 2); }
-        else { RSK_WIRE(14, 5, 108, 2); RSK_WIRE(14, 4, 2, 2); }
+        else if (v == 9) { RSK_WIRE(14, 5, 108, 2); RSK_WIRE(14, 4, 2, 2); }
+        else { RSK_WIRE4(14, 5, 108, 2); RSK_WIRE(14, 4, 2, 2); }
     } else {
         if (v == 1) RSK_WIRE(0, 0, 2, 4);
         else if (v == 2) RSK_WIRE(0, 1, 2, 2);
@@ -2202,9 +2228,11 @@ int rsk_encode_wire_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const
         else if (v == 6) { RSK_WIRE(0, 3, 104, 2); RSK_WIRE(0, 4, 2, 2); }
         else if (v == 7) { RSK_WIRE(0, 3, 116, 2); RSK_WIRE(0, 4, 2, 2); }
         else if (v == 8) { RSK_WIRE(0, 3, 108, 2); RSK_WIRE(0, 4, 2, 2); }
-        else { RSK_WIRE(0, 5, 108, 2); RSK_WIRE(0, 4, 2, 2); }
+        else if (v == 9) { RSK_WIRE(0, 5, 108, 2); RSK_WIRE(0, 4, 2, 2); }
+        else { RSK_WIRE4(0, 5, 108, 2); RSK_WIRE(0, 4, 2, 2); }
     }
 #undef RSK_WIRE
+#undef RSK_WIRE4
     return launch_check("k_encode_wire");
 }
 

@@ -105,7 +105,7 @@ def _rand_fields(rng, n):
             rng.integers(0, 2**63, n, dtype=np.uint64) * 2 + rng.integers(0, 2, n, dtype=np.uint64))
 
 
-ENC_VARIANTS = list(range(26))
+ENC_VARIANTS = list(range(29))
 
 
 @pytest.fixture(params=ENC_VARIANTS, ids=lambda v: f"encv{v}")

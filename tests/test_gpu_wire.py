@@ -20,7 +20,7 @@ KEY = b"hello135"
 @pytest.mark.parametrize("layout", ["aligned", "odd_payload", "odd_wire"])
 @pytest.mark.parametrize("pad16", [False, True])
 @pytest.mark.parametrize("mix", ["mixed", "short", "bimodal", "long"])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8])  # see rsk__set_wire_variant
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])  # see rsk__set_wire_variant
 def test_wire_batch(codec, gpu, oracle, eth, layout, pad16, mix, variant):
     import torch
 
