@@ -20,6 +20,7 @@
  *   rsk_parse_decode_slots_batch <- the same on host-staged header slots (payloads stay in the capture buffer)
  *                            + RawTcp::cap2uv size check (RawTcp.cpp:239-244) fused with RConn::OnRecv
  *   rsk_tcpinfo_encode_batch <- char* TcpInfo::Encode(char*, int) (21-B hand-off record)      bean/TcpInfo.cpp:20-32, bean/ConnInfo.cpp:12-20
+ *   rsk_syncinput_decode_batch <- RawTcp::syncInput -> TcpInfo::Decode -> RConn::OnRecv     conn/RawTcp.cpp:262-276, bean/TcpInfo.cpp:35-47
  *   rsk_encode_wire_batch <- RConn::Output + RawTcp::SendRawTcp -> libnet_build_tcp/ipv4     conn/RawTcp.cpp:280-341
  *   rsk_key_for_tcp/udp   <- KeyGenerator::KeyForTcp / KeyForUdp                              src/util/KeyGenerator.cpp:16-36
  *   rsk_capture_filter_batch <- the pcap filter RCap installs: BuildFilterStr("tcp", srcIp, dstIp, srcPorts,
@@ -287,6 +288,18 @@ int rsk_stage_capture_slots(uint32_t n, const uint8_t *arena, const uint64_t *ca
 int rsk_tcpinfo_encode_batch(rsk_ctx *ctx, uint32_t n, const uint32_t *src, const uint32_t *dst,
                              const uint16_t *sp, const uint16_t *dp, const uint32_t *seq,
                              const uint32_t *ack, const uint8_t *flag, uint8_t *rec, void *stream);
+/* The consumer side (RawTcp::syncInput, conn/RawTcp.cpp:262-276 -> TcpInfo::Decode,
+ * bean/TcpInfo.cpp:35-47 -> RConn::OnRecv): record i = nread[i] bytes at rec_arena + rec_off[i], a
+ * 21-B TcpInfo record followed by the frame (what cap2uv sends, RawTcp.cpp:239-260).  A record of
+ * nread >= 21 bytes gets parse_status RSK_PARSE_DELIVER, its TcpInfo fields, cap_pay_off 21,
+ * cap_pay_len nread - 21, and dec = rsk_decode_batch on the frame with is_tcp_close = flag &
+ * (FIN|RST).  nread < 21: RSK_PARSE_DROP, zero TcpInfo, dec->status RSK_RECV_DROP (syncInput
+ * returns before Input for nread <= 0 and for a failed Decode; for 12 <= nread < 21 the reference's
+ * Decode does not fail but reads its receive buffer past nread — TcpInfo.cpp:40 compares the
+ * bytes consumed, not those left — so this is the one deliberate deviation, on malformed input). */
+int rsk_syncinput_decode_batch(rsk_ctx *ctx, uint32_t n, const uint8_t *rec_arena, const uint64_t *rec_off,
+                               const int32_t *nread, const rsk_tcpinfo_out *tcp, const rsk_decode_out *dec,
+                               void *stream);
 
 /* ---- fake-TCP connection state on either side of the codec --------------------------------------- */
 /* Send: FakeTcp::Output (conn/FakeTcp.cpp:43-49) advances its connection's seq by

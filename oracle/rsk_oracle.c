@@ -311,6 +311,24 @@ int orc_tcpinfo_decode(const uint8_t *rec, int len, orc_tcpinfo *t) {
     return 21;
 }
 
+/* RawTcp::syncInput (conn/RawTcp.cpp:262-276) + RConn::OnRecv: the loop thread's side of cap2uv's
+ * hand-off.  A record is the 21-B TcpInfo followed by the frame.  nread <= 0 never reaches Decode;
+ * a failed Decode returns -1 before Input (both: parse_status DROP, dec DROP); otherwise
+ * Input(nread - 21) reaches RConn::OnRecv with is_tcp_close = HasCloseFlag() (TcpInfo.h:31-33). */
+int orc_syncinput(const uint8_t *key, size_t key_len, const uint8_t *rec, int nread, orc_tcpinfo *t,
+                  orc_dec *d) {
+    memset(t, 0, sizeof *t);
+    memset(d, 0, sizeof *d);
+    d->status = RSK_RECV_DROP;
+    t->parse_status = RSK_PARSE_DROP;
+    if (nread <= 0 || orc_tcpinfo_decode(rec, nread, t) < 0) return RSK_PARSE_DROP;
+    t->parse_status = RSK_PARSE_DELIVER;
+    t->cap_pay_off = 21;
+    t->cap_pay_len = (uint16_t)(nread - 21);
+    orc_rconn_onrecv(key, key_len, rec + 21, nread - 21, (t->flag & (RSK_TH_FIN | RSK_TH_RST)) != 0, d);
+    return RSK_PARSE_DELIVER;
+}
+
 /* ------------------------------------------------------------------------------------------------
  * Send-side wire build: RawTcp::SendRawTcp (conn/RawTcp.cpp:280-341) = libnet_build_tcp(sp, dp,
  * seq, ack, flag, win 65535, sum 0 = auto, urg 0, len = 20 + frame) + libnet_build_ipv4(

@@ -76,6 +76,10 @@ int orc_rawinput(const uint8_t *pkt, uint32_t wire_len, uint32_t cap_len, int da
 /* TcpInfo::Encode / Decode (bean/TcpInfo.cpp:20-45, bean/ConnInfo.cpp:12-32): 21-byte record. */
 int orc_tcpinfo_encode(const orc_tcpinfo *t, uint8_t rec[21]);
 int orc_tcpinfo_decode(const uint8_t *rec, int len, orc_tcpinfo *t);
+/* RawTcp::syncInput (conn/RawTcp.cpp:262-276) -> RConn::OnRecv on one hand-off record (21-B TcpInfo
+ * + frame, nread bytes).  Returns the parse status (DELIVER when Decode succeeded). */
+int orc_syncinput(const uint8_t *key, size_t key_len, const uint8_t *rec, int nread, orc_tcpinfo *t,
+                  orc_dec *d);
 
 /* RawTcp::SendRawTcp (conn/RawTcp.cpp:280-341) through libnet 1.1.6: the wire packet for one frame.
  * [eth 14 if eth != NULL] | IPv4 20 (v4, IHL 5, tos 0, tot_len, id, DF, ttl 64, proto 6, checksum,

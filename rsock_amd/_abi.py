@@ -149,6 +149,8 @@ SIGNATURES = [
     ("rsk_stage_capture_slots", ctypes.c_int, [ctypes.c_uint32, _vp, _vp, _vp, ctypes.c_uint32, _vp, ctypes.c_int]),
     ("rsk_tcpinfo_encode_batch", ctypes.c_int,
      [_vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("rsk_syncinput_decode_batch", ctypes.c_int,
+     [_vp, ctypes.c_uint32, _vp, _vp, _vp, ctypes.POINTER(TcpInfoOut), ctypes.POINTER(DecodeOut), _vp]),
     ("rsk_capture_filter_batch", ctypes.c_int,
      [_vp, ctypes.c_uint32, _vp, _vp, _vp, ctypes.c_int, ctypes.POINTER(CaptureFilter), _vp, _vp, _vp, _vp]),
     ("rsk_filter_str", ctypes.c_int, [ctypes.POINTER(CaptureFilter), ctypes.c_char_p, ctypes.c_size_t]),

@@ -317,6 +317,17 @@ class Codec:
                                             ctypes.byref(dout), _stream(stream)),
                "rsk_parse_decode_batch")
 
+    def syncinput_batch(self, rec, rec_off, nread, tcp: TcpInfoBuffers, out: DecodeBuffers, compact: bool = True,
+                        stream=None) -> None:
+        """RawTcp::syncInput -> TcpInfo::Decode -> RConn::OnRecv for n hand-off records (21-B TcpInfo
+        + frame, nread[i] bytes at rec + rec_off[i])."""
+        n = nread.numel()
+        tout = tcp.abi()
+        dout = out.abi(compact)
+        _check(lib().rsk_syncinput_decode_batch(self._ctx, n, _ptr(rec), _ptr(rec_off), _ptr(nread),
+                                                ctypes.byref(tout), ctypes.byref(dout), _stream(stream)),
+               "rsk_syncinput_decode_batch")
+
     def rawinput_slots_batch(self, slots, slot: int, wire_len, cap_len, datalink: int, flags: int,
                              tcp: TcpInfoBuffers, out: DecodeBuffers, compact: bool = True, stream=None) -> None:
         """rawinput_batch on host-staged header slots (rsk_parse_decode_slots_batch): packet i's first

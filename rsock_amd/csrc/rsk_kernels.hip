@@ -1563,6 +1563,56 @@ __global__ __launch_bounds__(kBlock) void k_parse_decode(ParseArgs a, DecOut d, 
     if (d.masks) compact_epilogue(d, valid);
 }
 
+// ---- RawTcp::syncInput (conn/RawTcp.cpp:262-276) + RConn::OnRecv: the loop thread's side of
+// cap2uv's hand-off.  Record i (nread[i] bytes at rec + rec_off[i]) = TcpInfo::Encode's 21 B
+// (src LE32 | dst LE32 | sp LE16 | dp LE16 | seq LE32 | ack LE32 | flag; TcpInfo.cpp:20-32,
+// ConnInfo.cpp:12-20) then the frame.  A record of fewer than 21 bytes is not decoded (see
+// rsk_syncinput_decode_batch); otherwise the frame (nread - 21 bytes) goes through decode_frame
+// with is_tcp_close = HasCloseFlag() (TcpInfo.h:31-33).  One lane per record.
+struct SyncArgs {
+    const uint8_t *rec;
+    const uint64_t *rec_off;
+    const int32_t *nread;
+    uint32_t *src, *dst;
+    uint16_t *sp, *dp;
+    uint32_t *seq, *ack;
+    uint8_t *flag;
+    int8_t *pst;
+    uint16_t *cpo, *cpl;
+    uint32_t n;
+};
+
+__global__ __launch_bounds__(kBlock) void k_syncinput_decode(SyncArgs a, DecOut d, KeySched ks) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    bool valid = false;
+    if (i < a.n) {
+        const uint8_t *r = a.rec + a.rec_off[i];
+        const int nr = a.nread[i];
+        uint32_t w[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+        Dec o = {0, 0, 0, 0, 0, 0, 0, 0, RSK_RECV_DROP};
+        const bool ok = nr >= RSK_TCPINFO_WIRE_SIZE;
+        if (ok) {
+            rsk::load_window<6>(r, r + (RSK_TCPINFO_WIRE_SIZE - 1), w);
+            w[5] &= 0xffu;
+            o = decode_frame(r + RSK_TCPINFO_WIRE_SIZE, nr - RSK_TCPINFO_WIRE_SIZE,
+                             (w[5] & (RSK_TH_FIN | RSK_TH_RST)) != 0u, ks);
+        }
+        a.src[i] = w[0];
+        a.dst[i] = w[1];
+        a.sp[i] = (uint16_t)(w[2] & 0xffffu);
+        a.dp[i] = (uint16_t)(w[2] >> 16);
+        a.seq[i] = w[3];
+        a.ack[i] = w[4];
+        a.flag[i] = (uint8_t)w[5];
+        a.pst[i] = (int8_t)(ok ? RSK_PARSE_DELIVER : RSK_PARSE_DROP);
+        a.cpo[i] = (uint16_t)(ok ? RSK_TCPINFO_WIRE_SIZE : 0);
+        a.cpl[i] = (uint16_t)(ok ? nr - RSK_TCPINFO_WIRE_SIZE : 0);
+        store_dec(d, i, o);
+        valid = o.st == RSK_RECV_VALID;
+    }
+    if (d.masks) compact_epilogue(d, valid);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Order-stable compaction of VALID indices
 // ---------------------------------------------------------------------------------------------
@@ -2370,6 +2420,37 @@ int rsk_parse_decode_slots_batch(rsk_ctx *c, uint32_t n, const uint8_t *slots, u
                                  const rsk_tcpinfo_out *tcp, const rsk_decode_out *dec, void *stream) {
     if (slot < RSK_CAP_SLOT_MIN || (slot & 15u) || (reinterpret_cast<uintptr_t>(slots) & 15u)) return RSK_EINVAL;
     return parse_decode(c, n, slots, nullptr, slot, wire_len, cap_len, datalink, flags, tcp, dec, stream);
+}
+
+int rsk_syncinput_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *rec_arena, const uint64_t *rec_off,
+                               const int32_t *nread, const rsk_tcpinfo_out *tcp, const rsk_decode_out *dec,
+                               void *stream) {
+    if (!c || !tcp || !dec) return RSK_EINVAL;
+    if (n == 0) return empty_batch(c, dec->n_valid, stream);
+    if (!rec_arena || !rec_off || !nread || !dec_out_ok(dec)) return RSK_EINVAL;
+    if (!tcp->src || !tcp->dst || !tcp->sp || !tcp->dp || !tcp->seq || !tcp->ack || !tcp->flag ||
+        !tcp->parse_status || !tcp->cap_pay_off || !tcp->cap_pay_len)
+        return RSK_EINVAL;
+    DeviceGuard g(c->device);
+    if (!g.ok) return RSK_EDEVICE;
+    const bool compact = dec->valid_idx || dec->n_valid;
+    uint64_t *masks = nullptr;
+    uint32_t *counts = nullptr, *offsets = nullptr;
+    if (compact) {
+        int r = ensure_ws(c, n);
+        if (r) return r;
+        ws_split(c, n, masks, counts, offsets);
+    }
+    SyncArgs a;
+    a.rec = rec_arena; a.rec_off = rec_off; a.nread = nread;
+    a.src = tcp->src; a.dst = tcp->dst; a.sp = tcp->sp; a.dp = tcp->dp; a.seq = tcp->seq; a.ack = tcp->ack;
+    a.flag = tcp->flag; a.pst = tcp->parse_status; a.cpo = tcp->cap_pay_off; a.cpl = tcp->cap_pay_len;
+    a.n = n;
+    const DecOut d = make_dec_out(dec, masks, counts);
+    hipLaunchKernelGGL(k_syncinput_decode, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, a, d, c->ks);
+    int r = launch_check("k_syncinput_decode");
+    if (r || !compact) return r;
+    return run_compaction(c, n, masks, counts, offsets, dec, (hipStream_t)stream);
 }
 
 int rsk_filter_parse_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *cap_arena, const uint64_t *cap_off,

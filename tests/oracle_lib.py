@@ -55,6 +55,8 @@ class Oracle:
                                    ctypes.c_int, ctypes.POINTER(OrcTcpInfo)]
         L.orc_tcpinfo_encode.argtypes = [ctypes.POINTER(OrcTcpInfo), ctypes.c_char_p]
         L.orc_tcpinfo_decode.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(OrcTcpInfo)]
+        L.orc_syncinput.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_int,
+                                    ctypes.POINTER(OrcTcpInfo), ctypes.POINTER(OrcDec)]
         L.orc_build_wire.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint16,
                                      ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint8,
                                      ctypes.c_uint16, ctypes.c_char_p, ctypes.c_char_p]
@@ -123,6 +125,12 @@ class Oracle:
         t = OrcTcpInfo()
         self.L.orc_rawinput(bytes(pkt), wire_len, cap_len, datalink, flags, ctypes.byref(t))
         return t
+
+    def syncinput(self, key: bytes, rec: bytes, nread: int) -> tuple[OrcTcpInfo, OrcDec]:
+        """RawTcp::syncInput -> RConn::OnRecv on one hand-off record (rec holds >= 21 bytes)."""
+        t, d = OrcTcpInfo(), OrcDec()
+        self.L.orc_syncinput(key, len(key), bytes(rec), nread, ctypes.byref(t), ctypes.byref(d))
+        return t, d
 
     def tcpinfo_encode(self, t: OrcTcpInfo) -> bytes:
         out = ctypes.create_string_buffer(21)

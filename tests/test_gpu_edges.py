@@ -55,6 +55,10 @@ def test_empty_batches_are_noops(codec, gpu):
         codec.rawinput_slots_batch(u8, 96, i32, i32, dl, 3, tcp, dec)
         torch.cuda.synchronize()
         assert int(dec.n_valid.item()) == 0
+    dec.n_valid.fill_(7)
+    codec.syncinput_batch(u8, i64, i32, tcp, dec)
+    torch.cuda.synchronize()
+    assert int(dec.n_valid.item()) == 0
     nm = _poisoned_count(gpu)
     codec.capture_filter_batch(u8, i64, i32, 1, rc.make_filter(dst_singles=[10001]), u8, i32, nm)
     torch.cuda.synchronize()
@@ -108,6 +112,11 @@ def test_missing_arrays_and_bad_arguments_rejected(codec, gpu):
     ein = _abi.EncodeIn(p, p, p, p, p, p, p + 3, (ctypes.c_uint8 * 8)())
     eout = _abi.EncodeOut(p, p, p, 0)
     assert lib.rsk_encode_batch(ctx, n, ctypes.byref(ein), ctypes.byref(eout), None) == _abi.EINVAL
+    # syncinput: missing nread, missing TcpInfo array
+    assert lib.rsk_syncinput_decode_batch(ctx, n, p, p, None, ctypes.byref(tcp.abi()), ctypes.byref(dout.abi()),
+                                          None) == _abi.EINVAL
+    assert lib.rsk_syncinput_decode_batch(ctx, n, p, p, p, ctypes.byref(t), ctypes.byref(dout.abi()),
+                                          None) == _abi.EINVAL
     # tcpinfo: a missing field array
     assert lib.rsk_tcpinfo_encode_batch(ctx, n, p, p, p, p, p, None, p, p, None) == _abi.EINVAL
     # null context everywhere

@@ -129,6 +129,19 @@ def main():
     assert bool((pdec.status == 1).all()) and int(pdec.n_valid.item()) == n
     ops.pop("decode")  # decode now sees the corrupted frames; time it on them too
     ops["decode"] = lambda: cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, w.dec, stream=s)
+    # syncInput hand-off records: 21-B TcpInfo (from the parse above) + the frame, one per slot
+    fp = d.frame_pitch
+    rp = (21 + fp + 15) // 16 * 16
+    hand = torch.zeros(n * rp, dtype=torch.uint8, device=dev)
+    h2 = hand.view(n, rp)
+    h2[:, 21:21 + fp] = w.frame[: n * fp].view(n, fp)
+    hrec = torch.empty(n * 21, dtype=torch.uint8, device=dev)
+    cx.tcpinfo_encode_batch(tcp.src, tcp.dst, tcp.sp, tcp.dp, tcp.seq, tcp.ack, tcp.flag, hrec, stream=s)
+    h2[:, :21] = hrec.view(n, 21)
+    hoff = torch.arange(n, device=dev, dtype=torch.int64) * rp
+    hlen = w.frame_len.to(torch.int32) + 21
+    tcp3, sdec = rc.TcpInfoBuffers.alloc(n, dev), rc.DecodeBuffers.alloc(n, dev)
+    ops["syncinput_decode"] = lambda: cx.syncinput_batch(hand, hoff, hlen, tcp3, sdec, stream=s)
     nseg = [int(dmx.n_seg.item()), int(dmx64.n_seg.item())]
     times = {k: [] for k in ops}
     for _ in range(args.rounds):
@@ -158,7 +171,12 @@ def main():
         "encode_hdr": 1 + 2 + 1 + 4 + 8 + 32 + 4,
         "tcp_send_seq": 4 + 4 + 4 + 2,  # conn, status in; seq, ip_id out
         "tcp_recv_ack": 4 + 1 + 4,      # conn, delivered, seq in
+        # record bytes [0, 53) + rec_off + nread in; TcpInfo (26) + decode fields (27) + valid_idx out
+        "syncinput_decode": 53 + 8 + 4 + 26 + 27 + 4,
     }
+    cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, w.dec, stream=s)
+    torch.cuda.synchronize()
+    assert torch.equal(sdec.status, w.dec.status) and torch.equal(sdec.n_valid, w.dec.n_valid)
     out = {}
     for k, t in times.items():
         m = float(np.median(t))
