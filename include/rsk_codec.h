@@ -310,7 +310,8 @@ int rsk_syncinput_decode_batch(rsk_ctx *ctx, uint32_t n, const uint8_t *rec_aren
  *       conn[i] < n_conn: seq[i] = conn_seq[conn[i]], then conn_seq[conn[i]] += status[i] (mod 2^32)
  *   otherwise, or conn[i] >= n_conn: seq[i] = 0 (ip_id[i] = 0 when not framed)
  * conn_seq [n_conn] and ip_id_next [1] are device state updated in place; seq / ip_id are what
- * rsk_encode_wire_batch takes.  n <= 2^30; uses the demux workspace plus ~35 B per packet. */
+ * rsk_encode_wire_batch takes.  n <= 2^30.  Workspace: n_conn < 2048 takes a per-tile connection table
+ * (<= 4 B per packet); wider n_conn the demux group-by (its workspace plus ~35 B per packet). */
 int rsk_tcp_send_seq_batch(rsk_ctx *ctx, uint32_t n, const uint32_t *conn, const int32_t *status,
                            uint32_t n_conn, uint32_t *conn_seq, uint16_t *ip_id_next, uint32_t *seq,
                            uint16_t *ip_id, void *stream);

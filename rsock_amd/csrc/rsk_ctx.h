@@ -26,6 +26,7 @@ struct rsk_ctx {
     // connection-state workspace (rsk_tcp_send_seq_batch, rsk_demux.hip)
     void *sq_ws = nullptr;
     size_t sq_ws_bytes = 0;
+    bool sq_force_groupby = false;  // see rsk__set_send_seq_groupby
     // demux workspace (rsk_demux.hip)
     void *dm_ws = nullptr;
     size_t dm_ws_bytes = 0;

@@ -737,6 +737,185 @@ __global__ __launch_bounds__(kBlock) void k_ack_lds(const uint32_t *conn, const 
         if (tab[c]) atomicMax(conn_ack + c, tab[c]);  // max with 0 changes nothing
 }
 
+// ---- send seq / IP id, table path (n_conn + 1 <= kSqCols) --------------------------------------
+// Without the group-by: the batch is cut into wave tiles of W packets (W >= n_conn + 1, so the table
+// below is at most 4 B per packet).  Column c < n_conn of a tile's row is connection c's framed
+// bytes in the tile, column n_conn its framed-packet count (the IP id column).
+//   k_sqt_sum    per wave tile, a wave-private LDS row (ds_add), written to tab[tile][col]
+//   k_sqt_scan   per column, exclusive scan down the tiles, rebased on conn_seq[c] / *ip_id_next,
+//                in place; the column's total advances the state
+//   k_sqt_apply  per wave tile in batch order: the row back into LDS, then per 64-packet round the
+//                in-wave per-connection exclusive prefix by a readlane walk of the 64 lanes; the last
+//                lane of each connection carries the row forward
+// Every packet is read twice (conn + status, 8 B) and written once (seq + ip_id, 6 B).
+constexpr uint32_t kSqCols = 2048;
+constexpr uint32_t kSqScanThreads = 1024;
+
+__device__ __forceinline__ void sqt_load4(const uint32_t *conn, const int32_t *status, uint64_t r, uint64_t end,
+                                          uint32_t lane, int32_t (&st)[4], uint32_t (&cn)[4]) {
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint64_t i = r + 64u * k + lane;
+        const bool in = i < end;
+        st[k] = in ? status[i] : 0;
+        cn[k] = in ? conn[i] : 0u;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_sqt_sum(const uint32_t *conn, const int32_t *status, uint32_t n,
+                                                    uint32_t n_conn, uint32_t W, uint32_t nwt, uint32_t *tab) {
+    extern __shared__ uint32_t sq_lds[];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, ncol = n_conn + 1u;
+    const uint32_t wt = blockIdx.x * kWaves + wv;
+    uint32_t *t = sq_lds + wv * ncol;
+    for (uint32_t c = lane; c < n_conn; c += 64u) t[c] = 0u;
+    __syncthreads();
+    uint32_t nfr = 0;
+    if (wt < nwt) {
+        const uint64_t base = (uint64_t)wt * W, end = base + W < n ? base + W : n;
+        for (uint64_t r = base; r < end; r += 256u) {
+            int32_t st[4];
+            uint32_t cn[4];
+            sqt_load4(conn, status, r, end, lane, st, cn);
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) {
+                const bool fr = st[k] > 0;
+                nfr += (uint32_t)__popcll(__ballot(fr));
+                if (fr && cn[k] < n_conn) atomicAdd(t + cn[k], (uint32_t)st[k]);
+            }
+        }
+    }
+    __syncthreads();
+    if (wt < nwt) {
+        uint32_t *row = tab + (uint64_t)wt * ncol;
+        for (uint32_t c = lane; c < n_conn; c += 64u) row[c] = t[c];
+        if (lane == 0) row[n_conn] = nfr;
+    }
+}
+
+// cb columns per block (a power of two), 1024 / cb row groups; group g scans rows [g R, (g + 1) R)
+__global__ __launch_bounds__(kSqScanThreads) void k_sqt_scan(uint32_t *tab, uint32_t nwt, uint32_t n_conn, uint32_t cb,
+                                                             uint32_t *conn_seq, uint16_t *ip_next) {
+    __shared__ uint32_t part[kSqScanThreads];
+    const uint32_t ncol = n_conn + 1u, cl = threadIdx.x % cb, g = threadIdx.x / cb, ng = kSqScanThreads / cb;
+    const uint32_t c = blockIdx.x * cb + cl;
+    const bool ok = c < ncol;
+    const uint32_t R = (nwt + ng - 1u) / ng, r0 = g * R < nwt ? g * R : nwt, r1 = r0 + R < nwt ? r0 + R : nwt;
+    const uint32_t state = ok ? (c < n_conn ? conn_seq[c] : (uint32_t)*ip_next) : 0u;  // read before any write
+    uint32_t s = 0;
+    if (ok) {
+        uint32_t r = r0;
+        for (; r + 8u <= r1; r += 8u) {
+            uint32_t v[8];
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k) v[k] = tab[(uint64_t)(r + k) * ncol + c];
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k) s += v[k];
+        }
+        for (; r < r1; ++r) s += tab[(uint64_t)r * ncol + c];
+    }
+    // inclusive scan of the group sums down each column (Hillis-Steele over the ng groups)
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (uint32_t off = 1; off < ng; off <<= 1) {
+        const uint32_t v = part[threadIdx.x] + (g >= off ? part[threadIdx.x - off * cb] : 0u);
+        __syncthreads();
+        part[threadIdx.x] = v;
+        __syncthreads();
+    }
+    if (!ok) return;
+    uint32_t run = state + part[threadIdx.x] - s;  // mod 2^32 (TcpInfo::seq) / mod 2^16 once stored (mIpId)
+    uint32_t r = r0;
+    for (; r + 8u <= r1; r += 8u) {
+        uint32_t v[8];
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) v[k] = tab[(uint64_t)(r + k) * ncol + c];
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) {
+            tab[(uint64_t)(r + k) * ncol + c] = run;
+            run += v[k];
+        }
+    }
+    for (; r < r1; ++r) {
+        const uint32_t v = tab[(uint64_t)r * ncol + c];
+        tab[(uint64_t)r * ncol + c] = run;
+        run += v;
+    }
+    if (g == ng - 1u) {  // the last group ends on the column's total
+        if (c < n_conn) conn_seq[c] = run;
+        else *ip_next = (uint16_t)run;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_sqt_apply(const uint32_t *conn, const int32_t *status, uint32_t n,
+                                                      uint32_t n_conn, uint32_t W, uint32_t nwt, const uint32_t *tab,
+                                                      uint32_t *seq, uint16_t *ip_id) {
+    extern __shared__ uint32_t sq_lds[];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, ncol = n_conn + 1u;
+    const uint32_t wt = blockIdx.x * kWaves + wv;
+    uint32_t *t = sq_lds + wv * ncol;
+    uint32_t ip = 0;
+    if (wt < nwt) {
+        const uint32_t *row = tab + (uint64_t)wt * ncol;
+        for (uint32_t c = lane; c < n_conn; c += 64u) t[c] = row[c];
+        ip = row[n_conn];
+    }
+    __syncthreads();
+    if (wt >= nwt) return;
+    const uint64_t lt = lanemask_lt(lane);
+    const uint64_t base = (uint64_t)wt * W, end = base + W < n ? base + W : n;
+    for (uint64_t r = base; r < end; r += 256u) {
+        int32_t st[4];
+        uint32_t cn[4];
+        sqt_load4(conn, status, r, end, lane, st, cn);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint64_t i = r + 64u * k + lane;
+            const bool fr = st[k] > 0;
+            const uint32_t key = fr && cn[k] < n_conn ? cn[k] : kNone;
+            const uint32_t len = fr ? (uint32_t)st[k] : 0u;
+            const uint64_t m = __ballot(fr);
+            const uint32_t my_ip = ip + (uint32_t)__popcll(m & lt);
+            ip += (uint32_t)__popcll(m);
+            // FakeTcp::Output order inside the round: earlier lanes of the same connection go first.
+            // Lane d's peers are one compare into an SGPR mask: the peers above d add lane d's len (the
+            // mask drives the select directly, no per-lane index compare) and the peers below d have a
+            // later lane of their connection (scalar OR).  6 VALU per d; a scalar loop over the
+            // distinct connections of the round instead was slower (branches), DESIGN.md §4.8
+            uint32_t ex = 0;
+            uint64_t laterm = 0;  // lanes with a later lane of their connection (scalar)
+#pragma unroll
+            for (int d = 0; d < 64; ++d) {
+                const uint32_t sk = (uint32_t)__builtin_amdgcn_readlane((int)key, d);
+                const uint32_t sl = (uint32_t)__builtin_amdgcn_readlane((int)len, d);
+                const uint64_t eq = __ballot(key == sk);
+                const uint64_t above = d == 63 ? 0ull : eq & (~0ull << (d + 1));
+                ex += __builtin_amdgcn_inverse_ballot_w64(above) ? sl : 0u;
+                laterm |= eq & ((1ull << d) - 1ull);
+                asm volatile("" : "+v"(ex), "+s"(laterm));  // no sinking: consume each mask in its own step
+            }
+            const bool later = __builtin_amdgcn_inverse_ballot_w64(laterm);
+            uint32_t sv = 0;
+            if (key != kNone) {
+                const uint32_t pre = t[key];
+                sv = pre + ex;
+                if (!later) t[key] = sv + len;  // one lane per connection carries the row
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (i < end) {
+                seq[i] = sv;
+                ip_id[i] = fr ? (uint16_t)my_ip : (uint16_t)0;
+            }
+        }
+    }
+}
+
+uint32_t sqt_wave_tile(uint32_t n_conn) {
+    uint32_t w = 512;
+    while (w < n_conn + 1u) w <<= 1;
+    return w;
+}
+
 struct SqWs {
     int8_t *part;
     uint8_t *cmd0;
@@ -784,7 +963,9 @@ extern "C" int rsk_tcp_send_seq_batch(rsk_ctx *c, uint32_t n, const uint32_t *co
     rsk::DeviceGuard g(c->device);
     if (!g.ok) return RSK_EDEVICE;
     hipStream_t s = (hipStream_t)stream;
-    const size_t need = sq_layout(n, n_conn, nullptr, nullptr);
+    const bool table = n_conn + 1ull <= kSqCols && !c->sq_force_groupby;
+    const uint32_t W = sqt_wave_tile(n_conn), nwt = (uint32_t)((n + (uint64_t)W - 1) / W);
+    const size_t need = table ? 4ull * nwt * (n_conn + 1ull) : sq_layout(n, n_conn, nullptr, nullptr);
     if (!c->sq_ws || c->sq_ws_bytes < need) {
         if (c->sq_ws) {
             hipError_t e = hipDeviceSynchronize();
@@ -797,10 +978,22 @@ extern "C" int rsk_tcp_send_seq_batch(rsk_ctx *c, uint32_t n, const uint32_t *co
         if (e != hipSuccess) { rsk::set_error("hipMalloc(seq workspace)", e); return RSK_ENOMEM; }
         c->sq_ws_bytes = need;
     }
+    int r;
+    if (table) {
+        uint32_t *tab = static_cast<uint32_t *>(c->sq_ws);
+        const unsigned nbt = (nwt + kWaves - 1) / kWaves;
+        const size_t lds = 4ull * kWaves * (n_conn + 1ull);
+        const uint32_t cb = n_conn + 1u <= 128u ? 1u : n_conn + 1u <= 512u ? 16u : 64u;  // more row groups when narrow
+        hipLaunchKernelGGL(k_sqt_sum, dim3(nbt), dim3(kBlock), lds, s, conn, status, n, n_conn, W, nwt, tab);
+        hipLaunchKernelGGL(k_sqt_scan, dim3((n_conn + cb) / cb), dim3(kSqScanThreads), 0, s, tab, nwt, n_conn, cb,
+                           conn_seq, ip_id_next);
+        hipLaunchKernelGGL(k_sqt_apply, dim3(nbt), dim3(kBlock), lds, s, conn, status, n, n_conn, W, nwt, tab, seq,
+                           ip_id);
+        return rsk::launch_check("k_sqt_apply");
+    }
     SqWs w;
     sq_layout(n, n_conn, static_cast<uint8_t *>(c->sq_ws), &w);
     const unsigned nb = (n + kBlock - 1) / kBlock, nb1 = (n + 1 + kBlock - 1) / kBlock;
-    int r;
     hipError_t e = hipMemsetAsync(seq, 0, 4ull * n, s);
     if (e != hipSuccess) { rsk::set_error("hipMemsetAsync(seq)", e); return RSK_EDEVICE; }
     hipLaunchKernelGGL(k_sq_flags, dim3(nb), dim3(kBlock), 0, s, conn, status, n, n_conn, w.part, w.cmd0, w.framed);
@@ -825,6 +1018,13 @@ extern "C" int rsk_tcp_send_seq_batch(rsk_ctx *c, uint32_t n, const uint32_t *co
                        w.base);
     hipLaunchKernelGGL(k_sq_seq, dim3(nb), dim3(kBlock), 0, s, w.perm, w.nvalid, conn, w.base, w.pre, seq);
     return rsk::launch_check("k_sq_seq");
+}
+
+// internal A/B + test knob (not in the public header): 1 sends every n_conn through the group-by path
+extern "C" int rsk__set_send_seq_groupby(rsk_ctx *c, int v) {
+    if (!c || v < 0 || v > 1) return RSK_EINVAL;
+    c->sq_force_groupby = v != 0;
+    return RSK_OK;
 }
 
 extern "C" int rsk_tcp_recv_ack_batch(rsk_ctx *c, uint32_t n, const uint32_t *conn, const uint8_t *delivered,

@@ -19,13 +19,20 @@ def _dev(a, gpu, dt):
     return torch.from_numpy(np.ascontiguousarray(a).view(dt)).to(gpu)
 
 
-@pytest.mark.parametrize("n,n_conn", [(1, 1), (777, 1), (5000, 7), (70_000, 300), (300_000, 70_000)])
-def test_send_seq_matches_oracle(codec, gpu, oracle, n, n_conn):
+# n_conn + 1 <= 2048 takes the per-tile table path (k_sqt_*), larger ones the demux group-by; groupby=1
+# forces the group-by for every case so both paths stay pinned to the oracle
+@pytest.mark.parametrize("groupby", [0, 1])
+@pytest.mark.parametrize("n,n_conn", [(1, 1), (777, 1), (5000, 7), (70_000, 300), (300_000, 70_000), (1, 0),
+                                      (100_000, 0), (513, 64), (1_000_003, 64), (200_000, 511), (200_000, 512),
+                                      (250_001, 2047), (250_001, 2048), (70_000, 1)])
+def test_send_seq_matches_oracle(codec, gpu, oracle, n, n_conn, groupby):
     import torch
 
+    codec.set_send_seq_groupby(groupby)
     rng = np.random.default_rng(n + n_conn)
     conn_seq0 = rng.integers(0, 2**32, n_conn, dtype=np.uint64).astype(np.uint32)
-    conn_seq0[0] = 0xFFFFF000
+    if n_conn:
+        conn_seq0[0] = 0xFFFFF000
     d_cs = _dev(conn_seq0, gpu, np.int32)
     ipn = np.array([65000], np.uint16)
     d_ipn = _dev(ipn, gpu, np.int16)
@@ -42,6 +49,7 @@ def test_send_seq_matches_oracle(codec, gpu, oracle, n, n_conn):
         assert np.array_equal(ipid.cpu().numpy().view(np.uint16), ei), batch
         assert np.array_equal(d_cs.cpu().numpy().view(np.uint32), cs_host), batch
         assert int(d_ipn.cpu().numpy().view(np.uint16)[0]) == ip_host, batch
+    codec.set_send_seq_groupby(0)
 
 
 def test_recv_ack_matches_oracle(codec, gpu, oracle):

@@ -87,6 +87,12 @@ def main():
     sq_seq, sq_ip = torch.empty(n, dtype=torch.int32, device=dev), torch.empty(n, dtype=torch.int16, device=dev)
     deliv = torch.ones(n, dtype=torch.uint8, device=dev)
     ops["tcp_send_seq"] = lambda: cx.tcp_send_seq_batch(conn64, w.status, cseq, ipn, sq_seq, sq_ip, stream=s)
+    ops["tcp_send_seq_groupby"] = lambda: (cx.set_send_seq_groupby(1), cx.tcp_send_seq_batch(
+        conn64, w.status, cseq, ipn, sq_seq, sq_ip, stream=s), cx.set_send_seq_groupby(0))
+    conn2k = (torch.arange(n, device=dev, dtype=torch.int64) * 7919 % 2047).to(torch.int32)
+    cseq2k = torch.zeros(2047, dtype=torch.int32, device=dev)
+    ops["tcp_send_seq_2047conn"] = lambda: cx.tcp_send_seq_batch(conn2k, w.status, cseq2k, ipn, sq_seq, sq_ip,
+                                                                 stream=s)
     ops["tcp_recv_ack"] = lambda: cx.tcp_recv_ack_batch(conn64, deliv, sq_seq, cack, stream=s)
     # receive demux on the decoded fields (frames of this config; C4 marks 1/16 corrupted, 5% control)
     w.corrupt_frames()
@@ -170,6 +176,8 @@ def main():
         "decode_hdr": 32 + 2 + 27 + 4,
         "encode_hdr": 1 + 2 + 1 + 4 + 8 + 32 + 4,
         "tcp_send_seq": 4 + 4 + 4 + 2,  # conn, status in; seq, ip_id out
+        "tcp_send_seq_groupby": 4 + 4 + 4 + 2,
+        "tcp_send_seq_2047conn": 4 + 4 + 4 + 2,
         "tcp_recv_ack": 4 + 1 + 4,      # conn, delivered, seq in
         # record bytes [0, 53) + rec_off + nread in; TcpInfo (26) + decode fields (27) + valid_idx out
         "syncinput_decode": 53 + 8 + 4 + 26 + 27 + 4,
