@@ -265,7 +265,8 @@ class Codec:
 
     def set_send_seq_groupby(self, v: int) -> None:
         """Internal knob for rsk_tcp_send_seq_batch: 0 the per-tile table path when n_conn < 2048
-        (default), 1 the demux group-by path for every n_conn (parity tests and A/B)."""
+        (default), 1 the demux group-by path for every n_conn, 2 the table path with the one-kernel
+        column scan (parity tests and A/B)."""
         fn = lib().rsk__set_send_seq_groupby
         fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
         _check(fn(self._ctx, v), "rsk__set_send_seq_groupby")

@@ -27,6 +27,7 @@ struct rsk_ctx {
     void *sq_ws = nullptr;
     size_t sq_ws_bytes = 0;
     bool sq_force_groupby = false;  // see rsk__set_send_seq_groupby
+    int sq_scan_variant = 0;
     // demux workspace (rsk_demux.hip)
     void *dm_ws = nullptr;
     size_t dm_ws_bytes = 0;

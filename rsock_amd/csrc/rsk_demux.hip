@@ -847,6 +847,79 @@ __global__ __launch_bounds__(kSqScanThreads) void k_sqt_scan(uint32_t *tab, uint
     }
 }
 
+// Coalesced two-kernel form of the column scan: a wave reads 64 adjacent columns of one row per
+// load.  Rows are cut into nch chunks of RC rows (RC a multiple of 16, nch <= 64); grid (column
+// blocks of 64, chunks), 16 waves per block, wave w owns RC / 16 consecutive rows of the chunk.
+//   k_sqt_csum   chunk sums per column -> csum[chunk][col]; chunk 0 snapshots the state into st0
+//   k_sqt_cscan  chunk offset = st0 + earlier chunks' sums, wave offsets by LDS, rows rewritten as
+//                exclusive prefixes; the last chunk's last wave advances the state
+constexpr uint32_t kSqcWaves = 16;
+__global__ __launch_bounds__(kSqcWaves * 64) void k_sqt_csum(const uint32_t *tab, uint32_t nwt, uint32_t n_conn,
+                                                             uint32_t RC, uint32_t *csum, uint32_t *st0,
+                                                             const uint32_t *conn_seq, const uint16_t *ip_next) {
+    __shared__ uint32_t part[kSqcWaves][64];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, ncol = n_conn + 1u;
+    const uint32_t c = blockIdx.x * 64u + lane, ch = blockIdx.y, RW = RC / kSqcWaves;
+    const bool ok = c < ncol;
+    const uint32_t r0 = ch * RC + wv * RW;
+    uint32_t sm = 0;
+    if (ok) {
+#pragma unroll 16
+        for (uint32_t k = 0; k < RW; ++k)
+            if (r0 + k < nwt) sm += tab[(uint64_t)(r0 + k) * ncol + c];
+    }
+    part[wv][lane] = sm;
+    __syncthreads();
+    if (wv == 0 && ok) {
+        uint32_t tot = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < kSqcWaves; ++q) tot += part[q][lane];
+        csum[(uint64_t)ch * ncol + c] = tot;
+        if (ch == 0) st0[c] = c < n_conn ? conn_seq[c] : (uint32_t)*ip_next;
+    }
+}
+
+__global__ __launch_bounds__(kSqcWaves * 64) void k_sqt_cscan(uint32_t *tab, uint32_t nwt, uint32_t n_conn,
+                                                              uint32_t RC, uint32_t nch, const uint32_t *csum,
+                                                              const uint32_t *st0, uint32_t *conn_seq,
+                                                              uint16_t *ip_next) {
+    __shared__ uint32_t part[kSqcWaves][64];
+    __shared__ uint32_t cbase[64];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, ncol = n_conn + 1u;
+    const uint32_t c = blockIdx.x * 64u + lane, ch = blockIdx.y, RW = RC / kSqcWaves;
+    const bool ok = c < ncol;
+    const uint32_t r0 = ch * RC + wv * RW;
+    uint32_t sm = 0;
+    if (ok) {
+#pragma unroll 16
+        for (uint32_t k = 0; k < RW; ++k)
+            if (r0 + k < nwt) sm += tab[(uint64_t)(r0 + k) * ncol + c];
+    }
+    part[wv][lane] = sm;
+    if (wv == 0) {
+        uint32_t b = ok ? st0[c] : 0u;
+        if (ok)
+            for (uint32_t q = 0; q < ch; ++q) b += csum[(uint64_t)q * ncol + c];
+        cbase[lane] = b;
+    }
+    __syncthreads();
+    if (!ok) return;
+    uint32_t run = cbase[lane];  // mod 2^32 (TcpInfo::seq) / mod 2^16 once stored (mIpId)
+    for (uint32_t q = 0; q < wv; ++q) run += part[q][lane];
+#pragma unroll 16
+    for (uint32_t k = 0; k < RW; ++k) {
+        if (r0 + k >= nwt) break;
+        uint32_t *e = tab + (uint64_t)(r0 + k) * ncol + c;
+        const uint32_t v = *e;
+        *e = run;
+        run += v;
+    }
+    if (ch == nch - 1u && wv == kSqcWaves - 1u) {
+        if (c < n_conn) conn_seq[c] = run;
+        else *ip_next = (uint16_t)run;
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void k_sqt_apply(const uint32_t *conn, const int32_t *status, uint32_t n,
                                                       uint32_t n_conn, uint32_t W, uint32_t nwt, const uint32_t *tab,
                                                       uint32_t *seq, uint16_t *ip_id) {
@@ -965,7 +1038,7 @@ extern "C" int rsk_tcp_send_seq_batch(rsk_ctx *c, uint32_t n, const uint32_t *co
     hipStream_t s = (hipStream_t)stream;
     const bool table = n_conn + 1ull <= kSqCols && !c->sq_force_groupby;
     const uint32_t W = sqt_wave_tile(n_conn), nwt = (uint32_t)((n + (uint64_t)W - 1) / W);
-    const size_t need = table ? 4ull * nwt * (n_conn + 1ull) : sq_layout(n, n_conn, nullptr, nullptr);
+    const size_t need = table ? 4ull * (nwt + 64ull + 1ull) * (n_conn + 1ull) : sq_layout(n, n_conn, nullptr, nullptr);
     if (!c->sq_ws || c->sq_ws_bytes < need) {
         if (c->sq_ws) {
             hipError_t e = hipDeviceSynchronize();
@@ -983,10 +1056,22 @@ extern "C" int rsk_tcp_send_seq_batch(rsk_ctx *c, uint32_t n, const uint32_t *co
         uint32_t *tab = static_cast<uint32_t *>(c->sq_ws);
         const unsigned nbt = (nwt + kWaves - 1) / kWaves;
         const size_t lds = 4ull * kWaves * (n_conn + 1ull);
-        const uint32_t cb = n_conn + 1u <= 128u ? 1u : n_conn + 1u <= 512u ? 16u : 64u;  // more row groups when narrow
         hipLaunchKernelGGL(k_sqt_sum, dim3(nbt), dim3(kBlock), lds, s, conn, status, n, n_conn, W, nwt, tab);
-        hipLaunchKernelGGL(k_sqt_scan, dim3((n_conn + cb) / cb), dim3(kSqScanThreads), 0, s, tab, nwt, n_conn, cb,
-                           conn_seq, ip_id_next);
+        if (c->sq_scan_variant == 1) {
+            const uint32_t cb = n_conn + 1u <= 128u ? 1u : n_conn + 1u <= 512u ? 16u : 64u;  // more row groups when narrow
+            hipLaunchKernelGGL(k_sqt_scan, dim3((n_conn + cb) / cb), dim3(kSqScanThreads), 0, s, tab, nwt, n_conn, cb,
+                               conn_seq, ip_id_next);
+        } else {
+            uint32_t RC = 256;
+            while ((nwt + RC - 1) / RC > 64u) RC <<= 1;
+            const uint32_t nch = (nwt + RC - 1) / RC;
+            uint32_t *csum = tab + (size_t)nwt * (n_conn + 1u), *st0 = csum + (size_t)nch * (n_conn + 1u);
+            const dim3 g((n_conn + 64u) / 64u, nch);
+            hipLaunchKernelGGL(k_sqt_csum, g, dim3(kSqcWaves * 64), 0, s, tab, nwt, n_conn, RC, csum, st0, conn_seq,
+                               ip_id_next);
+            hipLaunchKernelGGL(k_sqt_cscan, g, dim3(kSqcWaves * 64), 0, s, tab, nwt, n_conn, RC, nch, csum, st0,
+                               conn_seq, ip_id_next);
+        }
         hipLaunchKernelGGL(k_sqt_apply, dim3(nbt), dim3(kBlock), lds, s, conn, status, n, n_conn, W, nwt, tab, seq,
                            ip_id);
         return rsk::launch_check("k_sqt_apply");
@@ -1020,10 +1105,12 @@ extern "C" int rsk_tcp_send_seq_batch(rsk_ctx *c, uint32_t n, const uint32_t *co
     return rsk::launch_check("k_sq_seq");
 }
 
-// internal A/B + test knob (not in the public header): 1 sends every n_conn through the group-by path
+// internal A/B + test knob (not in the public header): 1 sends every n_conn through the group-by path,
+// 2 keeps the table path with the one-kernel column scan (k_sqt_scan, A/B)
 extern "C" int rsk__set_send_seq_groupby(rsk_ctx *c, int v) {
-    if (!c || v < 0 || v > 1) return RSK_EINVAL;
-    c->sq_force_groupby = v != 0;
+    if (!c || v < 0 || v > 2) return RSK_EINVAL;
+    c->sq_force_groupby = v == 1;
+    c->sq_scan_variant = v == 2 ? 1 : 0;
     return RSK_OK;
 }
 

@@ -20,8 +20,8 @@ def _dev(a, gpu, dt):
 
 
 # n_conn + 1 <= 2048 takes the per-tile table path (k_sqt_*), larger ones the demux group-by; groupby=1
-# forces the group-by for every case so both paths stay pinned to the oracle
-@pytest.mark.parametrize("groupby", [0, 1])
+# forces the group-by for every case so both paths stay pinned to the oracle (2: the one-kernel column scan)
+@pytest.mark.parametrize("groupby", [0, 1, 2])
 @pytest.mark.parametrize("n,n_conn", [(1, 1), (777, 1), (5000, 7), (70_000, 300), (300_000, 70_000), (1, 0),
                                       (100_000, 0), (513, 64), (1_000_003, 64), (200_000, 511), (200_000, 512),
                                       (250_001, 2047), (250_001, 2048), (70_000, 1)])

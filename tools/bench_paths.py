@@ -89,6 +89,8 @@ def main():
     ops["tcp_send_seq"] = lambda: cx.tcp_send_seq_batch(conn64, w.status, cseq, ipn, sq_seq, sq_ip, stream=s)
     ops["tcp_send_seq_groupby"] = lambda: (cx.set_send_seq_groupby(1), cx.tcp_send_seq_batch(
         conn64, w.status, cseq, ipn, sq_seq, sq_ip, stream=s), cx.set_send_seq_groupby(0))
+    ops["tcp_send_seq_scan1"] = lambda: (cx.set_send_seq_groupby(2), cx.tcp_send_seq_batch(
+        conn64, w.status, cseq, ipn, sq_seq, sq_ip, stream=s), cx.set_send_seq_groupby(0))
     conn2k = (torch.arange(n, device=dev, dtype=torch.int64) * 7919 % 2047).to(torch.int32)
     cseq2k = torch.zeros(2047, dtype=torch.int32, device=dev)
     ops["tcp_send_seq_2047conn"] = lambda: cx.tcp_send_seq_batch(conn2k, w.status, cseq2k, ipn, sq_seq, sq_ip,
@@ -177,6 +179,7 @@ def main():
         "encode_hdr": 1 + 2 + 1 + 4 + 8 + 32 + 4,
         "tcp_send_seq": 4 + 4 + 4 + 2,  # conn, status in; seq, ip_id out
         "tcp_send_seq_groupby": 4 + 4 + 4 + 2,
+        "tcp_send_seq_scan1": 4 + 4 + 4 + 2,
         "tcp_send_seq_2047conn": 4 + 4 + 4 + 2,
         "tcp_recv_ack": 4 + 1 + 4,      # conn, delivered, seq in
         # record bytes [0, 53) + rec_off + nread in; TcpInfo (26) + decode fields (27) + valid_idx out
