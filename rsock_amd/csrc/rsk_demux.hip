@@ -742,8 +742,9 @@ __global__ __launch_bounds__(kBlock) void k_ack_lds(const uint32_t *conn, const 
 // below is at most 4 B per packet).  Column c < n_conn of a tile's row is connection c's framed
 // bytes in the tile, column n_conn its framed-packet count (the IP id column).
 //   k_sqt_sum    per wave tile, a wave-private LDS row (ds_add), written to tab[tile][col]
-//   k_sqt_scan   per column, exclusive scan down the tiles, rebased on conn_seq[c] / *ip_id_next,
-//                in place; the column's total advances the state
+//   k_sqt_csum / k_sqt_cscan   per column, exclusive scan down the tiles, rebased on conn_seq[c] /
+//                *ip_id_next, in place; the column's total advances the state (k_sqt_scan: the
+//                one-kernel form, A/B)
 //   k_sqt_apply  per wave tile in batch order: the row back into LDS, then per 64-packet round the
 //                in-wave per-connection exclusive prefix by a readlane walk of the 64 lanes; the last
 //                lane of each connection carries the row forward
