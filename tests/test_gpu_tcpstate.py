@@ -52,6 +52,32 @@ def test_send_seq_matches_oracle(codec, gpu, oracle, n, n_conn, groupby):
     codec.set_send_seq_groupby(0)
 
 
+# BASELINE C3 size (4M packets) with bursty traffic: runs of 1-200 packets of one connection, as a
+# sender drains one connection's queue at a time, so rounds of 64 lanes hold long same-connection runs
+@pytest.mark.parametrize("n_conn", [1, 64, 2047])
+def test_send_seq_fullsize_bursts(codec, gpu, oracle, n_conn):
+    import torch
+
+    n = 4 * 1024 * 1024
+    rng = np.random.default_rng(n_conn)
+    runs = rng.integers(1, 201, n // 50 + 1)
+    owner = rng.integers(0, n_conn, runs.size)
+    conn = np.repeat(owner, runs)[:n].astype(np.uint32)
+    status = np.where(rng.random(n) < 0.97, 31 + 1400, 0).astype(np.int32)
+    cs0 = rng.integers(0, 2**32, n_conn, dtype=np.uint64).astype(np.uint32)
+    d_cs = _dev(cs0, gpu, np.int32)
+    d_ipn = _dev(np.array([123], np.uint16), gpu, np.int16)
+    seq = torch.empty(n, dtype=torch.int32, device=gpu)
+    ipid = torch.empty(n, dtype=torch.int16, device=gpu)
+    codec.tcp_send_seq_batch(_dev(conn, gpu, np.int32), _dev(status, gpu, np.int32), d_cs, d_ipn, seq, ipid)
+    torch.cuda.synchronize()
+    es, ei, cs_host, ip_host = oracle.tcp_send_seq_batch(conn, status, cs0, 123)
+    assert np.array_equal(seq.cpu().numpy().view(np.uint32), es)
+    assert np.array_equal(ipid.cpu().numpy().view(np.uint16), ei)
+    assert np.array_equal(d_cs.cpu().numpy().view(np.uint32), cs_host)
+    assert int(d_ipn.cpu().numpy().view(np.uint16)[0]) == ip_host
+
+
 def test_recv_ack_matches_oracle(codec, gpu, oracle):
     import torch
 
