@@ -964,7 +964,9 @@ __global__ __launch_bounds__(kBlock) void k_sqt_apply(const uint32_t *conn, cons
                 const uint32_t sl = (uint32_t)__builtin_amdgcn_readlane((int)len, d);
                 const uint64_t eq = __ballot(key == sk);
                 const uint64_t above = d == 63 ? 0ull : eq & (~0ull << (d + 1));
-                ex += __builtin_amdgcn_inverse_ballot_w64(above) ? sl : 0u;
+                uint32_t ex1 = ex + sl;                  // v_add with the SGPR operand, then a select on
+                asm volatile("" : "+v"(ex1));            // the mask (not folded back into add(select))
+                ex = __builtin_amdgcn_inverse_ballot_w64(above) ? ex1 : ex;
                 laterm |= eq & ((1ull << d) - 1ull);
                 asm volatile("" : "+v"(ex), "+s"(laterm));  // no sinking: consume each mask in its own step
             }
