@@ -1,13 +1,19 @@
 #!/usr/bin/env python3
 """Benchmark: device-resident EncHead+MD5 encode then decode+verify+compact (BASELINE.json metric).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3] [--no-cpu-baseline]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4|c5] [--no-cpu-baseline]
 
 One step = one pass of the hot path over one batch: k_encode (RConn::Output framing of every
 packet) followed by k_decode + compaction (RConn::OnRecv of every frame), inputs resident in HBM.
-N > 1 runs under torch.distributed.run, one rank per GPU, each rank on its own shard of packets
-(weak scaling, no data-path collective; the only collectives are the timing barrier/max).
-Rank 0 prints ONE JSON line.
+
+Workload: N = 1 defaults to C3 (4M x 1400-B packets, the metric's target config); N > 1 defaults
+to C5 (BASELINE configs[4]: 64M x 1400-B packets in total, contiguous shards, strong scaling), so
+`--gpus 8` IS config 5 and `--gpus 1 --config c5` is the scaling curve's N = 1 point.
+
+N > 1: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set) this process is one rank;
+without a launcher, `--gpus N` starts the N rank processes itself (from this parent, which never
+touches the GPU) and relays rank 0's line.  No data-path collective: the only collectives are the
+timing barrier and the max over ranks.  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -26,7 +32,7 @@ METRIC = "Mpkt/s + GiB/s device-resident EncHead+MD5 encode/decode at 1/2/4/8 GP
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
-def enc_bytes_per_pkt(p: int) -> int:
+def enc_bytes_per_pkt(p):
     """Algorithmic bytes of k_encode per packet: reads payload P, cmd 1,
     conv 4, connKey 8, pay_len 2, pay_off 8, frame_off 8; writes frame 31+P, status 4."""
     return p + 1 + 4 + 8 + 2 + 8 + 8 + (31 + p) + 4
@@ -41,51 +47,76 @@ def dec_bytes_per_pkt() -> int:
 
 def load_traffic(cfg: str, n: int) -> dict | None:
     """HBM traffic per k_encode launch measured by tools/pmc_traffic.py (separate rocprofv3 --pmc
-    passes, gfx950 FETCH_SIZE x2 correction), if a matching record exists under profiles/."""
+    passes, gfx950 FETCH_SIZE x2 correction) for this (config, packets), if profiles/ holds one."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     if not os.path.exists(path):
         return None
     try:
-        rec = json.load(open(path))
+        table = json.load(open(path))
     except Exception:
         return None
-    if rec.get("config") != cfg or int(rec.get("packets", -1)) != n:
+    if "config" in table:  # single-record form
+        table = {f"{table['config']}:{table['packets']}": table}
+    return table.get(f"{cfg}:{n}")
+
+
+def _cpu_quota() -> float | None:
+    """CPUs the cgroup grants this process (cgroup v2 cpu.max), None when unlimited/unknown."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
         return None
-    return rec
 
 
 def cpu_baseline(cfg: str, n_sample: int, min_seconds: float) -> dict:
     """The reference's own codec (oracle/_ref, compiled from /root/reference sources) or, if that
-    was not built, the C restatement, timed on this host's cores over a bounded sample."""
+    was not built, the C restatement, timed on this host's cores over a bounded sample
+    (SURVEY.md §8d: std::thread x every core of the affinity mask, contiguous shards, plus a
+    1-thread number on the same arenas)."""
     from rsock_amd import workload
     from tests import oracle_lib
 
-    threads = min(16, len(os.sched_getaffinity(0)))
+    cores = len(os.sched_getaffinity(0))
     d = workload.describe(cfg, 0, n_sample)
     payload = workload.payload_bytes_np(d)
     frames = np.zeros(d.n * d.frame_pitch, np.uint8)
     key = b"hello135"
     if oracle_lib.ref_available():
         ref = oracle_lib.RefOracle()
-        run = lambda: ref.bench_codec(key, payload, d, workload.ID_UNIFORM, frames, threads)  # noqa: E731
         kind = "reference"
+
+        def run(threads, m):
+            ref.bench_codec(key, payload, _prefix(d, m), workload.ID_UNIFORM, frames, threads)
     else:
         orc = oracle_lib.Oracle()
-
-        def run():
-            fr, st = orc.encode_batch(key, payload, d, workload.ID_UNIFORM, nthreads=threads)
-            orc.decode_batch(key, fr, d.frame_off, d.frame_len, nthreads=threads)
-
         kind = "port"
-    run()  # warm (page faults on the frame arena)
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        run()
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= min_seconds:
-            break
-    pkts = reps * d.n
+
+        def run(threads, m):
+            dm = _prefix(d, m)
+            fr, st = orc.encode_batch(key, payload, dm, workload.ID_UNIFORM, nthreads=threads)
+            orc.decode_batch(key, fr, dm.frame_off, dm.frame_len, nthreads=threads)
+
+    def timed(threads, m, seconds):
+        run(threads, m)  # warm (page faults on the frame arena)
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            run(threads, m)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                return reps * m / el / 1e6, reps, el
+
+    # every core of the affinity mask (SURVEY §8d); when a cgroup quota grants fewer CPUs than the
+    # mask shows, that many threads too, and the faster of the two is the baseline
+    quota = _cpu_quota()
+    runs = {cores: timed(cores, d.n, min_seconds)}
+    if quota and int(quota) < cores:
+        runs[max(1, int(quota))] = timed(max(1, int(quota)), d.n, min_seconds)
+    best = max(runs, key=lambda t: runs[t][0])
+    v_all, reps_all, el_all = runs[best]
+    m1 = min(d.n, 1 << 16)
+    v_one, reps_one, el_one = timed(1, m1, min_seconds / 2)
     cpu_model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -94,15 +125,73 @@ def cpu_baseline(cfg: str, n_sample: int, min_seconds: float) -> dict:
                 break
     except OSError:
         pass
+    p = d.pay_len.astype(np.int64)
+    pay = f"{int(p[0])}-B payloads" if p.min() == p.max() else \
+        f"mixed {int(p.min())}-{int(p.max())}-B payloads, mean {p.mean():.0f} B"
     return {
-        "value": round(pkts / el / 1e6, 3),
+        "value": round(v_all, 3),
         "unit": "Mpkt/s",
-        "cores": threads,
+        "cores": best,
         "kind": kind,
-        "sample": f"{d.n} packets of {cfg.upper()} ({int(d.pay_len[0])}-B payloads) x {reps} passes, "
-                  f"{el:.1f} s wall; per packet: RConn::Output framing (compute_hash + Enc2Buf + memcpy into "
-                  f"a zeroed 1500-B buffer) then DecodeBuf + hash_equal; {threads} threads; {cpu_model}",
+        "value_1thread": round(v_one, 3),
+        "by_threads": {str(t): round(r[0], 3) for t, r in sorted(runs.items())},
+        "affinity_cpus": cores,
+        "cgroup_cpus": quota,
+        "sample": f"{d.n} packets of {cfg.upper()} ({pay}) x {reps_all} passes on {best} threads "
+                  f"({el_all:.1f} s; threads tried: {sorted(runs)} = affinity mask"
+                  + (f", cgroup quota {quota} CPUs" if quota else "") + f"), and {m1} packets x {reps_one} passes "
+                  f"on 1 thread ({el_one:.1f} s); per packet: RConn::Output framing (compute_hash + Enc2Buf + memcpy "
+                  f"into a zeroed 1500-B buffer) then DecodeBuf + hash_equal; {cpu_model}",
     }
+
+
+def _prefix(d, m: int):
+    """The first m packets of a shard's descriptors (same arenas)."""
+    import dataclasses
+
+    if m >= d.n:
+        return d
+    return dataclasses.replace(d, n=m, pay_off=d.pay_off[:m], pay_len=d.pay_len[:m], cmd=d.cmd[:m],
+                               conv=d.conv[:m], conn_key=d.conn_key[:m], frame_off=d.frame_off[:m],
+                               frame_len=d.frame_len[:m], corrupt=d.corrupt[:m])
+
+
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int) -> int:
+    """`--gpus N` without a launcher: start N rank processes of this script (this parent never
+    initialises the GPU), rank r on GPU r, rendezvous on 127.0.0.1; rank 0's stdout is ours.
+    A failed rank ends the others (their exact PIDs) and its exit code is returned."""
+    import subprocess
+
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in pending:
+                    q.kill()
+        time.sleep(0.05)
+    return rc if rc >= 0 else 128 - rc
 
 
 def main() -> None:
@@ -110,17 +199,22 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4", "c5"],
+    ap.add_argument("--config", default=None, choices=["c2", "c3", "c4", "c5"],
                     help="c2/c3/c4: that config per GPU (weak scaling); c5: BASELINE config 5, 64M 1400-B "
-                         "packets in total split over the ranks (strong scaling; 1 GPU holds all 64M: ~185 GB)")
-    ap.add_argument("--packets", type=int, default=0, help="packets per GPU (default: the config's)")
+                         "packets in total split over the ranks (strong scaling; 1 GPU holds all 64M: ~185 GB). "
+                         "Default: c3 at N = 1, c5 at N > 1")
+    ap.add_argument("--packets", type=int, default=0,
+                    help="packets per GPU (c2-c4) or in total (c5); default: the config's")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1 << 20)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=6.0)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal only: every rank uses GPU 0 (N ranks on a 1-GPU box)")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
 
     import torch
     import torch.distributed as dist
@@ -131,8 +225,8 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}")
     gpu = 0 if args.same_device else local
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
@@ -142,7 +236,7 @@ def main() -> None:
         else:
             dist.init_process_group(args.dist_backend)
 
-    cfg = args.config
+    cfg = args.config or ("c3" if world == 1 else "c5")
     strong = cfg == "c5"
     if strong:
         # strong scaling: the config's total is split over the ranks (contiguous shards)
@@ -199,8 +293,9 @@ def main() -> None:
     total_pkts = (n_total if strong else world * d.n) * args.steps
     mpkts = total_pkts / elapsed_max / 1e6
     p = int(d.pay_len[0]) if workload.CONFIGS[cfg][2] == workload.CONFIGS[cfg][3] else int(d.pay_len.mean())
-    bytes_step = d.n * (enc_bytes_per_pkt(p) + dec_bytes_per_pkt())
-    enc_bytes = d.n * enc_bytes_per_pkt(p)
+    # algorithmic bytes of this rank's launch, summed over its packets' actual payload lengths
+    enc_bytes = int(enc_bytes_per_pkt(d.pay_len.astype(np.int64)).sum())
+    bytes_step = enc_bytes + d.n * dec_bytes_per_pkt()
     achieved = enc_bytes / (enc_ms * 1e-3) / 1e9
 
     if rank == 0:

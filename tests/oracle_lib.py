@@ -13,6 +13,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle.so")
 REF_SO = os.path.join(ROOT, "oracle", "_ref", "librsk_ref.so")
+REF_PARSE_SO = os.path.join(ROOT, "oracle", "_ref", "librsk_ref_parse.so")
 
 _vp = ctypes.c_void_p
 
@@ -350,5 +351,37 @@ class RefOracle:
                                       _p(fo), nthreads)
 
 
+class RefParse:
+    """The reference's own RawTcp::RawInput (oracle/_ref/librsk_ref_parse.so, conn/RawTcp.cpp:138-237
+    compiled with the objects it needs; oracle/ref_parse_harness.cpp).  Loaded with RTLD_LAZY: the
+    libnet / pcap / service functions RawInput never calls stay unbound (oracle/Makefile)."""
+
+    FIELDS = ("ret", "called", "src", "dst", "sp", "dp", "seq", "ack", "flag", "pay_off", "payload_len",
+              "base_ret", "pool_n", "pool_src", "pool_dst", "pool_sp", "pool_dp", "pool_seq", "pool_ack",
+              "pool_flag")
+
+    def __init__(self, path: str = REF_PARSE_SO):
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        L = self.L = ctypes.CDLL(path, mode=os.RTLD_LAZY)
+        L.ref_rawinput.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_int, _vp]
+
+    def rawinput(self, pkt: bytes, wire_len: int, cap_len: int, datalink: int, is_server: bool,
+                 with_ack_pool: bool) -> dict:
+        out = np.zeros(20, np.uint32)
+        # the reference reads headers without looking at caplen: give it slack past the packet
+        self.L.ref_rawinput(bytes(pkt) + bytes(128), wire_len, cap_len, datalink, int(is_server),
+                            int(with_ack_pool), out.ctypes.data)
+        r = {k: int(v) for k, v in zip(self.FIELDS, out)}
+        for k in ("ret", "payload_len", "base_ret"):
+            r[k] = int(np.int32(np.uint32(r[k])))
+        return r
+
+
 def ref_available() -> bool:
     return os.path.exists(REF_SO)
+
+
+def ref_parse_available() -> bool:
+    return os.path.exists(REF_PARSE_SO)

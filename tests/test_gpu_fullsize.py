@@ -1,5 +1,5 @@
-"""Full BASELINE sizes (C2 1M x 64 B, C3 4M x 1400 B, C4 1M mixed) through size-independent
-properties checked on the device:
+"""Full BASELINE sizes (C2 1M x 64 B, C3 4M x 1400 B, C4 1M mixed, a C5 shard of 8M x 1400 B)
+through size-independent properties checked on the device:
   * encode -> decode round trip: every framed packet verifies, compaction is the identity list
   * frame payload region == payload bytes; header bytes == the SoA fields (LE)
   * tag bytes == the oracle's 256-entry tag table at payload[0] (the tag depends only on it)
@@ -33,11 +33,27 @@ def _le_bytes(x, nbytes):
 @pytest.mark.parametrize("cfg", ["c3", "c2", "c4"])
 @pytest.mark.parametrize("pad16", [True, False])
 def test_fullsize_roundtrip(codec, gpu, oracle, cfg, pad16):
+    _roundtrip(codec, gpu, oracle, workload.describe(cfg), pad16)
+
+
+@pytest.mark.parametrize("rank", [7, 0])
+def test_c5_shard_roundtrip(codec, gpu, oracle, rank):
+    """BASELINE config 5 (64M x 1400-B packets sharded 8 ways): the shard rank `rank` of 8 runs on
+    one device (8M packets, ~23 GB of arenas) — what each GPU of the 8-GPU bench line computes."""
+    lo, hi = workload.shard_range(64 << 20, rank, 8)
+    d = workload.describe("c5", lo, hi, n=64 << 20)
+    assert d.n == 8 << 20 and d.first == lo
+    _roundtrip(codec, gpu, oracle, d, True)
+
+
+def _roundtrip(codec, gpu, oracle, d, pad16):
     import torch
 
-    d = workload.describe(cfg)
     w = workload.DeviceWorkload(d, gpu)
     n = d.n
+    # the device-generated arena is this shard's slice of the config's payload byte stream
+    head = workload.splitmix_bytes_np(d.payload_seed, 1 << 16, d.first * d.pay_pitch)
+    assert np.array_equal(w.payload[: 1 << 16].cpu().numpy(), head)
     codec.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
                        w.status, id_uniform=workload.ID_UNIFORM, pad16=pad16)
     torch.cuda.synchronize()

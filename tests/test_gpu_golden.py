@@ -89,3 +89,43 @@ def test_enchead_shims_match_reference(codec):
         if r is not None:
             assert r[1:] == (int(g["dec_cmd"][i]), g["dec_id"][8 * i: 8 * i + 8].tobytes(), int(g["dec_conv"][i]),
                              int(g["dec_key"][i]))
+
+
+@pytest.mark.parametrize("flags", [0, 1, 3])
+@pytest.mark.parametrize("align", [1, 16])
+def test_parse_matches_reference_rawinput(codec, gpu, oracle, flags, align):
+    """k_parse_decode == the reference's own RawTcp::RawInput (tests/golden/parse.npz, made by
+    tests/golden/make_parse_golden.py from oracle/_ref/librsk_ref_parse.so) on every case of the
+    SURVEY §8c parse list; the decode half == the oracle (itself pinned to the reference's OnRecv)."""
+    import torch
+
+    from rsock_amd.codec import DecodeBuffers, TcpInfoBuffers
+    from tests import pkt as P
+    from tests.test_gpu_parity import assert_dec_equal
+
+    g = gold("parse.npz")
+    j = list(g["flags"]).index(flags)
+    for dl in (1, 0):
+        sel = np.nonzero(g["datalink"] == dl)[0]
+        recs = [g["arena"][int(g["off"][i]): int(g["off"][i]) + int(g["cap_len"][i])].tobytes() for i in sel]
+        arena, offs, cl = P.pack_records(recs, align=align, base_pad=0 if align == 16 else 3)
+        wl = g["wire_len"][sel].astype(np.uint32)
+        n = len(sel)
+        tcp, out = TcpInfoBuffers.alloc(n, gpu), DecodeBuffers.alloc(n, gpu)
+        codec.rawinput_batch(dev(arena, gpu), dev(offs, gpu, np.int64), dev(wl, gpu, np.int32), dev(cl, gpu, np.int32),
+                             dl, flags, tcp, out)
+        torch.cuda.synchronize()
+        th = tcp.to_host()
+        st = th["parse_status"].view(np.int8)
+        refused = g["syn_refused"][sel, j]
+        exp_st = np.where(refused, 2, g["status"][sel, j])
+        bad = np.nonzero(st != exp_st)[0]
+        assert bad.size == 0, (dl, sel[bad[:5]], st[bad[:5]], exp_st[bad[:5]])
+        pin = (exp_st == 1) | ((exp_st == 2) & ~refused)
+        for k, dt in (("src", np.uint32), ("dst", np.uint32), ("sp", np.uint16), ("dp", np.uint16), ("seq", np.uint32),
+                      ("ack", np.uint32), ("flag", np.uint8)):
+            assert np.array_equal(th[k].view(dt)[pin], g[k][sel, j][pin]), (dl, k)
+        dl_ = exp_st == 1
+        assert np.array_equal(th["cap_pay_off"].view(np.uint16)[dl_], g["pay_off"][sel, j][dl_])
+        assert np.array_equal(th["cap_pay_len"].view(np.uint16)[dl_], g["pay_len"][sel, j][dl_])
+        assert_dec_equal(out.to_host(), oracle.parse_decode_batch(KEY, arena, offs, wl, cl, dl, flags))

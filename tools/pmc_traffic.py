@@ -49,7 +49,13 @@ def main():
     s = json.dumps(rec, indent=1)
     print(s)
     if a.out:
-        open(a.out, "w").write(s + "\n")
+        # one record per (config, packets): profiles/traffic.json maps "c3:4194304" -> record
+        table = {}
+        if os.path.exists(a.out):
+            old = json.load(open(a.out))
+            table = {f"{old['config']}:{old['packets']}": old} if "config" in old else old
+        table[f"{a.config}:{a.packets}"] = rec
+        open(a.out, "w").write(json.dumps(table, indent=1) + "\n")
 
 
 if __name__ == "__main__":
