@@ -116,10 +116,17 @@ typedef struct rsk_ctx rsk_ctx;
 rsk_ctx *rsk_create(const uint8_t *key, uint32_t key_len, int device);
 void rsk_destroy(rsk_ctx *ctx);
 
-/* Pre-size the context's device workspace (decode compaction scratch) for batches of up to n
- * packets.  Batch calls grow it on demand, which allocates and synchronises; call this first if
- * batch calls will be captured into a hipGraph. */
+/* Streams: a context may be used from several streams at once.  Its device scratch (compaction
+ * masks and counts, demux and send-seq tables) is kept per stream, so calls on different streams
+ * never share it; calls on ONE stream must be issued in the order the caller wants them to run
+ * (from one host thread at a time, as with any hipStream_t).  The only per-context state the
+ * kernels read is the immutable key schedule.
+ *
+ * Pre-size the compaction scratch of `stream` (rsk_reserve: the legacy default stream, NULL) for
+ * batches of up to n packets.  Batch calls grow it on demand, which waits for that stream to
+ * drain and allocates; reserve first if batch calls will be captured into a hipGraph. */
 int rsk_reserve(rsk_ctx *ctx, uint32_t n_max);
+int rsk_reserve_stream(rsk_ctx *ctx, uint32_t n_max, void *stream);
 
 /* Text of the last HIP error seen by this thread (static storage). */
 const char *rsk_last_error(void);
@@ -318,7 +325,8 @@ int rsk_tcp_send_seq_batch(rsk_ctx *ctx, uint32_t n, const uint32_t *conn, const
 /* Receive: FakeTcp::OnRecv (conn/FakeTcp.cpp:52-66) raises its connection's ack to a delivered
  * packet's TcpInfo seq (rsk_parse_decode_batch's tcp->seq) when that is larger (unsigned compare,
  * as the reference), so over a batch conn_ack[c] = max(conn_ack[c], seq[i] of every packet i with
- * delivered[i] != 0 and conn[i] == c) — independent of order; conn[i] >= n_conn is skipped. */
+ * delivered[i] != 0 and conn[i] == c) — independent of order; conn[i] >= n_conn is skipped.
+ * n <= 2^30 (RSK_EINVAL above). */
 int rsk_tcp_recv_ack_batch(rsk_ctx *ctx, uint32_t n, const uint32_t *conn, const uint8_t *delivered,
                            const uint32_t *seq, uint32_t n_conn, uint32_t *conn_ack, void *stream);
 

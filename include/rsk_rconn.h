@@ -40,8 +40,10 @@ void rsk_rconn_destroy(rsk_rconn *r); /* flushes first */
 void rsk_rconn_set_callbacks(rsk_rconn *r, rsk_send_fn send, rsk_reset_fn reset, rsk_recv_fn recv,
                              void *cb_arg);
 
-/* RConn::Output: nread < 0 -> nread; nread == 0 -> reset callback's value; 31 + nread > 1500 -> -1;
- * otherwise the packet is queued and 31 + nread is returned. */
+/* RConn::Output: nread < 0 -> nread; 31 + nread > 1500 -> -1; otherwise the packet is queued and
+ * 31 + nread is returned.  nread == 0 (RConnReset::SendReset, RConn.cpp:119-123) is queued too and
+ * returns 0: its reset callback fires at delivery, after the send callbacks of every packet queued
+ * before it and before those queued after it (send and reset callbacks come in input order). */
 int rsk_rconn_output(rsk_rconn *r, int64_t nread, const char *base, uint8_t cmd, const uint8_t id[8],
                      uint32_t conv, uint64_t conn_key, void *user);
 /* RConn::OnRecv: queues the frame (tcp_close = TcpInfo::HasCloseFlag on a TCP frame); returns 0 or

@@ -10,7 +10,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librsk.so")
+# RSK_LIB selects another in-tree build of the same library (tools: librsk_ab.so, the A/B build)
+LIB_PATH = os.path.join(_HERE, os.environ.get("RSK_LIB", "librsk.so"))
 
 # ---- constants (include/rsk_codec.h) ------------------------------------------------------------
 HASH_BUF_SIZE = 8
@@ -125,6 +126,7 @@ SIGNATURES = [
     ("rsk_create", _vp, [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_int]),
     ("rsk_destroy", None, [_vp]),
     ("rsk_reserve", ctypes.c_int, [_vp, ctypes.c_uint32]),
+    ("rsk_reserve_stream", ctypes.c_int, [_vp, ctypes.c_uint32, _vp]),
     ("rsk_last_error", ctypes.c_char_p, []),
     ("rsk_version", ctypes.c_char_p, []),
     ("rsk_encode_batch", ctypes.c_int,

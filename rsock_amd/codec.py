@@ -48,6 +48,15 @@ class RskError(RuntimeError):
     pass
 
 
+def _ab_fn(name: str):
+    try:
+        fn = getattr(lib(), name)
+    except AttributeError:
+        raise RskError(f"{name}: A/B knob of the tools build only (make -C rsock_amd ab; RSK_LIB=librsk_ab.so)")
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    return fn
+
+
 def _check(rc: int, what: str) -> None:
     if rc != 0:
         err = lib().rsk_last_error()
@@ -245,22 +254,15 @@ class Codec:
             pass
 
     def set_encode_variant(self, v: int) -> None:
-        """Internal tuning knob (not in the public header) selecting k_encode's copy path: 0 hybrid
-        with the one-load DPP per-packet copy, 12 packets per iteration, the tag computed in the copy loop
-        for sets of long frames and nontemporal stores for sets whose frames leave gaps (default); 1-12
-        per-packet / flat / non-temporal / interleaved variants, 13 the two-load hybrid, 14-24 DPP
-        variants, 25 the default with XCD-contiguous block numbering,
-        26-28 the default with 2 / 4 / 8 sets per wave; + 100 * cap holds the kernel to cap blocks per CU (list in rsk_kernels.hip).  Every variant is parity-tested; used for in-process A/B."""
-        fn = lib().rsk__set_encode_variant
-        fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        """A/B build only (RSK_LIB=librsk_ab.so, `make -C rsock_amd ab`): selects a k_encode variant
+        for in-process A/B runs (tools/ab_encode.py; the list is in rsk_kernels.hip).  The shipped
+        librsk.so has exactly one encode kernel and no such knob."""
+        fn = _ab_fn("rsk__set_encode_variant")
         _check(fn(self._ctx, v), "rsk__set_encode_variant")
 
     def set_wire_variant(self, v: int) -> None:
-        """Internal tuning knob for k_encode_wire: 0 two-launch hybrid with the DPP per-packet copy
-        and the tag deferred into the copy loop for long frames (default), 1 per-packet, 2 flat, 3 one-launch
-        hybrid, 4-9 A/B variants (8 = the default with the tag in phase 1; list in rsk_kernels.hip)."""
-        fn = lib().rsk__set_wire_variant
-        fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        """A/B build only, as set_encode_variant, for k_encode_wire (tools/bench_paths.py)."""
+        fn = _ab_fn("rsk__set_wire_variant")
         _check(fn(self._ctx, v), "rsk__set_wire_variant")
 
     def set_send_seq_groupby(self, v: int) -> None:
@@ -271,8 +273,9 @@ class Codec:
         fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
         _check(fn(self._ctx, v), "rsk__set_send_seq_groupby")
 
-    def reserve(self, n_max: int) -> None:
-        _check(lib().rsk_reserve(self._ctx, n_max), "rsk_reserve")
+    def reserve(self, n_max: int, stream=None) -> None:
+        """Pre-size the compaction scratch of `stream` (default: torch's current stream)."""
+        _check(lib().rsk_reserve_stream(self._ctx, n_max, _stream(stream)), "rsk_reserve_stream")
 
     # ---- batch paths ---------------------------------------------------------------------
     def output_batch(self, payload, pay_off, pay_len, cmd, conv, conn_key, frame, frame_off, status,

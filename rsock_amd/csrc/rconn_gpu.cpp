@@ -135,13 +135,15 @@ void RConnGpu::free_slots() {
 // ---- send side -------------------------------------------------------------------------------
 int RConnGpu::Output(ssize_t nread, const char *base, const EncHeadFields &head, void *user) {
     if (nread < 0) return (int)nread;                                   // RConn.cpp:127
-    if (nread == 0) return reset_cb_ ? reset_cb_(user) : 0;             // RConn.cpp:119-123
     if (RSK_HEAD_SIZE + nread > RSK_MAX_PKT_SIZE) return RSK_SEND_OVERSIZE;  // RConn.cpp:94-98
     if (!ok_) return RSK_EDEVICE;
+    // nread == 0 is RConnReset::SendReset (RConn.cpp:119-123).  It is queued like a frame (the kernel
+    // gives it status RSK_SEND_RESET) so that deliver_enc fires the reset callback in input order,
+    // after the frames queued before it, as the reference's synchronous Output would.
     EncSlot &s = enc_[enc_cur_];
     const uint32_t i = s.count;
-    std::memcpy(s.frame + (size_t)i * kFramePitch + RSK_HEAD_SIZE, base, (size_t)nread);  // RConn.cpp:104
-    s.h_b0[i] = (uint8_t)base[0];
+    if (nread) std::memcpy(s.frame + (size_t)i * kFramePitch + RSK_HEAD_SIZE, base, (size_t)nread);  // RConn.cpp:104
+    s.h_b0[i] = nread ? (uint8_t)base[0] : 0;
     s.h_len[i] = (uint16_t)nread;
     s.h_cmd[i] = head.cmd;
     std::memcpy(s.h_id + 8 * (size_t)i, head.id, 8);
@@ -152,7 +154,7 @@ int RConnGpu::Output(ssize_t nread, const char *base, const EncHeadFields &head,
         const int r = rotate_enc();
         if (r) return r;
     }
-    return (int)(RSK_HEAD_SIZE + nread);
+    return nread == 0 ? 0 : (int)(RSK_HEAD_SIZE + nread);
 }
 
 int RConnGpu::launch_enc(EncSlot &s) {
@@ -186,6 +188,7 @@ int RConnGpu::deliver_enc(EncSlot &s) {
         char *f = reinterpret_cast<char *>(s.frame) + (size_t)i * kFramePitch;
         if (st > 0) std::memcpy(f, s.h_hdr + 32 * (size_t)i, RSK_HEAD_SIZE);  // tag | EncHead (RConn.cpp:101-103)
         if (st > 0 && send_cb_) send_cb_(f, st, s.user[i]);
+        if (st == RSK_SEND_RESET && reset_cb_) reset_cb_(s.user[i]);
         ++n_sent_;
     }
     s.count = 0;

@@ -4,9 +4,11 @@
 
 #include <hip/hip_runtime.h>
 
+#include <array>
 #include <cstdint>
 #include <cstdio>
 #include <mutex>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/rsk_codec.h"
@@ -14,23 +16,27 @@
 
 struct ShimIO;  // rsk_kernels.hip
 
+namespace rsk {
+// Device scratch of one kind for the calls ordered on one stream.
+enum WsKind { WS_COMPACT = 0, WS_SEQ = 1, WS_DEMUX = 2, WS_KINDS = 3 };
+struct WsBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+};
+}  // namespace rsk
+
 struct rsk_ctx {
     int device = 0;
-    int enc_variant = 0;   // see rsk__set_encode_variant
-    int wire_variant = 0;  // see rsk__set_wire_variant
+    int enc_variant = 0;   // see rsk__set_encode_variant (A/B build)
+    int wire_variant = 0;  // see rsk__set_wire_variant (A/B build)
     std::vector<uint8_t> key;
     rsk::KeySched ks;
-    // compaction workspace
-    void *ws = nullptr;
-    uint32_t ws_n = 0;
-    // connection-state workspace (rsk_tcp_send_seq_batch, rsk_demux.hip)
-    void *sq_ws = nullptr;
-    size_t sq_ws_bytes = 0;
+    // Scratch per stream (compaction masks/counts, send-seq tables, demux tables): calls on
+    // different streams never share scratch, calls on one stream are ordered by it (rsk_codec.h).
+    std::mutex ws_mu;
+    std::unordered_map<hipStream_t, std::array<rsk::WsBuf, rsk::WS_KINDS>> ws;
     bool sq_force_groupby = false;  // see rsk__set_send_seq_groupby
     int sq_scan_variant = 0;
-    // demux workspace (rsk_demux.hip)
-    void *dm_ws = nullptr;
-    size_t dm_ws_bytes = 0;
     // single-packet shim buffers
     ShimIO *shim_dev = nullptr;
     ShimIO *shim_host = nullptr;
@@ -73,5 +79,34 @@ struct DeviceGuard {
         if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
     }
 };
+
+// At least `need` bytes of `kind` scratch for stream s.  Growing waits for s to drain (the old
+// buffer may still be read by work queued on s) and then reallocates.
+inline int stream_ws(rsk_ctx *c, hipStream_t s, int kind, size_t need, void **out) {
+    std::lock_guard<std::mutex> lk(c->ws_mu);
+    WsBuf &b = c->ws[s][kind];
+    if (!b.p || b.bytes < need) {
+        if (b.p) {
+            hipError_t e = hipStreamSynchronize(s);
+            if (e != hipSuccess) { set_error("hipStreamSynchronize", e); return RSK_EDEVICE; }
+            (void)hipFree(b.p);
+            b.p = nullptr;
+            b.bytes = 0;
+        }
+        hipError_t e = hipMalloc(&b.p, need);
+        if (e != hipSuccess) { set_error("hipMalloc(workspace)", e); b.p = nullptr; return RSK_ENOMEM; }
+        b.bytes = need;
+    }
+    *out = b.p;
+    return RSK_OK;
+}
+
+inline void free_ws(rsk_ctx *c) {
+    std::lock_guard<std::mutex> lk(c->ws_mu);
+    for (auto &kv : c->ws)
+        for (WsBuf &b : kv.second)
+            if (b.p) (void)hipFree(b.p);
+    c->ws.clear();
+}
 
 }  // namespace rsk

@@ -568,22 +568,6 @@ size_t dm_layout(uint32_t n, uint8_t *base, DmWs *w) {
     return off;
 }
 
-int ensure_dm_ws(rsk_ctx *c, uint32_t n) {
-    const size_t need = dm_layout(n, nullptr, nullptr);
-    if (c->dm_ws && c->dm_ws_bytes >= need) return RSK_OK;
-    if (c->dm_ws) {
-        hipError_t e = hipDeviceSynchronize();
-        if (e != hipSuccess) { rsk::set_error("hipDeviceSynchronize", e); return RSK_EDEVICE; }
-        (void)hipFree(c->dm_ws);
-        c->dm_ws = nullptr;
-        c->dm_ws_bytes = 0;
-    }
-    hipError_t e = hipMalloc(&c->dm_ws, need);
-    if (e != hipSuccess) { rsk::set_error("hipMalloc(demux workspace)", e); return RSK_ENOMEM; }
-    c->dm_ws_bytes = need;
-    return RSK_OK;
-}
-
 }  // namespace
 
 extern "C" int rsk_demux_batch(rsk_ctx *c, uint32_t n, const rsk_demux_in *in, uint32_t fields,
@@ -607,10 +591,11 @@ extern "C" int rsk_demux_batch(rsk_ctx *c, uint32_t n, const rsk_demux_in *in, u
         if (e != hipSuccess) { rsk::set_error("hipMemsetAsync", e); return RSK_EDEVICE; }
         return RSK_OK;
     }
-    int r = ensure_dm_ws(c, n);
+    void *wsp = nullptr;
+    int r = rsk::stream_ws(c, s, rsk::WS_DEMUX, dm_layout(n, nullptr, nullptr), &wsp);
     if (r) return r;
     DmWs w;
-    dm_layout(n, static_cast<uint8_t *>(c->dm_ws), &w);
+    dm_layout(n, static_cast<uint8_t *>(wsp), &w);
     DmIn a;
     a.status = in->status;
     a.cmd = in->cmd;
@@ -1042,21 +1027,11 @@ extern "C" int rsk_tcp_send_seq_batch(rsk_ctx *c, uint32_t n, const uint32_t *co
     const bool table = n_conn + 1ull <= kSqCols && !c->sq_force_groupby;
     const uint32_t W = sqt_wave_tile(n_conn), nwt = (uint32_t)((n + (uint64_t)W - 1) / W);
     const size_t need = table ? 4ull * (nwt + 64ull + 1ull) * (n_conn + 1ull) : sq_layout(n, n_conn, nullptr, nullptr);
-    if (!c->sq_ws || c->sq_ws_bytes < need) {
-        if (c->sq_ws) {
-            hipError_t e = hipDeviceSynchronize();
-            if (e != hipSuccess) { rsk::set_error("hipDeviceSynchronize", e); return RSK_EDEVICE; }
-            (void)hipFree(c->sq_ws);
-            c->sq_ws = nullptr;
-            c->sq_ws_bytes = 0;
-        }
-        hipError_t e = hipMalloc(&c->sq_ws, need);
-        if (e != hipSuccess) { rsk::set_error("hipMalloc(seq workspace)", e); return RSK_ENOMEM; }
-        c->sq_ws_bytes = need;
-    }
-    int r;
+    void *sq_ws = nullptr;
+    int r = rsk::stream_ws(c, s, rsk::WS_SEQ, need, &sq_ws);
+    if (r) return r;
     if (table) {
-        uint32_t *tab = static_cast<uint32_t *>(c->sq_ws);
+        uint32_t *tab = static_cast<uint32_t *>(sq_ws);
         const unsigned nbt = (nwt + kWaves - 1) / kWaves;
         const size_t lds = 4ull * kWaves * (n_conn + 1ull);
         hipLaunchKernelGGL(k_sqt_sum, dim3(nbt), dim3(kBlock), lds, s, conn, status, n, n_conn, W, nwt, tab);
@@ -1080,7 +1055,7 @@ extern "C" int rsk_tcp_send_seq_batch(rsk_ctx *c, uint32_t n, const uint32_t *co
         return rsk::launch_check("k_sqt_apply");
     }
     SqWs w;
-    sq_layout(n, n_conn, static_cast<uint8_t *>(c->sq_ws), &w);
+    sq_layout(n, n_conn, static_cast<uint8_t *>(sq_ws), &w);
     const unsigned nb = (n + kBlock - 1) / kBlock, nb1 = (n + 1 + kBlock - 1) / kBlock;
     hipError_t e = hipMemsetAsync(seq, 0, 4ull * n, s);
     if (e != hipSuccess) { rsk::set_error("hipMemsetAsync(seq)", e); return RSK_EDEVICE; }
@@ -1122,6 +1097,7 @@ extern "C" int rsk_tcp_recv_ack_batch(rsk_ctx *c, uint32_t n, const uint32_t *co
     if (!c) return RSK_EINVAL;
     if (n == 0) return RSK_OK;
     if (!conn || !delivered || !seq || (n_conn && !conn_ack)) return RSK_EINVAL;
+    if (n > (1u << 30)) return RSK_EINVAL;  // as rsk_tcp_send_seq_batch: 32-bit grid arithmetic stays exact
     rsk::DeviceGuard g(c->device);
     if (!g.ok) return RSK_EDEVICE;
     if (n_conn <= kAckLds)

@@ -2017,26 +2017,16 @@ size_t ws_bytes(uint32_t n) {
     return nb * kWavesPerBlock * sizeof(uint64_t) + 2 * nb * sizeof(uint32_t) + 256;
 }
 
-int ensure_ws(rsk_ctx *c, uint32_t n) {
-    if (n <= c->ws_n && c->ws) return RSK_OK;
-    if (c->ws) {
-        hipError_t e = hipDeviceSynchronize();
-        if (e != hipSuccess) { set_error("hipDeviceSynchronize", e); return RSK_EDEVICE; }
-        (void)hipFree(c->ws);
-        c->ws = nullptr;
-        c->ws_n = 0;
-    }
-    hipError_t e = hipMalloc(&c->ws, ws_bytes(n));
-    if (e != hipSuccess) { set_error("hipMalloc(workspace)", e); return RSK_ENOMEM; }
-    c->ws_n = n;
-    return RSK_OK;
-}
-
-void ws_split(rsk_ctx *c, uint32_t n, uint64_t *&masks, uint32_t *&counts, uint32_t *&offsets) {
+// compaction scratch of stream s for n packets: masks | counts | offsets
+int ensure_ws(rsk_ctx *c, uint32_t n, hipStream_t s, uint64_t *&masks, uint32_t *&counts, uint32_t *&offsets) {
+    void *p = nullptr;
+    int r = rsk::stream_ws(c, s, rsk::WS_COMPACT, ws_bytes(n), &p);
+    if (r) return r;
     const uint64_t nb = (n + kBlock - 1ull) / kBlock;
-    masks = reinterpret_cast<uint64_t *>(c->ws);
+    masks = reinterpret_cast<uint64_t *>(p);
     counts = reinterpret_cast<uint32_t *>(masks + nb * kWavesPerBlock);
     offsets = counts + nb;
+    return RSK_OK;
 }
 
 int run_compaction(rsk_ctx *c, uint32_t n, uint64_t *masks, uint32_t *counts, uint32_t *offsets,
@@ -2096,6 +2086,7 @@ const char *rsk_last_error(void) { return g_last_error; }
 
 const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 
+#ifdef RSK_AB
 // Internal tuning knob (not part of include/rsk_codec.h): selects the encode kernel variant for
 // in-process A/B measurements.  k_encode<MODE, PU, U, NT>: MODE 0 per-packet, 1 flat, 2 hybrid,
 // 3 hybrid with the one-load DPP per-packet copy, 4 DPP per-packet only; PU packets per per-packet
@@ -2129,6 +2120,7 @@ int rsk__set_wire_variant(rsk_ctx *c, int v) {
     c->wire_variant = v;
     return RSK_OK;
 }
+#endif  // RSK_AB
 
 rsk_ctx *rsk_create(const uint8_t *key, uint32_t key_len, int device) {
     if (!key && key_len) { snprintf(g_last_error, sizeof g_last_error, "rsk_create: null key"); return nullptr; }
@@ -2152,20 +2144,22 @@ rsk_ctx *rsk_create(const uint8_t *key, uint32_t key_len, int device) {
 void rsk_destroy(rsk_ctx *c) {
     if (!c) return;
     DeviceGuard g(c->device);
-    if (c->ws) (void)hipFree(c->ws);
-    if (c->dm_ws) (void)hipFree(c->dm_ws);
-    if (c->sq_ws) (void)hipFree(c->sq_ws);
+    rsk::free_ws(c);
     if (c->shim_dev) (void)hipFree(c->shim_dev);
     if (c->shim_host) (void)hipHostFree(c->shim_host);
     if (c->shim_stream) (void)hipStreamDestroy(c->shim_stream);
     delete c;
 }
 
-int rsk_reserve(rsk_ctx *c, uint32_t n_max) {
+int rsk_reserve(rsk_ctx *c, uint32_t n_max) { return rsk_reserve_stream(c, n_max, nullptr); }
+
+int rsk_reserve_stream(rsk_ctx *c, uint32_t n_max, void *stream) {
     if (!c) return RSK_EINVAL;
     DeviceGuard g(c->device);
     if (!g.ok) return RSK_EDEVICE;
-    return ensure_ws(c, n_max);
+    uint64_t *m;
+    uint32_t *cn, *o;
+    return ensure_ws(c, n_max, (hipStream_t)stream, m, cn, o);
 }
 
 int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_encode_out *out,
@@ -2190,7 +2184,9 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
     const unsigned grid = (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
     hipStream_t st = (hipStream_t)stream;
     const dim3 gd(grid), bd(kBlock);
-    // A/B only: variant + 100 * cap limits residency to `cap` blocks per CU through unused dynamic LDS
+#ifdef RSK_AB
+    // A/B build only (make -C rsock_amd ab -> librsk_ab.so, tools/): variant + 100 * cap limits
+    // residency to `cap` blocks per CU through unused dynamic LDS
     const int cap = c->enc_variant / 100;
     const size_t lds = cap ? (size_t)(163840 / cap) - 16384 : 0;
     switch (c->enc_variant % 100) {
@@ -2224,6 +2220,12 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         case 12: hipLaunchKernelGGL((k_encode_blk<2>), gd, bd, 0, st, a, c->ks); break;
         default: hipLaunchKernelGGL((k_encode<6, 12, 4, -1>), gd, bd, lds, st, a, c->ks); break;
     }
+#else
+    // the shipped kernel: per-wave hybrid (flat chunk list for short frames, one-load DPP per-packet
+    // copy with 12 packets per iteration for the rest), tag in the copy loop for long-frame sets,
+    // per-set store policy
+    hipLaunchKernelGGL((k_encode<6, 12, 4, -1>), gd, bd, 0, st, a, c->ks);
+#endif
     return launch_check("k_encode");
 }
 
@@ -2257,6 +2259,7 @@ int rsk_encode_wire_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const
     const hipStream_t st = (hipStream_t)stream;
 #define RSK_WIRE(E, M, PU, U) hipLaunchKernelGGL((k_encode_wire<E, M, PU, U>), dim3(grid), dim3(kBlock), 0, st, a, w, c->ks)
 #define RSK_WIRE4(E, M, PU, U) hipLaunchKernelGGL((k_encode_wire_w4<E, M, PU, U>), dim3(grid), dim3(kBlock), 0, st, a, w, c->ks)
+#ifdef RSK_AB
     const int v = c->wire_variant;
     if (wire->with_eth) {
         if (v == 1) RSK_WIRE(14, 0, 2, 4);
@@ -2281,6 +2284,12 @@ int rsk_encode_wire_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const
         else if (v == 9) { RSK_WIRE(0, 5, 108, 2); RSK_WIRE(0, 4, 2, 2); }
         else { RSK_WIRE4(0, 5, 108, 2); RSK_WIRE(0, 4, 2, 2); }
     }
+#else
+    // the shipped kernels: per-packet half (DPP copy, 8 packets per iteration, tag + payload prefix in
+    // the copy loop for long-frame sets, 4 waves/SIMD) then the flat half
+    if (wire->with_eth) { RSK_WIRE4(14, 5, 108, 2); RSK_WIRE(14, 4, 2, 2); }
+    else { RSK_WIRE4(0, 5, 108, 2); RSK_WIRE(0, 4, 2, 2); }
+#endif
 #undef RSK_WIRE
 #undef RSK_WIRE4
     return launch_check("k_encode_wire");
@@ -2298,9 +2307,8 @@ int rsk_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *frame_arena, const u
     uint64_t *masks = nullptr;
     uint32_t *counts = nullptr, *offsets = nullptr;
     if (compact) {
-        int r = ensure_ws(c, n);
+        int r = ensure_ws(c, n, (hipStream_t)stream, masks, counts, offsets);
         if (r) return r;
-        ws_split(c, n, masks, counts, offsets);
     }
     DecArgs a{frame_arena, frame_off, frame_len, is_tcp_close, n};
     DecOut d = make_dec_out(out, masks, counts);
@@ -2341,9 +2349,8 @@ int rsk_decode_headers_batch(rsk_ctx *c, uint32_t n, const uint8_t *hdr, const u
     uint64_t *masks = nullptr;
     uint32_t *counts = nullptr, *offsets = nullptr;
     if (compact) {
-        int r = ensure_ws(c, n);
+        int r = ensure_ws(c, n, (hipStream_t)stream, masks, counts, offsets);
         if (r) return r;
-        ws_split(c, n, masks, counts, offsets);
     }
     DecArgs a{hdr, nullptr, frame_len, is_tcp_close, n};
     DecOut d = make_dec_out(out, masks, counts);
@@ -2382,9 +2389,8 @@ int parse_decode(rsk_ctx *c, uint32_t n, const uint8_t *cap_arena, const uint64_
     uint64_t *masks = nullptr;
     uint32_t *counts = nullptr, *offsets = nullptr;
     if (compact) {
-        int r = ensure_ws(c, n);
+        int r = ensure_ws(c, n, (hipStream_t)stream, masks, counts, offsets);
         if (r) return r;
-        ws_split(c, n, masks, counts, offsets);
     }
     ParseArgs a;
     a.cap = cap_arena; a.cap_off = cap_off; a.wire_len = wire_len; a.cap_len = cap_len;
@@ -2437,9 +2443,8 @@ int rsk_syncinput_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *rec_arena,
     uint64_t *masks = nullptr;
     uint32_t *counts = nullptr, *offsets = nullptr;
     if (compact) {
-        int r = ensure_ws(c, n);
+        int r = ensure_ws(c, n, (hipStream_t)stream, masks, counts, offsets);
         if (r) return r;
-        ws_split(c, n, masks, counts, offsets);
     }
     SyncArgs a;
     a.rec = rec_arena; a.rec_off = rec_off; a.nread = nread;
@@ -2471,9 +2476,8 @@ int rsk_filter_parse_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *cap_are
     uint64_t *masks = nullptr;
     uint32_t *counts = nullptr, *offsets = nullptr;
     if (compact) {
-        int r = ensure_ws(c, n);
+        int r = ensure_ws(c, n, (hipStream_t)stream, masks, counts, offsets);
         if (r) return r;
-        ws_split(c, n, masks, counts, offsets);
     }
     ParseArgs a;
     a.cap = cap_arena; a.cap_off = cap_off; a.wire_len = wire_len; a.cap_len = cap_len;
@@ -2504,9 +2508,8 @@ int rsk_capture_filter_batch(rsk_ctx *c, uint32_t n, const uint8_t *cap_arena, c
     uint64_t *masks = nullptr;
     uint32_t *counts = nullptr, *offsets = nullptr;
     if (compact) {
-        int r = ensure_ws(c, n);
+        int r = ensure_ws(c, n, (hipStream_t)stream, masks, counts, offsets);
         if (r) return r;
-        ws_split(c, n, masks, counts, offsets);
     }
     FiltArgs a;
     a.cap = cap_arena; a.cap_off = cap_off; a.cap_len = cap_len; a.match = match; a.n = n;

@@ -18,9 +18,10 @@ class Adapter:
         self.L = _abi.load()
         self.r = self.L.rsk_rconn_create(KEY, len(KEY), 0, batch)
         assert self.r, self.L.rsk_last_error()
-        self.sent, self.resets, self.recvd = [], [], []
-        self._send = _abi.SEND_FN(lambda f, n, u, a: (self.sent.append((ctypes.string_at(f, n), u)), 0)[1])
-        self._reset = _abi.RESET_FN(lambda u, a: (self.resets.append(u), 7)[1])
+        self.sent, self.resets, self.recvd, self.events = [], [], [], []
+        self._send = _abi.SEND_FN(lambda f, n, u, a: (self.sent.append((ctypes.string_at(f, n), u)),
+                                                      self.events.append(("send", u)), 0)[2])
+        self._reset = _abi.RESET_FN(lambda u, a: (self.resets.append(u), self.events.append(("reset", u)), 7)[2])
 
         def recv(st, hlen, cmd, idp, conv, key, pay, plen, u, a):
             rec = (st, u)
@@ -45,16 +46,20 @@ def test_adapter_output_onrecv(gpu, oracle, batch):
     try:
         pkts = []
         lens = [0, 1, 1469, 1470, 5000] + list(rng.integers(1, 1470, 300))
+        lens[40:40] = [0]  # a reset in the middle of a batch (and at a batch edge for batch 37)
+        lens[74:74] = [0, 0]
         for k, ln in enumerate(lens):
             p = rng.integers(0, 256, int(ln), dtype=np.uint8).tobytes()
             fields = (int(rng.integers(0, 5)), rng.integers(0, 256, 8, dtype=np.uint8).tobytes(),
                       int(rng.integers(0, 2**32)), int(rng.integers(0, 2**63)))
             r = ad.L.rsk_rconn_output(ad.r, len(p), p, fields[0], fields[1], fields[2], fields[3], k + 1)
-            exp = 7 if ln == 0 else (-1 if ln + 31 > 1500 else ln + 31)  # reset cb returns 7
+            exp = 0 if ln == 0 else (-1 if ln + 31 > 1500 else ln + 31)  # resets are queued: 0
             assert r == exp, (ln, r)
             pkts.append((p, fields, k + 1))
         assert ad.L.rsk_rconn_flush(ad.r) == 0
-        assert ad.resets == [1]
+        assert ad.resets == [u for p, _, u in pkts if len(p) == 0] and len(ad.resets) == 4
+        # send and reset callbacks interleave in input order (RConn::Output is synchronous)
+        assert ad.events == [("reset" if len(p) == 0 else "send", u) for p, _, u in pkts if len(p) <= 1469]
         framed = [(p, f, u) for p, f, u in pkts if 0 < len(p) <= 1469]
         assert [u for _, u in ad.sent] == [u for _, _, u in framed]  # input order
         for (frame, _), (p, f, u) in zip(ad.sent, framed):

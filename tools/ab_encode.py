@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """In-process A/B of encode-kernel variants (interleaved rounds in ONE process, guide §5.4 rule 24).
-   python tools/ab_encode.py [--config c3] [--rounds 10] [--reps 10] [--variants 0,1,2,3]
-Prints per-variant median/min k_encode ms and algorithmic GB/s, and checks every variant's frame
+   make -C rsock_amd ab && python tools/ab_encode.py [--config c3] [--rounds 10] [--reps 10] [--variants 0,1,2,3]
+Runs on the A/B build of the library (rsock_amd/librsk_ab.so, selected here through RSK_LIB).  Prints per-variant median/min k_encode ms and algorithmic GB/s, and checks every variant's frame
 arena is byte-identical to variant 1's."""
 import argparse
 import json
@@ -11,6 +11,7 @@ import sys
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("RSK_LIB", "librsk_ab.so")
 
 
 def main():

@@ -61,19 +61,12 @@ def main():
         "encode_wire_eth": lambda: cx.output_wire_batch(*common, src, dst, sp, dp, seq, ack, flag, ipid, wiree, offe,
                                                         ste, eth=eth, id_uniform=workload.ID_UNIFORM, pad16=True,
                                                         stream=s),
-        "encode_wire_raw4_pkt": lambda: (cx.set_wire_variant(1), cx.output_wire_batch(
-            *common, src, dst, sp, dp, seq, ack, flag, ipid, wire4, off4, st4, id_uniform=workload.ID_UNIFORM,
-            pad16=True, stream=s), cx.set_wire_variant(0)),
-        "encode_wire_raw4_flat": lambda: (cx.set_wire_variant(2), cx.output_wire_batch(
-            *common, src, dst, sp, dp, seq, ack, flag, ipid, wire4, off4, st4, id_uniform=workload.ID_UNIFORM,
-            pad16=True, stream=s), cx.set_wire_variant(0)),
-        "encode_wire_raw4_hyb1": lambda: (cx.set_wire_variant(3), cx.output_wire_batch(
-            *common, src, dst, sp, dp, seq, ack, flag, ipid, wire4, off4, st4, id_uniform=workload.ID_UNIFORM,
-            pad16=True, stream=s), cx.set_wire_variant(0)),
         "decode": lambda: cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, w.dec, stream=s),
         "parse_decode": lambda: cx.rawinput_batch(wiree, offe, ste, ste, 1, 0, tcp, pdec, stream=s),
     }
-    for v in [int(x) for x in args.wire_variants.split(",") if x]:
+    # the A/B build (RSK_LIB=librsk_ab.so) exposes the wire variants: 1 per-packet, 2 flat, 3 one-launch
+    ab = os.environ.get("RSK_LIB", "") == "librsk_ab.so"
+    for v in ([1, 2, 3] if ab else []) + [int(x) for x in args.wire_variants.split(",") if x]:
         ops[f"encode_wire_raw4_v{v}"] = (lambda v=v: (cx.set_wire_variant(v), cx.output_wire_batch(
             *common, src, dst, sp, dp, seq, ack, flag, ipid, wire4, off4, st4, id_uniform=workload.ID_UNIFORM,
             pad16=True, stream=s), cx.set_wire_variant(0)))
