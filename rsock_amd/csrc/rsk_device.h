@@ -49,22 +49,55 @@ __device__ __forceinline__ uint4 funnel16(const uint4 &A, const uint4 &B, uint32
     return o;
 }
 
-// Store bytes [0, lim) of v at p (p 16-byte aligned, 0 < lim < 16): dword stores for whole
-// dwords, byte stores for the tail.  Neighbouring frames may own the rest of the 16-B chunk.
-__device__ __forceinline__ void store_partial16(uint8_t *p, const uint4 &v, int lim) {
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+// Store bytes [lo, hi) of the 16-byte chunk v at p (16-byte aligned, 0 <= lo < hi <= 16) with the
+// fewest stores: a byte and a short up to the first dword boundary, one dword / dwordx2 / dwordx3 /
+// dwordx4 for the whole dwords, then a short and a byte.  Neighbouring frames may own the rest of
+// the 16-B chunk, so nothing outside [lo, hi) is written.  lo / hi may be per lane.
+__device__ __forceinline__ uint32_t word_at(const uint4 &v, uint32_t d) {
+    // dword d (0..3) as AND/OR of masks: a select chain on a per-lane index is turned into a
+    // dynamic vector extract, which the backend lowers through scratch memory
+    auto m = [d](uint32_t i) { return (uint32_t)((int32_t)((d ^ i) - 1u) >> 31); };
+    return (v.x & m(0)) | (v.y & m(1)) | (v.z & m(2)) | (v.w & m(3));
+}
+__device__ __forceinline__ void store_range16(uint8_t *p, const uint4 &v, uint32_t lo, uint32_t hi) {
     RSK_GLOBAL uint8_t *g = gptr(p);
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-        const int lo = 4 * d;
-        if (lo + 4 <= lim) {
-            *reinterpret_cast<RSK_GLOBAL uint32_t *>(g + lo) = w[d];
-        } else if (lo < lim) {
-#pragma unroll
-            for (int b = 0; b < 3; ++b)
-                if (lo + b < lim) g[lo + b] = (uint8_t)(w[d] >> (8 * b));
-        }
+    uint32_t x = lo;
+    if ((x & 1u) && x < hi) {
+        g[x] = (uint8_t)(word_at(v, x >> 2) >> (8u * (x & 3u)));
+        x += 1u;
     }
+    if ((x & 2u) && x + 2u <= hi) {
+        *reinterpret_cast<RSK_GLOBAL uint16_t *>(g + x) = (uint16_t)(word_at(v, x >> 2) >> 16);
+        x += 2u;
+    }
+    const uint32_t nd = x < hi ? (hi - x) >> 2 : 0u;  // x is a multiple of 4 here when nd > 0
+    const uint32_t d = x >> 2;
+    typedef uint32_t v2 __attribute__((ext_vector_type(2)));
+    typedef uint32_t v3 __attribute__((ext_vector_type(3)));
+    typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+    if (nd == 4u) {
+        const v4 q = {v.x, v.y, v.z, v.w};
+        *reinterpret_cast<RSK_GLOBAL v4 *>(g) = q;
+    } else if (nd == 3u) {
+        const v3 q = {word_at(v, d), word_at(v, d + 1u), word_at(v, d + 2u)};
+        *reinterpret_cast<RSK_GLOBAL v3 *>(g + x) = q;
+    } else if (nd == 2u) {
+        const v2 q = {word_at(v, d), word_at(v, d + 1u)};
+        *reinterpret_cast<RSK_GLOBAL v2 *>(g + x) = q;
+    } else if (nd == 1u) {
+        *reinterpret_cast<RSK_GLOBAL uint32_t *>(g + x) = word_at(v, d);
+    }
+    x += 4u * nd;
+    if (x + 2u <= hi) {
+        *reinterpret_cast<RSK_GLOBAL uint16_t *>(g + x) = (uint16_t)(word_at(v, x >> 2) >> (8u * (x & 3u)));
+        x += 2u;
+    }
+    if (x < hi) g[x] = (uint8_t)(word_at(v, x >> 2) >> (8u * (x & 3u)));
+}
+
+// Store bytes [0, lim) of v at p (16-byte aligned, 0 < lim < 16).
+__device__ __forceinline__ void store_partial16(uint8_t *p, const uint4 &v, int lim) {
+    store_range16(p, v, 0u, (uint32_t)lim);
 }
 
 // v with bytes [lim, 16) cleared (0 < lim < 16)

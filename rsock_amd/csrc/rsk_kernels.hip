@@ -167,216 +167,13 @@ __device__ __forceinline__ uint32_t padded_len(const uint8_t *d, uint32_t flen, 
     return flen + ((m + 1u - ((uint32_t)(reinterpret_cast<uintptr_t>(d) + flen) & m)) & m);
 }
 
-// ---- per-packet copy: the wave streams the frames of the packets in `vm` (16-B aligned), PU
-// packets per iteration.  A frame has at most 94 16-B chunks (1500 B), so chunk slots
-// k = lane and k = lane + 64 cover it; all PU x 2 slots' loads are issued before any store. -------
-template <int PU, int NT>
-__device__ __forceinline__ void copy_pkt(const EncArgs &a, const Lane1 &L, uint32_t lane, uint64_t vm) {
-    while (vm) {
-        uint32_t js[PU];
-        bool on[PU];
-#pragma unroll
-        for (int p = 0; p < PU; ++p) {
-            on[p] = vm != 0ull;
-            js[p] = on[p] ? (uint32_t)__builtin_ctzll(vm) : 0u;
-            if (on[p]) vm &= vm - 1ull;
-        }
-        uint4 A[PU][2], B[PU][2];
-        const uint8_t *srcp[PU];
-        uint8_t *dstp[PU];
-        uint32_t flen[PU], sh[PU];
-        int32_t last_rel[PU];
-#pragma unroll
-        for (int p = 0; p < PU; ++p) {
-            flen[p] = on[p] ? rdl((uint32_t)L.st, js[p]) : 0u;
-            const uint8_t *src = a.payload + rdl64(L.po, js[p]);
-            dstp[p] = a.frame + rdl64(L.fo, js[p]);
-            sh[p] = (uint32_t)((reinterpret_cast<uintptr_t>(src) + 1u) & 15u);
-            srcp[p] = src + 1 - sh[p];  // chunk k >= 2 = payload bytes [16k-31, 16k-15)
-            last_rel[p] = (int32_t)flen[p] - RSK_HEAD_SIZE + (int32_t)sh[p] - 2;
-            const uint32_t nch = (flen[p] + 15u) >> 4;  // chunks holding frame bytes (loads)
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const uint32_t k = lane + 64u * q;
-                A[p][q] = make_uint4(0u, 0u, 0u, 0u);
-                B[p][q] = make_uint4(0u, 0u, 0u, 0u);
-                if (k >= 2u && k < nch) {
-                    const uint32_t ro = 16u * (k - 2u);
-                    A[p][q] = ld16<NT>(srcp[p] + ro);
-                    if (sh[p] != 0u && (int32_t)(ro + 16u) <= last_rel[p]) B[p][q] = ld16<NT>(srcp[p] + ro + 16u);
-                }
-            }
-        }
-#pragma unroll
-        for (int p = 0; p < PU; ++p) {
-            if (!on[p]) continue;
-            const uint32_t nch = (padded_len(dstp[p], flen[p], a.pad) + 15u) >> 4;  // chunks stored
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const uint32_t k = lane + 64u * q;
-                if (k >= nch) continue;
-                uint4 v;
-                if (k >= 2u) {
-                    v = rsk::funnel16(A[p][q], B[p][q], sh[p]);
-                } else {
-                    uint32_t Hj[8];  // uniform: readlane every word, then select per lane
-#pragma unroll
-                    for (int t = 0; t < 8; ++t) Hj[t] = rdl(L.H[t], js[p]);
-                    v = k == 0u ? make_uint4(Hj[0], Hj[1], Hj[2], Hj[3]) : make_uint4(Hj[4], Hj[5], Hj[6], Hj[7]);
-                }
-                store_last16<NT>(dstp[p] + 16u * k, v, (int)flen[p] - 16 * (int)k, a.pad != 0u);
-            }
-        }
-    }
-}
-
-// ---- per-packet copy, one load per chunk: lane k loads aligned source chunk k - 2 and takes the
-// second funnel operand (chunk k - 1) from lane k + 1 by a DPP wave shift (lane 63 of slot 0 from
-// lane 0 of slot 1), so a packet holds 2 instead of 4 uint4 registers per lane and more waves fit
-// per SIMD.  The shifts run with every lane active (DPP reads disabled lanes as 0). -------------
-__device__ __forceinline__ uint32_t wave_shl1(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false);  // wave_shl:1
-}
-
-template <int PU, int NT>
-__device__ __forceinline__ void copy_pkt_dpp(const EncArgs &a, const Lane1 &L, uint32_t lane, uint64_t vm) {
-    while (vm) {
-        uint32_t js[PU];
-        bool on[PU];
-#pragma unroll
-        for (int p = 0; p < PU; ++p) {
-            on[p] = vm != 0ull;
-            js[p] = on[p] ? (uint32_t)__builtin_ctzll(vm) : 0u;
-            if (on[p]) vm &= vm - 1ull;
-        }
-        uint4 A[PU][2];
-        uint8_t *dstp[PU];
-        uint32_t flen[PU], sh[PU];
-#pragma unroll
-        for (int p = 0; p < PU; ++p) {
-            flen[p] = on[p] ? rdl((uint32_t)L.st, js[p]) : 0u;
-            const uint8_t *src = a.payload + rdl64(L.po, js[p]);
-            dstp[p] = a.frame + rdl64(L.fo, js[p]);
-            sh[p] = (uint32_t)((reinterpret_cast<uintptr_t>(src) + 1u) & 15u);
-            const uint8_t *srcp = src + 1 - sh[p];  // aligned source chunk m = payload bytes around [16m-sh+1, ...)
-            const int32_t last_rel = (int32_t)flen[p] - RSK_HEAD_SIZE + (int32_t)sh[p] - 2;
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const uint32_t k = lane + 64u * q;
-                A[p][q] = make_uint4(0u, 0u, 0u, 0u);
-                if (on[p] && k >= 2u && (int32_t)(16u * (k - 2u)) <= last_rel) A[p][q] = ld16<NT>(srcp + 16u * (k - 2u));
-            }
-        }
-#pragma unroll
-        for (int p = 0; p < PU; ++p) {
-            if (!on[p]) continue;
-            uint4 B[2];
-            B[0] = make_uint4(wave_shl1(A[p][0].x), wave_shl1(A[p][0].y), wave_shl1(A[p][0].z), wave_shl1(A[p][0].w));
-            B[1] = make_uint4(wave_shl1(A[p][1].x), wave_shl1(A[p][1].y), wave_shl1(A[p][1].z), wave_shl1(A[p][1].w));
-            const uint4 l0 = make_uint4(rdl(A[p][1].x, 0), rdl(A[p][1].y, 0), rdl(A[p][1].z, 0),
-                                        rdl(A[p][1].w, 0));  // read in uniform flow (see k_encode)
-            if (lane == 63u) B[0] = l0;
-            uint32_t Hj[8];  // packet's head words, read out in uniform control flow (SGPRs)
-#pragma unroll
-            for (int t = 0; t < 8; ++t) Hj[t] = rdl(L.H[t], js[p]);
-            const uint32_t nch = (padded_len(dstp[p], flen[p], a.pad) + 15u) >> 4;  // chunks stored
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const uint32_t k = lane + 64u * q;
-                if (k >= nch) continue;
-                uint4 v;
-                if (k >= 2u) v = rsk::funnel16(A[p][q], B[q], sh[p]);
-                else v = k == 0u ? make_uint4(Hj[0], Hj[1], Hj[2], Hj[3]) : make_uint4(Hj[4], Hj[5], Hj[6], Hj[7]);
-                store_last16<NT>(dstp[p] + 16u * k, v, (int)flen[p] - 16 * (int)k, a.pad != 0u);
-            }
-        }
-    }
-}
-
-// ---- copy_pkt_dpp with the tag computed in the copy loop (MODE 6): phase 1 skipped payload[0] and
-// the MD5, because its byte load fetches the payload's first line well before the copy reaches the
-// packet, and the line is gone from L2 by then (~128 B of extra HBM reads per packet, the excess
-// FETCH_SIZE shows).  Here lane p loads payload[0] of the iteration's packet p first, then the
-// chunks; the MD5 of the PU packets runs while the chunk loads are in flight, and the byte load
-// hits the lines those loads are fetching anyway. ------------------------------------------------
-template <int PU, int NT>
-__device__ __forceinline__ void copy_pkt_dpp_tag(const EncArgs &a, const KeySched &ks, const Lane1 &L, uint32_t lane,
-                                                 uint64_t vm) {
-    while (vm) {
-        uint32_t js[PU];
-        bool on[PU];
-#pragma unroll
-        for (int p = 0; p < PU; ++p) {
-            on[p] = vm != 0ull;
-            js[p] = on[p] ? (uint32_t)__builtin_ctzll(vm) : 0u;
-            if (on[p]) vm &= vm - 1ull;
-        }
-        // lane p: payload[0] of packet p (issued before the chunk loads)
-        uint32_t my_b0 = 0;
-#pragma unroll
-        for (int p = 0; p < PU; ++p)
-            if (on[p] && lane == (uint32_t)p) my_b0 = rsk::gptr(a.payload)[rdl64(L.po, js[p])];
-        uint4 A[PU][2];
-        uint8_t *dstp[PU];
-        uint32_t flen[PU], sh[PU];
-#pragma unroll
-        for (int p = 0; p < PU; ++p) {
-            flen[p] = on[p] ? rdl((uint32_t)L.st, js[p]) : 0u;
-            const uint8_t *src = a.payload + rdl64(L.po, js[p]);
-            dstp[p] = a.frame + rdl64(L.fo, js[p]);
-            sh[p] = (uint32_t)((reinterpret_cast<uintptr_t>(src) + 1u) & 15u);
-            const uint8_t *srcp = src + 1 - sh[p];
-            const int32_t last_rel = (int32_t)flen[p] - RSK_HEAD_SIZE + (int32_t)sh[p] - 2;
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const uint32_t k = lane + 64u * q;
-                A[p][q] = make_uint4(0u, 0u, 0u, 0u);
-                if (on[p] && k >= 2u && (int32_t)(16u * (k - 2u)) <= last_rel) A[p][q] = ld16<NT>(srcp + 16u * (k - 2u));
-            }
-        }
-        uint32_t t0, t1;  // lane p: tag of packet p
-        rsk::md5_tag(ks, my_b0, t0, t1);
-#pragma unroll
-        for (int p = 0; p < PU; ++p) {
-            if (!on[p]) continue;
-            uint4 B[2];
-            B[0] = make_uint4(wave_shl1(A[p][0].x), wave_shl1(A[p][0].y), wave_shl1(A[p][0].z), wave_shl1(A[p][0].w));
-            B[1] = make_uint4(wave_shl1(A[p][1].x), wave_shl1(A[p][1].y), wave_shl1(A[p][1].z), wave_shl1(A[p][1].w));
-            const uint4 l0 = make_uint4(rdl(A[p][1].x, 0), rdl(A[p][1].y, 0), rdl(A[p][1].z, 0),
-                                        rdl(A[p][1].w, 0));  // read in uniform flow (see k_encode)
-            if (lane == 63u) B[0] = l0;
-            uint32_t Hj[8];  // packet's head words, read out in uniform control flow (SGPRs)
-#pragma unroll
-            for (int t = 2; t < 8; ++t) Hj[t] = rdl(L.H[t], js[p]);
-            Hj[0] = rdl(t0, (uint32_t)p);
-            Hj[1] = rdl(t1, (uint32_t)p);
-            Hj[7] |= rdl(my_b0, (uint32_t)p) << 24;
-            const uint32_t nch = (padded_len(dstp[p], flen[p], a.pad) + 15u) >> 4;  // chunks stored
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const uint32_t k = lane + 64u * q;
-                if (k >= nch) continue;
-                uint4 v;
-                if (k >= 2u) v = rsk::funnel16(A[p][q], B[q], sh[p]);
-                else v = k == 0u ? make_uint4(Hj[0], Hj[1], Hj[2], Hj[3]) : make_uint4(Hj[4], Hj[5], Hj[6], Hj[7]);
-                store_last16<NT>(dstp[p] + 16u * k, v, (int)flen[p] - 16 * (int)k, a.pad != 0u);
-            }
-        }
-    }
-}
-
-// ---- flat copy: the payload chunks (k >= 2) of every packet in `vm` as one list of 16-B chunks;
-// lane l of iteration t takes chunk g = 64(U t + u) + l and finds its packet by a 6-step binary
-// search over the tile's prefix sums in this wave's LDS slice.  Chunks 0 and 1 (frame bytes
-// [0, 32): tag, EncHead, payload[0]) are stored by the packet's own lane.  Wave-local: no block
-// barrier, so waves of one block may take different copy paths. --------------------------------
 struct alignas(16) CopyRec {
-    const uint8_t *src_al;  // 16-B aligned source of chunk 2 (payload + 1 - sh)
-    uint8_t *dst;           // frame start (16-B aligned)
-    uint32_t cstart;        // first flat chunk index of this packet within the tile
-    uint32_t sh;            // funnel shift: (payload + 1) mod 16
+    const uint8_t *src_al;  // 16-B aligned source of chunk 2 (payload + 1 - sh; wire: its own base)
+    uint8_t *dst;           // 16-B aligned destination of chunk 0
+    uint32_t cstart;        // first flat chunk index of this packet within the set
+    uint32_t sh;            // funnel shift (bits 0-3) | frame offset r << 4 (encode)
     int32_t last_rel;       // last payload byte, relative to src_al
-    uint32_t flen;          // 31 + P
+    uint32_t flen;          // frame length (31 + P)
 };
 
 // 16 bytes at byte offset sh (0..15, per lane) of A||B, branch-free
@@ -404,27 +201,221 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int U, int NT>
+// ---- frame geometry: any destination alignment ---------------------------------------------------
+// A frame whose first byte sits r = dst mod 16 bytes into a 16-B chunk is written as destination
+// chunks k = 0 .. nst-1 at d0 = dst - r; chunk k holds frame-image bytes [16k - r, 16k - r + 16),
+// the image being the 31 header bytes (tag | EncHead) followed by the payload (image byte 31 =
+// payload[0]).  Chunks 0 and 1 and the first max(r, 1) - 1 bytes of chunk 2 are header bytes: the
+// packet's own lane stores them from its 8 header words (store_head).  Everything from image byte
+// 31 on is payload: chunk k >= 2 is the 16 bytes at offset sh of aligned source chunks k - 2 and
+// k - 1 of srcp = src + 1 - r - sh (sh = (src + 1 - r) mod 16), one funnel shift per chunk, stored
+// from byte max(r, 1) - 1 for k = 2 (r = 0 puts payload[0] in chunk 1, with the header words).
+// Chunk 0 of an unaligned frame is stored from byte r on and the last chunk up to the frame's end
+// (or, padded, to the 16-B boundary), so neighbouring frames packed at any byte offset are never
+// touched.  r = 0 is the aligned case.
+struct FrameGeo {
+    uint8_t *d0;           // 16-B aligned destination of chunk 0
+    const uint8_t *srcp;   // 16-B aligned source of chunk 2
+    uint32_t r, sh;        // dst mod 16, funnel shift
+    uint32_t nst;          // destination chunks stored
+    int32_t first_rel;     // payload[0]   relative to srcp (-1 .. 29)
+    int32_t last_rel;      // payload[P-1] relative to srcp
+};
+
+__device__ __forceinline__ FrameGeo frame_geo(const uint8_t *src, uint8_t *dst, uint32_t flen, uint32_t pad) {
+    FrameGeo g;
+    g.r = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15u);
+    g.d0 = dst - g.r;
+    g.sh = (uint32_t)((reinterpret_cast<uintptr_t>(src) + 1u - g.r) & 15u);
+    g.srcp = src + 1 - (int)g.r - (int)g.sh;
+    g.first_rel = (int32_t)(g.r + g.sh) - 1;
+    g.last_rel = g.first_rel + (int32_t)flen - RSK_HEAD_SIZE - 1;
+    g.nst = (g.r + padded_len(dst, flen, pad) + 15u) >> 4;
+    return g;
+}
+
+// aligned source chunk m (relative to srcp) holds at least one payload byte
+__device__ __forceinline__ bool src_chunk_live(int32_t m, int32_t first_rel, int32_t last_rel) {
+    return 16 * m <= last_rel && 16 * m + 16 > first_rel;
+}
+
+// first byte of chunk 2 that is payload (the header's last bytes precede it when r >= 2)
+__device__ __forceinline__ uint32_t chunk2_lo(uint32_t r) { return r >= 2u ? r - 1u : 0u; }
+
+// Store the bytes [lo, ...) of payload chunk v at p (16-B aligned) that belong to the frame: lim =
+// frame bytes from the chunk's start (>= 16: the whole chunk); with pad the tail is zero-filled to
+// the chunk's end.
+template <int NT>
+__device__ __forceinline__ void store_piece(uint8_t *p, uint4 v, uint32_t lo, int lim, bool pad) {
+    if (lim < 16 && pad) v = rsk::keep_bytes16(v, lim);
+    const uint32_t hi = lim < 16 && !pad ? (uint32_t)lim : 16u;
+    if (lo == 0u && hi == 16u) st16<NT>(p, v);
+    else rsk::store_range16(p, v, lo, hi);
+}
+
+// The header bytes of the lane's own frame (image bytes [0, 31), plus payload[0] at 31 when r = 0):
+// H = tag words, EncHead words and payload[0] in H[7]'s top byte.
+__device__ __forceinline__ void store_head(const uint32_t (&H)[8], uint8_t *dst) {
+    const uint32_t r = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15u);
+    uint8_t *d0 = dst - r;
+    const uint4 lo = make_uint4(H[0], H[1], H[2], H[3]), hi = make_uint4(H[4], H[5], H[6], H[7]);
+    if (r == 0u) {
+        st16<0>(d0, lo);
+        st16<0>(d0 + 16, hi);
+        return;
+    }
+    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+    rsk::store_range16(d0, funnel16_lane(z, lo, 16u - r), r, 16u);
+    st16<0>(d0 + 16, funnel16_lane(lo, hi, 16u - r));
+    if (r >= 2u) rsk::store_range16(d0 + 32, funnel16_lane(hi, z, 16u - r), 0u, r - 1u);
+}
+
+// ---- per-packet copy: the wave streams the payload chunks (k >= 2) of the frames of the packets
+// in `vm`, PU packets per iteration.  A frame spans at most 95 destination chunks (1500 B + 15 B of
+// offset), so chunk slots k = lane and k = lane + 64 cover it; all PU x 2 slots' loads are issued
+// before any store.  Lane k loads only aligned source chunk k - 2 and takes the funnel partner
+// (chunk k - 1) from lane k + 1 by a DPP wave shift (lane 63 of slot 0 from lane 0 of slot 1), so
+// a packet holds 2 uint4 registers per lane.  The shifts run with every lane active (DPP reads
+// disabled lanes as 0).  Lane p of an iteration stores the header chunks of the iteration's packet p
+// (store_head, header words fetched from the packet's lane by one ds_bpermute each).
+// tag (sets of long frames): phase 1 skipped payload[0] and the MD5, because that byte load
+// fetches the payload's first line well before the copy reaches the packet and the line is gone
+// from L2 by then; here lane p loads payload[0] of the iteration's packet p first, then the chunks,
+// and runs the MD5 of the PU packets while the chunk loads are in flight.
+__device__ __forceinline__ uint32_t wave_shl1(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false);  // wave_shl:1
+}
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
+    return (uint64_t)(uint32_t)__shfl((int)(uint32_t)v, (int)src) |
+           ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v >> 32), (int)src) << 32);
+}
+
+// Header-bearing destination chunk k < kh (kh = 2, or 3 when r >= 2) of a frame at offset r, for the
+// slot lanes 0..2 (TAG form): header image bytes [16k - r, 16k - r + 16) from the packet's header
+// words Hj (uniform, SGPRs), for k = 2 only its first r bytes, the rest from the payload funnel V.
+__device__ __forceinline__ uint4 head_chunk(const uint32_t (&H)[8], uint32_t k, uint32_t r, const uint4 &V) {
+    const uint4 lo = make_uint4(H[0], H[1], H[2], H[3]), hi = make_uint4(H[4], H[5], H[6], H[7]);
+    if (r == 0u) return k == 0u ? lo : hi;
+    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+    const uint4 X = k == 0u ? z : k == 1u ? lo : hi, Y = k == 0u ? lo : k == 1u ? hi : z;
+    const uint4 hs = rsk::funnel16(X, Y, 16u - r);  // r uniform: one scalar branch
+    if (k < 2u) return hs;
+    const uint4 m = rsk::keep_bytes16(make_uint4(~0u, ~0u, ~0u, ~0u), (int)r);  // first r bytes
+    return make_uint4((hs.x & m.x) | (V.x & ~m.x), (hs.y & m.y) | (V.y & ~m.y), (hs.z & m.z) | (V.z & ~m.z),
+                      (hs.w & m.w) | (V.w & ~m.w));
+}
+
+template <int PU, int NT, bool TAG>
+__device__ __forceinline__ void copy_pkt(const EncArgs &a, const KeySched &ks, const Lane1 &L, uint32_t lane,
+                                         uint64_t vm) {
+    while (vm) {
+        uint32_t js[PU];
+        bool on[PU];
+        uint32_t myj = 0;  // lane p: the packet of the iteration's slot p
+        bool mine = false;
+#pragma unroll
+        for (int p = 0; p < PU; ++p) {
+            on[p] = vm != 0ull;
+            js[p] = on[p] ? (uint32_t)__builtin_ctzll(vm) : 0u;
+            if (on[p]) vm &= vm - 1ull;
+            if (lane == (uint32_t)p) {
+                myj = js[p];
+                mine = on[p];
+            }
+        }
+        uint32_t my_b0 = 0;
+        if constexpr (TAG) {  // payload[0] of the lane's slot packet, issued before the chunk loads
+            const uint64_t po = shfl64(L.po, myj);
+            if (mine) my_b0 = rsk::gptr(a.payload)[po];
+        }
+        uint4 A[PU][2];
+        uint8_t *d0[PU];
+        uint32_t flen[PU], sh[PU], rr[PU], nst[PU];
+#pragma unroll
+        for (int p = 0; p < PU; ++p) {
+            flen[p] = on[p] ? rdl((uint32_t)L.st, js[p]) : 0u;
+            const FrameGeo g = frame_geo(a.payload + rdl64(L.po, js[p]), a.frame + rdl64(L.fo, js[p]), flen[p], a.pad);
+            d0[p] = g.d0;
+            sh[p] = g.sh;
+            rr[p] = g.r;
+            flen[p] += g.r;  // frame bytes counted from d0
+            nst[p] = on[p] ? g.nst : 0u;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int32_t m = (int32_t)(lane + 64u * q) - 2;
+                A[p][q] = make_uint4(0u, 0u, 0u, 0u);
+                if (on[p] && m >= 0 && src_chunk_live(m, g.first_rel, g.last_rel)) A[p][q] = ld16<NT>(g.srcp + 16 * m);
+            }
+        }
+        uint32_t t0 = 0, t1 = 0;
+        if constexpr (TAG) {
+            rsk::md5_tag(ks, my_b0, t0, t1);
+        } else {
+            // lane p stores the header chunks of its slot packet (store_head) beside the payload
+            // chunks, so each frame's first line is written whole while it is in L2
+            uint32_t H[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) H[t] = (uint32_t)__shfl((int)L.H[t], (int)myj);
+            const uint64_t my_fo = shfl64(L.fo, myj);
+            if (mine) store_head(H, a.frame + my_fo);
+        }
+#pragma unroll
+        for (int p = 0; p < PU; ++p) {
+            if (!on[p]) continue;
+            uint4 B[2];
+            B[0] = make_uint4(wave_shl1(A[p][0].x), wave_shl1(A[p][0].y), wave_shl1(A[p][0].z), wave_shl1(A[p][0].w));
+            B[1] = make_uint4(wave_shl1(A[p][1].x), wave_shl1(A[p][1].y), wave_shl1(A[p][1].z), wave_shl1(A[p][1].w));
+            const uint4 l0 = make_uint4(rdl(A[p][1].x, 0), rdl(A[p][1].y, 0), rdl(A[p][1].z, 0),
+                                        rdl(A[p][1].w, 0));  // read in uniform flow (see k_encode)
+            if (lane == 63u) B[0] = l0;
+            uint32_t Hj[8];  // TAG: the packet's header words (SGPRs), tag and payload[0] from lane p
+            if constexpr (TAG) {
+#pragma unroll
+                for (int t = 2; t < 8; ++t) Hj[t] = rdl(L.H[t], js[p]);
+                Hj[0] = rdl(t0, (uint32_t)p);
+                Hj[1] = rdl(t1, (uint32_t)p);
+                Hj[7] |= rdl(my_b0, (uint32_t)p) << 24;
+            }
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const uint32_t k = lane + 64u * q;
+                if (k >= nst[p] || (!TAG && k < 2u)) continue;
+                const uint4 V = rsk::funnel16(A[p][q], B[q], sh[p]);
+                if constexpr (TAG) {
+                    // TAG form: the header chunks in the packet's own slot stores (lanes 0..2)
+                    const uint4 v = k < (rr[p] >= 2u ? 3u : 2u) ? head_chunk(Hj, k, rr[p], V) : V;
+                    store_piece<NT>(d0[p] + 16u * k, v, k == 0u ? rr[p] : 0u, (int)flen[p] - 16 * (int)k,
+                                    a.pad != 0u);
+                } else {
+                    store_piece<NT>(d0[p] + 16u * k, V, k == 2u ? chunk2_lo(rr[p]) : 0u, (int)flen[p] - 16 * (int)k,
+                                    a.pad != 0u);
+                }
+            }
+        }
+    }
+}
+
+// ---- flat copy: the payload chunks (k >= 2) of every packet in `vm` as one list of 16-B chunks;
+// lane l of iteration t takes chunk g = 64(U t + u) + l and finds its packet by a 6-step binary
+// search over the set's prefix sums in this wave's LDS slice.  Wave-local: no block barrier, so
+// waves of one block may take different copy paths.
+template <int U>
 __device__ __forceinline__ void copy_flat(const EncArgs &a, const Lane1 &L, uint32_t lane, bool mine,
                                           CopyRec *recs, uint32_t *cend) {
     uint32_t cc = 0;
     CopyRec r;
     r.src_al = nullptr; r.dst = nullptr; r.cstart = 0; r.sh = 0; r.last_rel = 0; r.flen = 0;
     if (mine) {
-        const uint8_t *src = a.payload + L.po;
-        uint8_t *dst = a.frame + L.fo;
-        st16<NT>(dst, make_uint4(L.H[0], L.H[1], L.H[2], L.H[3]));  // frame bytes [0, 32): always
-        st16<NT>(dst + 16, make_uint4(L.H[4], L.H[5], L.H[6], L.H[7]));  // whole (31 + P >= 32)
         const uint32_t flen = (uint32_t)L.st;
-        cc = ((padded_len(dst, flen, a.pad) + 15u) >> 4) - 2u;
-        const uint32_t sh = (uint32_t)((reinterpret_cast<uintptr_t>(src) + 1u) & 15u);
-        r.src_al = src + 1 - sh;
-        r.dst = dst;
-        r.sh = sh;
-        r.last_rel = (int32_t)flen - RSK_HEAD_SIZE + (int32_t)sh - 2;
-        r.flen = flen;
+        const FrameGeo g = frame_geo(a.payload + L.po, a.frame + L.fo, flen, a.pad);
+        cc = g.nst - 2u;
+        r.src_al = g.srcp;
+        r.dst = g.d0;
+        r.sh = g.sh | (g.r << 4);
+        r.last_rel = g.last_rel;
+        r.flen = flen + g.r;  // frame bytes counted from d0
     }
-    uint32_t inc = cc;  // wave-inclusive scan -> tile chunk table
+    uint32_t inc = cc;  // wave-inclusive scan -> set chunk table
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
         const uint32_t v = __shfl_up(inc, off);
@@ -438,7 +429,7 @@ __device__ __forceinline__ void copy_flat(const EncArgs &a, const Lane1 &L, uint
     for (uint32_t g0 = 0; g0 < C; g0 += 64u * U) {
         uint4 A[U], B[U];
         uint8_t *dsts[U];
-        uint32_t shs[U];
+        uint32_t shs[U], los[U];
         int32_t lims[U];
         bool act[U];
 #pragma unroll
@@ -448,6 +439,7 @@ __device__ __forceinline__ void copy_flat(const EncArgs &a, const Lane1 &L, uint
             A[u] = make_uint4(0u, 0u, 0u, 0u);
             B[u] = make_uint4(0u, 0u, 0u, 0u);
             shs[u] = 0;
+            los[u] = 0;
             lims[u] = 0;
             dsts[u] = nullptr;
             if (act[u]) {
@@ -456,230 +448,92 @@ __device__ __forceinline__ void copy_flat(const EncArgs &a, const Lane1 &L, uint
                 for (uint32_t st = 32; st; st >>= 1)
                     if (cend[lo + st - 1] <= g) lo += st;
                 const CopyRec rr = recs[lo];
-                const uint32_t ro = 16u * (g - rr.cstart);
-                if ((int32_t)ro + 32 < (int32_t)rr.flen) {  // chunk holds frame bytes (else pure pad)
-                    A[u] = ld16<NT>(rr.src_al + ro);
-                    if (rr.sh != 0u && (int32_t)(ro + 16u) <= rr.last_rel) B[u] = ld16<NT>(rr.src_al + ro + 16);
-                }
-                shs[u] = rr.sh;
-                dsts[u] = rr.dst + 32u + ro;
-                lims[u] = (int32_t)rr.flen - 32 - (int32_t)ro;
+                const uint32_t rf = rr.sh >> 4, sh = rr.sh & 15u;
+                const int32_t m = (int32_t)(g - rr.cstart);  // source chunk of destination chunk m + 2
+                const int32_t first_rel = (int32_t)(rf + sh) - 1;
+                if (src_chunk_live(m, first_rel, rr.last_rel)) A[u] = ld16<0>(rr.src_al + 16 * m);
+                if (src_chunk_live(m + 1, first_rel, rr.last_rel)) B[u] = ld16<0>(rr.src_al + 16 * m + 16);
+                shs[u] = sh;
+                los[u] = m == 0 ? chunk2_lo(rf) : 0u;
+                dsts[u] = rr.dst + 32u + 16u * (uint32_t)m;
+                lims[u] = (int32_t)rr.flen - 32 - 16 * m;
             }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            if (act[u]) store_last16<NT>(dsts[u], funnel16_lane(A[u], B[u], shs[u]), lims[u], a.pad != 0u);
+            if (act[u]) store_piece<0>(dsts[u], funnel16_lane(A[u], B[u], shs[u]), los[u], lims[u], a.pad != 0u);
     }
     wave_lds_sync();  // LDS slice reusable by the caller afterwards
 }
 
-// ---- frames that are not 16-B aligned: byte path, one packet at a time -------------------------
-__device__ __forceinline__ void copy_bytes(const EncArgs &a, const Lane1 &L, uint32_t lane, uint64_t sm) {
-    while (sm) {
-        const uint32_t j = (uint32_t)__builtin_ctzll(sm);
-        sm &= sm - 1ull;
-        const uint32_t fl = rdl((uint32_t)L.st, j);
-        const uint8_t *src = a.payload + rdl64(L.po, j);
-        uint8_t *dst = a.frame + rdl64(L.fo, j);
-        uint32_t Hj[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) Hj[q] = rdl(L.H[q], j);
-        const uint32_t fend = padded_len(dst, fl, a.pad);
-        for (uint32_t f = lane; f < fend; f += 64u) {
-            uint32_t byte;
-            if (f >= fl) {
-                byte = 0;
-            } else if (f < (uint32_t)RSK_HEAD_SIZE) {
-                uint32_t wv = Hj[0];
-#pragma unroll
-                for (int q = 1; q < 8; ++q)
-                    if ((f >> 2) == (uint32_t)q) wv = Hj[q];
-                byte = (wv >> (8u * (f & 3u))) & 0xffu;
-            } else {
-                byte = rsk::gptr(src)[f - RSK_HEAD_SIZE];
-            }
-            rsk::gptr(dst)[f] = (uint8_t)byte;
-        }
-    }
-}
-
 // Copy-path choice for the hybrid kernel: the per-packet loop wastes lanes on short frames (a
 // 95-B frame uses 6 of 64 lanes), the flat list costs a binary search + LDS table per chunk.
-// Measured crossover: flat wins below a tile-mean frame of ~256 B.
+// Measured crossover: flat wins below a set-mean frame of ~256 B.
 constexpr uint32_t kFlatBelowMeanBytes = 256;
-// MODE 6: the tag moves into the copy loop (copy_pkt_dpp_tag) for sets of long frames only; with
-// short frames an iteration carries fewer bytes per MD5 (C4: +10 % with the tag deferred).
+// The tag moves into the copy loop for sets of long frames only; with short frames an iteration
+// carries fewer bytes per MD5 (C4: +10 % with the tag deferred).
 constexpr uint32_t kDeferTagMeanBytes = 1024;
 
-// One 64-packet set per wave: phase 1, then the chosen copy path.
-template <int MODE, int PU, int U, int NT>
-__device__ __forceinline__ void encode_copy(const EncArgs &a, const KeySched &ks, const Lane1 &L, uint32_t lane,
-                                            bool vec, uint64_t vm, bool flat, bool defer, CopyRec *recs,
-                                            uint32_t *cend) {
-    if (flat) copy_flat<U, NT>(a, L, lane, vec, recs, cend);
-    else if (MODE == 6 && defer) copy_pkt_dpp_tag<PU, NT>(a, ks, L, lane, vm);
-    else if constexpr (MODE >= 3) copy_pkt_dpp<PU, NT>(a, L, lane, vm);
-    else copy_pkt<PU, NT>(a, L, lane, vm);
-}
-
-// NT < 0: store policy chosen per set (below).
+// One 64-packet set per wave: phase 1, then the chosen copy path.  MODE 6 (shipped): per-wave
+// choice of path, tag deferred into the copy loop for sets of long frames; A/B build only: 3 = tag
+// always in phase 1, 7 = flat path only, 8 = per-packet path only.  NT < 0: store policy per set.
 template <int MODE, int PU, int U, int NT>
 __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks, uint64_t i, uint32_t lane,
                                            CopyRec *recs, uint32_t *cend) {
-    Lane1 L = encode_phase1<MODE != 6>(a, ks, i);
-    const bool vec = L.st > 0 && !L.slow;
+    Lane1 L = encode_phase1<MODE == 3 || MODE == 7>(a, ks, i);
+    const bool vec = L.st > 0;  // every framed packet takes a vector path, at any alignment
     const uint64_t vm = __ballot(vec);
-    bool flat = MODE == 1, defer = false;
-    if constexpr (MODE == 2 || MODE == 3 || MODE == 6) {
-        // set mean frame length over framed packets (wave reduction)
-        uint32_t fl = vec ? (uint32_t)L.st : 0u;
+    // set mean frame length over framed packets (wave reduction)
+    uint32_t fl = vec ? (uint32_t)L.st : 0u;
 #pragma unroll
-        for (int off = 32; off; off >>= 1) fl += __shfl_xor(fl, off);
-        const uint32_t cnt = (uint32_t)__popcll(vm);
-        flat = fl < kFlatBelowMeanBytes * cnt;
-        if constexpr (MODE == 6) defer = !flat && fl >= kDeferTagMeanBytes * cnt;
+    for (int off = 32; off; off >>= 1) fl += __shfl_xor(fl, off);
+    const uint32_t cnt = (uint32_t)__popcll(vm);
+    const bool flat = MODE == 7 ? true : MODE == 8 ? false : fl < kFlatBelowMeanBytes * cnt;
+    const bool defer = MODE != 3 && MODE != 7 && !flat && fl >= kDeferTagMeanBytes * cnt;
+    if constexpr (MODE != 3 && MODE != 7) {  // the tag now, except for the sets whose copy loop takes it
+        if (!defer) encode_tag(a, ks, L);
     }
-    if constexpr (MODE == 6) {  // the tag now, except for the frames the deferred-tag copy handles
-        if (!defer || L.slow) encode_tag(a, ks, L);
+    if (flat) {
+        if (vec) store_head(L.H, a.frame + L.fo);
+        copy_flat<U>(a, L, lane, vec, recs, cend);
+        return;
     }
+    bool nt = NT == 2;
     if constexpr (NT < 0) {
         // Store policy per set: frames packed back to back (each frame's padded end is the next
         // frame's start, so every line of the span is written in full) keep normal stores; any gap
         // leaves partially written lines, which nontemporal stores write without the memory-side
-        // read-modify-write (C4's 1440-B slots: -13 %; C3's packed frames: +4 % if streamed).  The
-        // flat path (short frames) keeps normal stores: streamed 95-B frames lose 10 %.
+        // read-modify-write (C4's 1440-B slots: -13 %; C3's packed frames: +4 % if streamed).
         const uint32_t fend = vec ? padded_len(a.frame + L.fo, (uint32_t)L.st, a.pad) : 0u;
         const uint64_t end = L.fo + fend;
         const uint64_t nfo = (uint64_t)(uint32_t)__shfl_down((int)(uint32_t)L.fo, 1) |
                              ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(L.fo >> 32), 1) << 32);
         const bool nvec = __shfl_down((int)vec, 1) != 0;
-        const bool gap = vec && nvec && lane != 63u && end != nfo;
-        if (!flat && __ballot(gap)) encode_copy<MODE, PU, U, 2>(a, ks, L, lane, vec, vm, flat, defer, recs, cend);
-        else encode_copy<MODE, PU, U, 0>(a, ks, L, lane, vec, vm, flat, defer, recs, cend);
-    } else {
-        encode_copy<MODE, PU, U, NT>(a, ks, L, lane, vec, vm, flat, defer, recs, cend);
+        nt = __ballot(vec && nvec && lane != 63u && end != nfo) != 0ull;
     }
-    copy_bytes(a, L, lane, __ballot(L.st > 0 && L.slow));
+    // Header chunks: sets with the tag in the copy loop (long frames) store them in the packet's
+    // first slot store (lanes 0..2, words by readlane); the others by the slot lane (store_head).
+    // Measured (A/B, profiles/r02_ab_head.json): C3 2.34 vs 2.55 ms with the first; C4 0.389 vs
+    // 0.420 ms with the second.
+    if (defer) {
+        if (nt) copy_pkt<PU, 2, true>(a, ks, L, lane, vm);
+        else copy_pkt<PU, 0, true>(a, ks, L, lane, vm);
+    } else {
+        if (nt) copy_pkt<PU, 2, false>(a, ks, L, lane, vm);
+        else copy_pkt<PU, 0, false>(a, ks, L, lane, vm);
+    }
 }
 
-// MODE: 0 per-packet, 1 flat, 2 hybrid (per-wave choice), 3 hybrid with the DPP per-packet copy,
-// 4 DPP per-packet only, 5 (unused), 6 = 3 with the tag deferred into the copy loop for long frames.
-// Tiled mapping: wave t takes packets [64t, 64t + 64) (coalesced descriptor loads, but the 5000+
-// co-resident waves each stream their own ~92 KB region).
-// MAP 1 (A/B): workgroups are dispatched round-robin over the 8 XCDs, so by default XCD x runs
-// blocks x, x + 8, ...; MAP 1 renumbers them so that XCD x owns one contiguous eighth of the batch.
-__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
-    const uint32_t x = b & 7u, k = b >> 3, q = nb >> 3, r = nb & 7u;
-    return x < r ? x * (q + 1u) + k : r * (q + 1u) + (x - r) * q + k;
-}
-
-// MAP >= 2 (A/B): each wave takes MAP consecutive sets (a MAP x 92-KB tile for C3), the grid MAP
-// times smaller.
-template <int MODE, int PU, int U, int NT, int MAP = 0>
+// Tiled mapping: wave t takes packets [64t, 64t + 64) (coalesced descriptor loads; the co-resident
+// waves each stream their own region of the arenas).
+template <int MODE, int PU, int U, int NT>
 __global__ __launch_bounds__(kBlock) void k_encode(EncArgs a, KeySched ks) {
     __shared__ CopyRec recs[kWavesPerBlock][64];
     __shared__ uint32_t cend[kWavesPerBlock][64];
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    const uint32_t blk = MAP == 1 ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    constexpr uint32_t S = MAP >= 2 ? MAP : 1;
-    for (uint32_t k = 0; k < S; ++k) {
-        const uint64_t base = (((uint64_t)blk * kWavesPerBlock + w) * S + k) * 64u;
-        if (base >= a.n) return;  // wave-uniform; no block barriers below
-        encode_set<MODE, PU, U, NT>(a, ks, base + lane, lane, recs[w], cend[w]);
-    }
-}
-
-
-// Block-interleaved per-packet copy (A/B variant 11): phase 1 as usual, then the block's 256
-// packet records go through LDS and wave w copies packets w, w + 4, w + 8, ... so the 4 waves of a
-// block stream adjacent frames instead of four regions 92 KB apart.
-struct alignas(16) PktRec {
-    const uint8_t *src;
-    uint8_t *dst;
-    uint32_t H[8];
-    int32_t st;
-    uint32_t slow;
-    uint32_t pad_[2];
-};
-
-template <int PU>
-__global__ __launch_bounds__(kBlock) void k_encode_blk(EncArgs a, KeySched ks) {
-    __shared__ PktRec rec[kBlock];
-    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    {
-        const Lane1 L = encode_phase1(a, ks, i);
-        PktRec r;
-        r.src = a.payload + L.po;
-        r.dst = a.frame + L.fo;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) r.H[q] = L.H[q];
-        r.st = L.st;
-        r.slow = L.slow ? 1u : 0u;
-        r.pad_[0] = r.pad_[1] = 0;
-        rec[threadIdx.x] = r;
-    }
-    __syncthreads();
-    for (uint32_t k0 = 0; k0 < 64u; k0 += PU) {
-        uint4 A[PU][2], B[PU][2];
-        uint32_t flen[PU], sh[PU];
-        const uint8_t *srcp[PU];
-        uint8_t *dstp[PU];
-        bool on[PU];
-#pragma unroll
-        for (int p = 0; p < PU; ++p) {
-            const PktRec &R = rec[w + 4u * (k0 + p)];
-            on[p] = R.st > 0 && !R.slow;
-            flen[p] = on[p] ? (uint32_t)R.st : 0u;
-            sh[p] = (uint32_t)((reinterpret_cast<uintptr_t>(R.src) + 1u) & 15u);
-            srcp[p] = R.src + 1 - sh[p];
-            dstp[p] = R.dst;
-            const int32_t last_rel = (int32_t)flen[p] - RSK_HEAD_SIZE + (int32_t)sh[p] - 2;
-            const uint32_t nch = (flen[p] + 15u) >> 4;
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const uint32_t k = lane + 64u * q;
-                A[p][q] = make_uint4(0u, 0u, 0u, 0u);
-                B[p][q] = make_uint4(0u, 0u, 0u, 0u);
-                if (k >= 2u && k < nch) {
-                    const uint32_t ro = 16u * (k - 2u);
-                    A[p][q] = ld16<0>(srcp[p] + ro);
-                    if (sh[p] != 0u && (int32_t)(ro + 16u) <= last_rel) B[p][q] = ld16<0>(srcp[p] + ro + 16u);
-                }
-            }
-        }
-#pragma unroll
-        for (int p = 0; p < PU; ++p) {
-            if (!on[p]) continue;
-            const uint32_t nch = (padded_len(dstp[p], flen[p], a.pad) + 15u) >> 4;
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const uint32_t k = lane + 64u * q;
-                if (k >= nch) continue;
-                uint4 v;
-                if (k >= 2u) {
-                    v = rsk::funnel16(A[p][q], B[p][q], sh[p]);
-                } else {
-                    const PktRec &R = rec[w + 4u * (k0 + p)];
-                    v = k == 0u ? make_uint4(R.H[0], R.H[1], R.H[2], R.H[3]) : make_uint4(R.H[4], R.H[5], R.H[6], R.H[7]);
-                }
-                store_last16<0>(dstp[p] + 16u * k, v, (int)flen[p] - 16 * (int)k, a.pad != 0u);
-            }
-        }
-    }
-    // frames that are not 16-B aligned: byte path, one packet at a time
-    for (uint32_t k = 0; k < 64u; ++k) {
-        const PktRec &R = rec[w + 4u * k];
-        if (R.st <= 0 || !R.slow) continue;
-        const uint32_t fl = (uint32_t)R.st, fend = padded_len(R.dst, fl, a.pad);
-        for (uint32_t f = lane; f < fend; f += 64u) {
-            uint32_t byte;
-            if (f >= fl) byte = 0;
-            else if (f < (uint32_t)RSK_HEAD_SIZE) byte = (R.H[f >> 2] >> (8u * (f & 3u))) & 0xffu;
-            else byte = rsk::gptr(R.src)[f - RSK_HEAD_SIZE];
-            rsk::gptr(R.dst)[f] = (uint8_t)byte;
-        }
-    }
+    const uint64_t base = ((uint64_t)blockIdx.x * kWavesPerBlock + w) * 64u;
+    if (base >= a.n) return;  // wave-uniform; no block barriers below
+    encode_set<MODE, PU, U, NT>(a, ks, base + lane, lane, recs[w], cend[w]);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2087,25 +1941,13 @@ const char *rsk_last_error(void) { return g_last_error; }
 const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 
 #ifdef RSK_AB
-// Internal tuning knob (not part of include/rsk_codec.h): selects the encode kernel variant for
-// in-process A/B measurements.  k_encode<MODE, PU, U, NT>: MODE 0 per-packet, 1 flat, 2 hybrid,
-// 3 hybrid with the one-load DPP per-packet copy, 4 DPP per-packet only; PU packets per per-packet
-// iteration; U chunks per lane per flat iteration; NT bit0 nontemporal loads, bit1 nontemporal stores.
-//   0 = hybrid-DPP<12,4>, tag computed in the copy loop for sets of long frames (MODE 6), per-set
-//       store policy (default: nontemporal stores for per-packet sets whose frames leave gaps)
-//   1 = pkt PU=1   2 = flat U=2    3 = flat U=4    4 = pkt PU=2
-//   5 = pkt PU=4                6 = hybrid nt-stores           7 = pkt PU=4 nt loads+stores
-//   8 = pkt PU=4 nt stores      9 = hybrid PU=2               10 = pkt PU=2 nt stores
-//  11 = block-interleaved pkt PU=4   12 = block-interleaved pkt PU=2
-//  13 = two-load hybrid<4,4> (the default before the DPP copy)
-//  14/15/16 = hybrid-DPP PU=4/8/12   17 = DPP per-packet only PU=16
-//  18/19 = hybrid-DPP PU=16/8 with nontemporal stores   20 = hybrid-DPP PU=16 (normal stores)
-//  21 = hybrid-DPP PU=16 with the per-set store policy (169 VGPRs: 2 waves/SIMD)
-//  22 = hybrid-DPP PU=12 with the per-set store policy, tag in phase 1 (the default before)
-//  23/24 = the default with PU=8/16
-// v + 100 * cap (cap 1..4): the same kernel held to `cap` blocks per CU by unused dynamic LDS.
+// A/B build only: selects the encode kernel variant for in-process A/B runs (tools/ab_encode.py).
+// k_encode<MODE, PU, U, NT> (see encode_set): 0 = the shipped <6, 12, 4, -1>; 1 = tag always in
+// phase 1; 2 / 3 = 8 / 16 packets per per-packet iteration; 4 = 2 chunks per lane per flat
+// iteration; 5 / 6 = normal / nontemporal stores on every per-packet set; 7 = flat path only;
+// 8 = per-packet path only.  v + 100 * cap (cap 1..4): the same kernel held to `cap` blocks per CU by unused LDS.
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
-    if (!c || v < 0 || v % 100 > 28 || v / 100 > 4) return RSK_EINVAL;
+    if (!c || v < 0 || v % 100 > 8 || v / 100 > 4) return RSK_EINVAL;
     c->enc_variant = v;
     return RSK_OK;
 }
@@ -2190,34 +2032,14 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
     const int cap = c->enc_variant / 100;
     const size_t lds = cap ? (size_t)(163840 / cap) - 16384 : 0;
     switch (c->enc_variant % 100) {
-        case 13: hipLaunchKernelGGL((k_encode<2, 4, 4, 0>), gd, bd, lds, st, a, c->ks); break;
-        case 14: hipLaunchKernelGGL((k_encode<3, 4, 4, 0>), gd, bd, lds, st, a, c->ks); break;
-        case 15: hipLaunchKernelGGL((k_encode<3, 8, 4, 0>), gd, bd, lds, st, a, c->ks); break;
-        case 16: hipLaunchKernelGGL((k_encode<3, 12, 4, 0>), gd, bd, lds, st, a, c->ks); break;
-        case 17: hipLaunchKernelGGL((k_encode<4, 16, 4, 0>), gd, bd, lds, st, a, c->ks); break;
-        case 18: hipLaunchKernelGGL((k_encode<3, 16, 4, 2>), gd, bd, lds, st, a, c->ks); break;
-        case 19: hipLaunchKernelGGL((k_encode<3, 8, 4, 2>), gd, bd, lds, st, a, c->ks); break;
-        case 20: hipLaunchKernelGGL((k_encode<3, 16, 4, 0>), gd, bd, lds, st, a, c->ks); break;
-        case 21: hipLaunchKernelGGL((k_encode<3, 16, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 22: hipLaunchKernelGGL((k_encode<3, 12, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 23: hipLaunchKernelGGL((k_encode<6, 8, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 24: hipLaunchKernelGGL((k_encode<6, 16, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 25: hipLaunchKernelGGL((k_encode<6, 12, 4, -1, 1>), gd, bd, lds, st, a, c->ks); break;
-        case 26: hipLaunchKernelGGL((k_encode<6, 12, 4, -1, 2>), dim3((grid + 1) / 2), bd, lds, st, a, c->ks); break;
-        case 27: hipLaunchKernelGGL((k_encode<6, 12, 4, -1, 4>), dim3((grid + 3) / 4), bd, lds, st, a, c->ks); break;
-        case 28: hipLaunchKernelGGL((k_encode<6, 12, 4, -1, 8>), dim3((grid + 7) / 8), bd, lds, st, a, c->ks); break;
-        case 1: hipLaunchKernelGGL((k_encode<0, 1, 4, 0>), gd, bd, 0, st, a, c->ks); break;
-        case 2: hipLaunchKernelGGL((k_encode<1, 4, 2, 0>), gd, bd, 0, st, a, c->ks); break;
-        case 3: hipLaunchKernelGGL((k_encode<1, 4, 4, 0>), gd, bd, 0, st, a, c->ks); break;
-        case 4: hipLaunchKernelGGL((k_encode<0, 2, 4, 0>), gd, bd, 0, st, a, c->ks); break;
-        case 5: hipLaunchKernelGGL((k_encode<0, 4, 4, 0>), gd, bd, 0, st, a, c->ks); break;
-        case 6: hipLaunchKernelGGL((k_encode<2, 4, 4, 2>), gd, bd, 0, st, a, c->ks); break;
-        case 7: hipLaunchKernelGGL((k_encode<0, 4, 4, 3>), gd, bd, 0, st, a, c->ks); break;
-        case 8: hipLaunchKernelGGL((k_encode<0, 4, 4, 2>), gd, bd, 0, st, a, c->ks); break;
-        case 9: hipLaunchKernelGGL((k_encode<2, 2, 4, 0>), gd, bd, 0, st, a, c->ks); break;
-        case 10: hipLaunchKernelGGL((k_encode<0, 2, 4, 2>), gd, bd, 0, st, a, c->ks); break;
-        case 11: hipLaunchKernelGGL((k_encode_blk<4>), gd, bd, 0, st, a, c->ks); break;
-        case 12: hipLaunchKernelGGL((k_encode_blk<2>), gd, bd, 0, st, a, c->ks); break;
+        case 1: hipLaunchKernelGGL((k_encode<3, 12, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 2: hipLaunchKernelGGL((k_encode<6, 8, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 3: hipLaunchKernelGGL((k_encode<6, 16, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 4: hipLaunchKernelGGL((k_encode<6, 12, 2, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 5: hipLaunchKernelGGL((k_encode<6, 12, 4, 0>), gd, bd, lds, st, a, c->ks); break;
+        case 6: hipLaunchKernelGGL((k_encode<6, 12, 4, 2>), gd, bd, lds, st, a, c->ks); break;
+        case 7: hipLaunchKernelGGL((k_encode<7, 12, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 8: hipLaunchKernelGGL((k_encode<8, 12, 4, -1>), gd, bd, lds, st, a, c->ks); break;
         default: hipLaunchKernelGGL((k_encode<6, 12, 4, -1>), gd, bd, lds, st, a, c->ks); break;
     }
 #else

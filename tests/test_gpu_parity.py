@@ -6,6 +6,7 @@ size-independent properties in test_gpu_fullsize.py.
 from __future__ import annotations
 
 import os
+import zlib
 
 import numpy as np
 import pytest
@@ -520,3 +521,63 @@ def test_parse_decode_slots(codec, gpu, oracle, slot, flags):
             assert plain.any() and not (short & plain).any()
         if slot == 64:
             assert short.any()
+
+
+@pytest.mark.parametrize("mix", ["short", "mixed", "long", "bimodal"])
+@pytest.mark.parametrize("layout,pad", [("packed_bytes", 0), ("rand_r", 0), ("rand_r", 16), ("every_r", 0),
+                                        ("every_r", 16)])
+@pytest.mark.parametrize("odd_payloads", [False, True])
+def test_encode_any_frame_alignment(codec, gpu, oracle, mix, layout, pad, odd_payloads):
+    """k_encode's vector paths at every destination offset r = frame_off mod 16:
+    flat path (short sets), per-packet path (mixed), per-packet with the tag in the copy loop (long),
+    frames packed back to back at byte granularity; bytes outside the frames must survive."""
+    rng = np.random.default_rng(zlib.crc32(repr((mix, layout, pad, odd_payloads)).encode()))
+    nset = 24
+    n = 64 * nset
+    if mix == "short":
+        plen = rng.integers(1, 120, n)
+    elif mix == "long":
+        plen = rng.integers(1100, 1470, n)
+    elif mix == "mixed":
+        plen = rng.integers(1, 1470, n)
+    else:  # alternate sets of short and long frames
+        plen = np.where((np.arange(n) // 64) % 2 == 0, rng.integers(1, 80, n), rng.integers(1200, 1470, n))
+    plen = plen.astype(np.uint16)
+    plen[rng.integers(0, n, 5)] = 0  # resets in the middle of sets
+    if odd_payloads:
+        pay_off = np.cumsum(np.concatenate([[7], plen[:-1].astype(np.int64) + rng.integers(0, 19, n - 1)]))
+    else:
+        pay_off = np.arange(n) * 1472
+    pay_off = pay_off.astype(np.uint64)
+    payload = rng.integers(0, 256, int(pay_off[-1]) + 1600, dtype=np.uint8)
+    flen = np.where(plen >= 1, plen.astype(np.int64) + 31, 0)
+    if layout == "packed_bytes":
+        frame_off = 3 + np.concatenate([[0], np.cumsum(flen)[:-1]])
+    elif layout == "rand_r":
+        frame_off = np.arange(n) * 1536 + rng.integers(0, 16, n)
+    else:  # every r in turn, so each set holds all 16 offsets
+        frame_off = np.arange(n) * 1536 + np.arange(n) % 16
+    frame_off = frame_off.astype(np.uint64)
+    frame_bytes = int(frame_off[-1]) + 1600
+    cmd, conv, ckey = _rand_fields(rng, n)
+
+    class D:
+        pass
+
+    d = D()
+    d.n, d.pay_off, d.pay_len, d.cmd, d.conv, d.conn_key, d.frame_off = n, pay_off, plen, cmd, conv, ckey, frame_off
+    fill = rng.integers(0, 256, frame_bytes, dtype=np.uint8)
+    got_frames, got_status = run_encode(codec, gpu, payload, pay_off, plen, cmd, conv, ckey, frame_off,
+                                        frame_bytes, frame_init=fill, pad16=pad == 16)
+    ef, es = oracle.encode_batch(KEY, payload, d, workload.ID_UNIFORM, frame_bytes=frame_bytes)
+    assert np.array_equal(got_status, es)
+    exp_frames = fill.copy()
+    for i in range(n):
+        if es[i] > 0:
+            o = int(frame_off[i])
+            exp_frames[o:o + es[i]] = ef[o:o + es[i]]
+            if pad:
+                e = o + int(es[i])
+                exp_frames[e:(e + pad - 1) // pad * pad] = 0
+    bad = np.nonzero(got_frames != exp_frames)[0]
+    assert bad.size == 0, f"{bad.size} bytes differ, first at {bad[:8]} (frame {np.searchsorted(frame_off, bad[0], 'right') - 1})"
