@@ -8,21 +8,23 @@
 // batch becomes segments (one per key and epoch, ordered by first packet, arrival order inside), so
 // the host does one lookup per segment.
 //
-// Pipeline (all stream-ordered, no host sync; n_valid and the segment count stay on the device):
-//   k_dm_flags   per-wave ballots of VALID and VALID-control packets + per-block counts
-//   scan x2      block offsets (compacted index, epoch = number of earlier control packets)
-//   k_dm_prep    cidx[j] = packet of compacted slot j, cep[j] = its epoch (CTRL for singletons)
-//   k_dm_insert  open-addressing table: a slot holds a key fingerprint and the compacted index of
-//                one packet of its key, so key confirmation reads the immutable input arrays (no
-//                lane ever waits on another lane's write); atomicMin leaves each key's first
-//                packet in tmin
-//   k_dm_leader  leader of j = tab_min[slot] (or j for a control packet); ballots of leaders
-//   scan         leader ranks = dense segment ids in first-occurrence order
-//   k_dm_rank    rank_at[leader], seg_first[rank]
-//   k_dm_segof   radix keys = segment id of each compacted packet, values = its packet index
-//   radix        stable LSD sort by segment id, 8-bit digits, as many passes as the segment count
-//                needs (passes beyond that return at once; the device-side count decides)
-//   k_dm_final   perm = sorted values, seg_off from the key boundaries, n_seg / n_valid
+// Pipeline (all stream-ordered, no host sync; n_valid and the segment count stay on the device),
+// 5 + passes launches after one fill (round 2: the block scans are decoupled look-backs inside the
+// kernels that produce the counts, and the radix sort is onesweep, one launch per pass):
+//   fill            key table + look-back state words to all-ones
+//   k_dm_flags_prep per-wave ballots of VALID and VALID-control packets, block offsets by look-back;
+//                   cidx[j] = packet of compacted slot j, cep[j] = its epoch (CTRL for singletons)
+//   k_dm_insert     open-addressing table: a slot holds a key fingerprint and the compacted index of
+//                   one packet of its key, so key confirmation reads the immutable input arrays (no
+//                   lane ever waits on another lane's write); atomicMin leaves each key's first
+//                   packet in tmin
+//   k_dm_leader_rank leader of j = tab_min[slot] (or j for a control packet); leader ranks = dense
+//                   segment ids in first-occurrence order by look-back; rank_at, seg_first, n_seg
+//   k_dm_segof_hist radix keys = segment id of each compacted packet, values = its packet index,
+//                   global digit histograms of every pass
+//   k_dm_onesweep   stable LSD pass by segment id (8-bit or narrower digits, as many passes as the
+//                   segment count needs; passes beyond that return at once), per-digit look-back
+//   k_dm_final      perm = sorted values, seg_off from the key boundaries, n_seg / n_valid
 #include <hip/hip_runtime.h>
 
 #include <cstring>
@@ -41,14 +43,6 @@ constexpr uint32_t kCtrl = 0xffffffffu;         // cep[] marker: control packet 
 constexpr uint32_t kScanChunk = 4096;           // elements per block in the multi-block scan
 
 __device__ __forceinline__ uint64_t lanemask_lt(uint32_t lane) { return (1ull << lane) - 1ull; }
-
-// XCD-aware tile index (bijective for any grid size): blocks are dealt round-robin over the 8 XCDs
-// (MI355X_MICROARCH.md), so block b runs tile xcd_tile(b) and each XCD streams a contiguous range of
-// tiles; the sectors two neighbouring tiles both write half of then meet in the same L2 (speed only).
-__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nwg) {
-    const uint32_t x = b % 8u, q = nwg / 8u, r = nwg % 8u;
-    return (x < r ? x * (q + 1u) : r * (q + 1u) + (x - r) * q) + b / 8u;
-}
 
 // ---- scans ----------------------------------------------------------------------------------
 // exclusive scan of 4096 u32 per pass by one 1024-thread block; carry across passes
@@ -143,45 +137,78 @@ struct DmIn {
     uint32_t n, fields;
 };
 
-// ballots of a block's 4 waves + the block's popcount
-__device__ __forceinline__ void block_ballot(bool p, uint64_t *masks, uint32_t *counts, uint32_t *wc) {
-    const uint64_t m = __ballot(p);
-    const uint32_t w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63u) == 0) {
-        masks[(uint64_t)blockIdx.x * kWaves + w] = m;
-        wc[w] = (uint32_t)__popcll(m);
+// ---- decoupled look-back: one-pass exclusive scan of per-block counts across a grid -----------
+// Block b publishes its aggregate, then reads its predecessors' words (a wave 64 at a time) until it
+// meets an inclusive prefix, and publishes its own inclusive prefix.  Blocks are dispatched in
+// index order, so a block only ever waits for blocks that are already resident or done.  State
+// words start as all-ones (the demux memset); a ready word is the value in bits 0..31 with bit 63
+// set for an inclusive prefix.  Device-scope RELAXED atomics (sc1 loads / stores, coherent across
+// the XCDs' L2s): the published words are the only data one block reads from another, so no
+// ordering is needed, and acquire / release at device scope would add an L2 invalidate / write-back
+// per access (first build: 0.56 ms for C4's flags pass instead of ~0.02).  A spin that outlives
+// kDlbSpinMax reads gives up (the batch result is then wrong, the GPU is not hung).
+constexpr unsigned long long kDlbEmpty = ~0ull;
+constexpr unsigned long long kDlbIncl = 1ull << 63;
+constexpr uint32_t kDlbSpinMax = 1u << 22;
+
+__device__ __forceinline__ void dlb_publish(unsigned long long *s, unsigned long long v) {
+    __hip_atomic_store(s, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long dlb_wait(unsigned long long *s) {
+    unsigned long long v;
+    uint32_t spins = 0;
+    do {
+        v = __hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } while (v == kDlbEmpty && ++spins < kDlbSpinMax);
+    return v == kDlbEmpty ? kDlbIncl : v;
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+// Called by all 64 lanes of one wave of block b; agg uniform; returns b's exclusive prefix (uniform).
+__device__ uint32_t dlb_wave(unsigned long long *st, uint32_t b, uint32_t agg, uint32_t lane) {
+    if (b == 0u) {
+        if (lane == 0u) dlb_publish(st, kDlbIncl | agg);
+        return 0u;
     }
-    __syncthreads();
-    if (threadIdx.x == 0) counts[blockIdx.x] = wc[0] + wc[1] + wc[2] + wc[3];
-}
-// exclusive rank of this lane's set bit among the block's ballots, plus the block's scanned offset
-__device__ __forceinline__ uint32_t block_rank(const uint64_t *masks, const uint32_t *offsets) {
-    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    const uint64_t *mb = masks + (uint64_t)blockIdx.x * kWaves;
-    uint32_t pos = offsets[blockIdx.x];
-    for (uint32_t q = 0; q < w; ++q) pos += (uint32_t)__popcll(mb[q]);
-    return pos + (uint32_t)__popcll(mb[w] & lanemask_lt(lane));
-}
-
-__global__ __launch_bounds__(kBlock) void k_dm_flags(DmIn a, uint64_t *mv, uint32_t *cv, uint64_t *mc, uint32_t *cc) {
-    __shared__ uint32_t wc[2][kWaves];
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    const bool valid = i < a.n && a.status[i] == RSK_RECV_VALID;
-    const bool ctrl = valid && (a.fields & RSK_DEMUX_CMD_BARRIER) && a.cmd[i] != RSK_CMD_DATA;
-    block_ballot(valid, mv, cv, wc[0]);
-    block_ballot(ctrl, mc, cc, wc[1]);
+    if (lane == 0u) dlb_publish(st + b, (unsigned long long)agg);
+    uint32_t excl = 0;
+    for (int64_t top = (int64_t)b - 1;; top -= 64) {
+        const int64_t j = top - (int64_t)lane;
+        const unsigned long long v = j >= 0 ? dlb_wait(st + j) : kDlbIncl;  // before block 0: inclusive 0
+        const uint64_t im = __ballot((v & kDlbIncl) != 0ull);
+        uint32_t val = (uint32_t)v;
+        if (im) {  // the nearest inclusive predecessor ends the walk
+            if (lane > (uint32_t)__builtin_ctzll(im)) val = 0u;
+            excl += wave_sum(val);
+            break;
+        }
+        excl += wave_sum(val);
+    }
+    if (lane == 0u) dlb_publish(st + b, kDlbIncl | (unsigned long long)(excl + agg));
+    return excl;
 }
 
-__global__ __launch_bounds__(kBlock) void k_dm_prep(DmIn a, const uint64_t *mv, const uint32_t *ov,
-                                                    const uint64_t *mc, const uint32_t *oc, uint32_t *cidx,
-                                                    uint32_t *cep) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    if (!((mv[(uint64_t)blockIdx.x * kWaves + w] >> lane) & 1ull)) return;
-    const uint32_t j = block_rank(mv, ov);
-    const bool ctrl = (mc[(uint64_t)blockIdx.x * kWaves + w] >> lane) & 1ull;
-    cidx[j] = i;
-    cep[j] = ctrl ? kCtrl : block_rank(mc, oc);  // epoch = control packets before this one
+// Per-digit look-back for the onesweep radix scatter: thread d of tile t publishes its digit count,
+// walks back over tiles until an inclusive word, publishes the inclusive count; returns the count
+// of digit d in tiles before t.
+__device__ uint32_t dlb_digit(unsigned long long *st, uint32_t t, uint32_t d, uint32_t cnt) {
+    if (t == 0u) {
+        dlb_publish(st + d, kDlbIncl | cnt);
+        return 0u;
+    }
+    dlb_publish(st + (uint64_t)t * 256u + d, (unsigned long long)cnt);
+    uint32_t excl = 0;
+    for (int64_t j = (int64_t)t - 1; j >= 0; --j) {
+        const unsigned long long v = dlb_wait(st + (uint64_t)j * 256u + d);
+        excl += (uint32_t)v;
+        if (v & kDlbIncl) break;
+    }
+    dlb_publish(st + (uint64_t)t * 256u + d, kDlbIncl | (unsigned long long)(excl + cnt));
+    return excl;
 }
 
 struct Key {
@@ -311,40 +338,6 @@ __global__ __launch_bounds__(kBlock) void k_dm_insert(DmIn a, const uint32_t *nv
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_dm_leader(const uint32_t *nvp, const uint32_t *hslot, const uint32_t *tmin,
-                                                      uint32_t *lead_of, uint64_t *ml, uint32_t *cl) {
-    __shared__ uint32_t wc[kWaves];
-    const uint32_t nv = *nvp;
-    const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
-    bool isl = false;
-    if (j < nv) {
-        const uint32_t h = hslot[j];
-        const uint32_t lead = h == kNone ? j : tmin[h];
-        lead_of[j] = lead;
-        isl = lead == j;
-    }
-    block_ballot(isl, ml, cl, wc);
-}
-
-__global__ __launch_bounds__(kBlock) void k_dm_rank(const uint32_t *nvp, const uint64_t *ml, const uint32_t *ol,
-                                                    const uint32_t *cidx, uint32_t *rank_at, uint32_t *seg_first) {
-    const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    if (j >= *nvp || !((ml[(uint64_t)blockIdx.x * kWaves + w] >> lane) & 1ull)) return;
-    const uint32_t r = block_rank(ml, ol);
-    rank_at[j] = r;
-    seg_first[r] = cidx[j];
-}
-
-__global__ __launch_bounds__(kBlock) void k_dm_segof(const uint32_t *nvp, const uint32_t *lead_of,
-                                                     const uint32_t *rank_at, const uint32_t *cidx, uint32_t *keys,
-                                                     uint32_t *vals) {
-    const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
-    if (j >= *nvp) return;
-    keys[j] = rank_at[lead_of[j]];
-    vals[j] = cidx[j];  // the packet index rides through the sort
-}
-
 // ---- stable LSD radix sort by segment id ------------------------------------------------------
 __device__ __forceinline__ uint32_t bits_for(uint32_t nseg) {  // bits of the largest key (< nseg)
     return nseg <= 1u ? 1u : 32u - (uint32_t)__builtin_clz(nseg - 1u);
@@ -367,47 +360,202 @@ __device__ __forceinline__ uint64_t digit_peers(bool v, uint32_t d, uint32_t wid
     return peers;
 }
 
-__global__ __launch_bounds__(kBlock) void k_dm_hist(uint32_t pass, const uint32_t *nvp, const uint32_t *nsegp,
-                                                    const uint32_t *keys, uint32_t *hist, uint32_t nt) {
-    __shared__ uint32_t lh[256];
-    const uint32_t nv = *nvp, ns = *nsegp;
-    if (pass >= n_passes(ns)) return;  // block-uniform
-    const uint32_t width = digit_width(ns), sh = width * pass, dm = (1u << width) - 1u;
-    const uint32_t t = threadIdx.x, lane = t & 63u, tile = xcd_tile(blockIdx.x, gridDim.x);
-    lh[t] = 0;
-    __syncthreads();
-    if (tile * kTile < nv) {  // tiles past n_valid count zeros
-        uint32_t kk[kItems];  // all of the thread's loads in flight before the first ballot
+// Look-back scans run over tiles of kTile items (16 rows of 256) so a 4M-item batch has 1024
+// look-back steps in its chain instead of 16384.
+constexpr uint32_t kRows = kTile / kBlock;
+
+// per-row ballots of the block -> this lane's wave offset within each row (rows before it included)
+__device__ __forceinline__ void tile_offsets(const uint64_t (*m)[kWaves], uint32_t w, uint32_t (&off)[kRows],
+                                             uint32_t &total) {
+    uint32_t acc = 0;
 #pragma unroll
-        for (uint32_t r = 0; r < kItems; ++r) {
-            const uint32_t k = tile * kTile + r * kBlock + t;
-            kk[r] = k < nv ? keys[k] : 0u;
+    for (uint32_t r = 0; r < kRows; ++r) {
+        uint32_t o = acc;
+#pragma unroll
+        for (uint32_t q = 0; q < (uint32_t)kWaves; ++q) {
+            const uint32_t c = (uint32_t)__popcll(m[r][q]);
+            if (q < w) o += c;
+            acc += c;
         }
+        off[r] = o;
+    }
+    total = acc;
+}
+
+// flags + both block scans + prep in one pass: per-row ballots of VALID and VALID-control packets,
+// the tile's exclusive offsets by decoupled look-back (wave 0: compacted index, wave 1: epoch), then
+// cidx[j] = packet of compacted slot j, cep[j] = its epoch (CTRL for singletons); the last tile
+// writes n_valid.
+__global__ __launch_bounds__(kBlock) void k_dm_flags_prep(DmIn a, unsigned long long *st_v,
+                                                          unsigned long long *st_c, uint32_t *cidx, uint32_t *cep,
+                                                          uint32_t *nvp) {
+    __shared__ uint64_t mv[kRows][kWaves], mc[kRows][kWaves];
+    __shared__ uint32_t pre[2];
+    const uint32_t b = blockIdx.x, t = threadIdx.x, w = t >> 6, lane = t & 63u;
+    uint32_t flags = 0;  // bit r: row r's item valid; bit 16 + r: control
+    int8_t stv[kRows];  // every row's loads in flight before the first ballot
+    uint8_t cmv[kRows];
+    const bool barrier = (a.fields & RSK_DEMUX_CMD_BARRIER) != 0u;
 #pragma unroll
-        for (uint32_t r = 0; r < kItems; ++r) {
-            const bool v = tile * kTile + r * kBlock + t < nv;
-            const uint32_t d = (kk[r] >> sh) & dm;
-            const uint64_t peers = digit_peers(v, d, width);
-            if (v && (peers & lanemask_lt(lane)) == 0) atomicAdd(&lh[d], (uint32_t)__popcll(peers));
+    for (uint32_t r = 0; r < kRows; ++r) {
+        const uint64_t i = (uint64_t)b * kTile + r * kBlock + t;
+        stv[r] = i < a.n ? a.status[i] : (int8_t)RSK_RECV_DROP;
+        cmv[r] = i < a.n && barrier ? a.cmd[i] : (uint8_t)RSK_CMD_DATA;
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < kRows; ++r) {
+        const bool valid = stv[r] == RSK_RECV_VALID;
+        const bool ctrl = valid && cmv[r] != RSK_CMD_DATA;
+        const uint64_t bv = __ballot(valid), bc = __ballot(ctrl);
+        if (lane == 0u) {
+            mv[r][w] = bv;
+            mc[r][w] = bc;
+        }
+        flags |= (valid ? 1u << r : 0u) | (ctrl ? 1u << (16 + r) : 0u);
+    }
+    __syncthreads();
+    uint32_t ov[kRows], oc[kRows], av, ac;
+    tile_offsets(mv, w, ov, av);
+    tile_offsets(mc, w, oc, ac);
+    if (w == 0u) {
+        const uint32_t e = dlb_wave(st_v, b, av, lane);
+        if (lane == 0u) {
+            pre[0] = e;
+            if (b == gridDim.x - 1u) *nvp = e + av;
+        }
+    } else if (w == 1u) {
+        const uint32_t e = dlb_wave(st_c, b, ac, lane);
+        if (lane == 0u) pre[1] = e;
+    }
+    __syncthreads();
+    const uint64_t lt = lanemask_lt(lane);
+#pragma unroll
+    for (uint32_t r = 0; r < kRows; ++r) {
+        if (!((flags >> r) & 1u)) continue;
+        const uint32_t i = b * kTile + r * kBlock + t;
+        const uint32_t j = pre[0] + ov[r] + (uint32_t)__popcll(mv[r][w] & lt);
+        cidx[j] = i;
+        cep[j] = ((flags >> (16 + r)) & 1u) ? kCtrl : pre[1] + oc[r] + (uint32_t)__popcll(mc[r][w] & lt);
+    }
+}
+
+// leader + scan + rank in one pass: lead_of[j] = the first packet of j's key (tmin of its slot, or j
+// for a control packet); the leaders' dense ranks (segment ids in first-occurrence order) by
+// decoupled look-back; rank_at[leader], seg_first[rank]; the last tile writes the segment count.
+// Block 0 also clears the radix digit histograms the next launch accumulates.
+__global__ __launch_bounds__(kBlock) void k_dm_leader_rank(const uint32_t *nvp, const uint32_t *hslot,
+                                                           const uint32_t *tmin, const uint32_t *cidx,
+                                                           unsigned long long *st_l, uint32_t *lead_of,
+                                                           uint32_t *rank_at, uint32_t *seg_first, uint32_t *nsegp,
+                                                           uint32_t *ghist) {
+    __shared__ uint64_t ml[kRows][kWaves];
+    __shared__ uint32_t pre;
+    const uint32_t nv = *nvp;
+    const uint32_t b = blockIdx.x, t = threadIdx.x, w = t >> 6, lane = t & 63u;
+    if (b == 0u)
+        for (uint32_t q = t; q < 4u * 256u; q += kBlock) ghist[q] = 0u;
+    uint32_t isl = 0;  // bit r: row r's item is its key's leader
+    uint32_t hs[kRows];
+#pragma unroll
+    for (uint32_t r = 0; r < kRows; ++r) {
+        const uint32_t j = b * kTile + r * kBlock + t;
+        hs[r] = j < nv ? hslot[j] : kNone;
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < kRows; ++r) {
+        const uint32_t j = b * kTile + r * kBlock + t;
+        bool l = false;
+        if (j < nv) {
+            const uint32_t lead = hs[r] == kNone ? j : tmin[hs[r]];
+            lead_of[j] = lead;
+            l = lead == j;
+        }
+        const uint64_t bl = __ballot(l);
+        if (lane == 0u) ml[r][w] = bl;
+        isl |= l ? 1u << r : 0u;
+    }
+    __syncthreads();
+    uint32_t ol[kRows], al;
+    tile_offsets(ml, w, ol, al);
+    if (w == 0u) {
+        const uint32_t e = dlb_wave(st_l, b, al, lane);
+        if (lane == 0u) {
+            pre = e;
+            if (b == gridDim.x - 1u) *nsegp = e + al;
         }
     }
     __syncthreads();
-    hist[t * nt + tile] = lh[t];  // bins >= 2^width stay 0
+    const uint64_t lt = lanemask_lt(lane);
+#pragma unroll
+    for (uint32_t r = 0; r < kRows; ++r) {
+        if (!((isl >> r) & 1u)) continue;
+        const uint32_t j = b * kTile + r * kBlock + t;
+        const uint32_t rk = pre + ol[r] + (uint32_t)__popcll(ml[r][w] & lt);
+        rank_at[j] = rk;
+        seg_first[rk] = cidx[j];
+    }
 }
 
-// Stable scatter of one tile: rank every item among the tile's equal digits (16 rounds of 256, in
-// input order), place it at its tile-local sorted position in LDS, then write the tile out digit
-// run by digit run — consecutive threads, consecutive addresses — so global stores are contiguous
-// runs instead of 4-B scatters (partially written sectors cost read-modify-write).
-__global__ __launch_bounds__(kBlock) void k_dm_scatter(uint32_t pass, const uint32_t *nvp, const uint32_t *nsegp,
-                                                       const uint32_t *kin, const uint32_t *vin,
-                                                       const uint32_t *hoff, uint32_t nt, uint32_t *kout,
-                                                       uint32_t *vout) {
+// segof + the global digit histograms of every radix pass: keys[j] = segment id of compacted packet
+// j, vals[j] = its packet index; one tile of kTile packets per block, LDS histograms per pass, one
+// global atomic per non-empty bin.
+__global__ __launch_bounds__(kBlock) void k_dm_segof_hist(const uint32_t *nvp, const uint32_t *nsegp,
+                                                          const uint32_t *lead_of, const uint32_t *rank_at,
+                                                          const uint32_t *cidx, uint32_t *keys, uint32_t *vals,
+                                                          uint32_t *ghist) {
+    __shared__ uint32_t lh[4][256];
+    const uint32_t nv = *nvp, ns = *nsegp, t = threadIdx.x, lane = t & 63u;
+    const uint32_t base = blockIdx.x * kTile;
+    if (base >= nv) return;  // block-uniform
+    const uint32_t np = n_passes(ns), width = digit_width(ns), dm = (1u << width) - 1u;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) lh[p][t] = 0u;
+    __syncthreads();
+    uint32_t kk[kItems], ld[kItems];  // all lead_of loads, then all rank_at gathers, in flight at once
+#pragma unroll
+    for (uint32_t r = 0; r < kItems; ++r) {
+        const uint32_t j = base + r * kBlock + t;
+        ld[r] = j < nv ? lead_of[j] : 0u;
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < kItems; ++r) {
+        const uint32_t j = base + r * kBlock + t;
+        kk[r] = j < nv ? rank_at[ld[r]] : 0u;
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < kItems; ++r) {
+        const uint32_t j = base + r * kBlock + t;
+        if (j < nv) {
+            keys[j] = kk[r];
+            vals[j] = cidx[j];  // the packet index rides through the sort
+        }
+    }
+    for (uint32_t p = 0; p < np; ++p) {  // np is block-uniform
+#pragma unroll
+        for (uint32_t r = 0; r < kItems; ++r) {
+            const bool v = base + r * kBlock + t < nv;
+            const uint32_t d = (kk[r] >> (width * p)) & dm;
+            const uint64_t peers = digit_peers(v, d, width);
+            if (v && (peers & lanemask_lt(lane)) == 0) atomicAdd(&lh[p][d], (uint32_t)__popcll(peers));
+        }
+    }
+    __syncthreads();
+    for (uint32_t p = 0; p < np; ++p)
+        if (lh[p][t]) atomicAdd(ghist + 256u * p + t, lh[p][t]);
+}
+
+// One radix pass, onesweep: tile t (= block t, dispatch order) counts its digits, gets the count of
+// each digit in tiles before it by per-digit decoupled look-back, adds the digit's global start
+// (exclusive scan of the pass's global histogram), ranks its items stably in LDS and writes the tile
+// out digit run by digit run (consecutive threads, consecutive addresses).
+__global__ __launch_bounds__(kBlock) void k_dm_onesweep(uint32_t pass, const uint32_t *nvp, const uint32_t *nsegp,
+                                                        const uint32_t *kin, const uint32_t *vin, const uint32_t *ghist,
+                                                        unsigned long long *st, uint32_t *kout, uint32_t *vout) {
     __shared__ uint32_t run[256], lbase[256], dbase[256];
     __shared__ uint32_t wcnt[kWaves][256];
     __shared__ uint32_t sk[kTile], sv[kTile];
-    const uint32_t nv = *nvp, ns = *nsegp, tile = xcd_tile(blockIdx.x, gridDim.x);
-    if (pass >= n_passes(ns) || tile * kTile >= nv) return;  // block-uniform
+    const uint32_t nv = *nvp, ns = *nsegp, tile = blockIdx.x;
+    if (pass >= n_passes(ns) || tile * kTile >= nv) return;  // block-uniform; no later tile waits on these
     const uint32_t width = digit_width(ns), sh = width * pass, dm = (1u << width) - 1u;
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     const uint32_t base = tile * kTile;
@@ -415,9 +563,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_scatter(uint32_t pass, const uint
     run[t] = 0;
 #pragma unroll
     for (int q = 0; q < kWaves; ++q) wcnt[q][t] = 0;
-    dbase[t] = hoff[t * nt + tile];  // this tile's first global slot for digit t
     __syncthreads();
-    // the thread's 16 items, all loads in flight at once (the rounds below are barrier-separated)
     uint32_t kk[kItems], vv[kItems];
 #pragma unroll
     for (uint32_t r = 0; r < kItems; ++r) {
@@ -425,7 +571,6 @@ __global__ __launch_bounds__(kBlock) void k_dm_scatter(uint32_t pass, const uint
         kk[r] = k < nv ? kin[k] : 0u;
         vv[r] = k < nv ? vin[k] : 0u;
     }
-    // tile histogram -> tile-local exclusive bases
 #pragma unroll
     for (uint32_t r = 0; r < kItems; ++r) {
         const bool v = base + r * kBlock + t < nv;
@@ -434,21 +579,37 @@ __global__ __launch_bounds__(kBlock) void k_dm_scatter(uint32_t pass, const uint
         if (v && (peers & lanemask_lt(lane)) == 0) atomicAdd(&run[d], (uint32_t)__popcll(peers));
     }
     __syncthreads();
-    if (w == 0) {  // exclusive scan of the 256 bins by wave 0 (4 per lane)
-        uint32_t c[4], s4 = 0;
+    // global position of this tile's first digit-t item: digits before t overall + digit t before this tile
+    const uint32_t before = dlb_digit(st + (uint64_t)pass * 256u * gridDim.x, tile, t, run[t]);
+    if (w == 0) {  // exclusive scans of the global histogram and of the tile's bins (4 per lane)
+        uint32_t g[4], c[4], gs = 0, cs = 0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) { c[q] = run[4 * lane + q]; s4 += c[q]; }
-        uint32_t inc = s4;
+        for (int q = 0; q < 4; ++q) {
+            g[q] = ghist[256u * pass + 4u * lane + q];
+            c[q] = run[4 * lane + q];
+            gs += g[q];
+            cs += c[q];
+        }
+        uint32_t gi = gs, ci = cs;
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t v = __shfl_up(inc, off);
-            if (lane >= (uint32_t)off) inc += v;
+            const uint32_t x = __shfl_up(gi, off), y = __shfl_up(ci, off);
+            if (lane >= (uint32_t)off) {
+                gi += x;
+                ci += y;
+            }
         }
-        uint32_t acc = inc - s4;
+        uint32_t ga = gi - gs, ca = ci - cs;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) { lbase[4 * lane + q] = acc; acc += c[q]; }
+        for (int q = 0; q < 4; ++q) {
+            dbase[4 * lane + q] = ga;
+            lbase[4 * lane + q] = ca;
+            ga += g[q];
+            ca += c[q];
+        }
     }
     __syncthreads();
+    dbase[t] += before;
     run[t] = 0;
     __syncthreads();
 #pragma unroll
@@ -507,15 +668,14 @@ __global__ __launch_bounds__(kBlock) void k_dm_final(const uint32_t *nvp, const 
 
 // ---- workspace ------------------------------------------------------------------------------
 struct DmWs {
-    uint64_t *mv, *mc, *ml;
-    uint32_t *cv, *ov, *cc, *oc, *cl, *ol;
     uint32_t *cidx, *cep, *hslot, *lead_of, *rank_at;
     uint32_t *kA, *vA, *kB, *vB;
-    unsigned long long *slots;
+    uint32_t *ghist;
+    unsigned long long *slots;  // slots | tmin | look-back states: one 0xff fill per call
     uint32_t *tmin;
-    uint32_t *hist, *hoff;
+    unsigned long long *st_v, *st_c, *st_l, *st_r;
+    size_t fill_bytes;
     uint32_t *nv, *nseg;
-    ScanWs scan;
     uint32_t nb, nt, tsize;
 };
 
@@ -527,7 +687,6 @@ uint32_t table_size(uint32_t n) {  // power of two >= 2 n (n <= 2^30, checked by
 
 size_t dm_layout(uint32_t n, uint8_t *base, DmWs *w) {
     const uint32_t nb = (n + kBlock - 1) / kBlock, nt = (n + kTile - 1) / kTile, T = table_size(n);
-    const uint32_t nh = 256u * nt, nc = (nh > nb ? nh : nb) / kScanChunk + 2;
     size_t off = 0;
     auto take = [&](size_t bytes) -> uint8_t * {
         uint8_t *p = base ? base + off : nullptr;
@@ -535,15 +694,6 @@ size_t dm_layout(uint32_t n, uint8_t *base, DmWs *w) {
         return p;
     };
     DmWs d;
-    d.mv = (uint64_t *)take(8ull * nb * kWaves);
-    d.mc = (uint64_t *)take(8ull * nb * kWaves);
-    d.ml = (uint64_t *)take(8ull * nb * kWaves);
-    d.cv = (uint32_t *)take(4ull * nb);
-    d.ov = (uint32_t *)take(4ull * nb);
-    d.cc = (uint32_t *)take(4ull * nb);
-    d.oc = (uint32_t *)take(4ull * nb);
-    d.cl = (uint32_t *)take(4ull * nb);
-    d.ol = (uint32_t *)take(4ull * nb);
     d.cidx = (uint32_t *)take(4ull * n);
     d.cep = (uint32_t *)take(4ull * n);
     d.hslot = (uint32_t *)take(4ull * n);
@@ -553,14 +703,17 @@ size_t dm_layout(uint32_t n, uint8_t *base, DmWs *w) {
     d.vA = (uint32_t *)take(4ull * n);
     d.kB = (uint32_t *)take(4ull * n);
     d.vB = (uint32_t *)take(4ull * n);
-    d.slots = (unsigned long long *)take(8ull * T);
-    d.tmin = (uint32_t *)take(4ull * T);
-    d.hist = (uint32_t *)take(4ull * nh);
-    d.hoff = (uint32_t *)take(4ull * nh);
-    d.scan.sums = (uint32_t *)take(4ull * nc);
-    d.scan.sum_off = (uint32_t *)take(4ull * nc);
+    d.ghist = (uint32_t *)take(4ull * 4 * 256);
     d.nv = (uint32_t *)take(8);
     d.nseg = (uint32_t *)take(8);
+    const size_t fill0 = off;
+    d.slots = (unsigned long long *)take(8ull * T);
+    d.tmin = (uint32_t *)take(4ull * T);
+    d.st_v = (unsigned long long *)take(8ull * nt);
+    d.st_c = (unsigned long long *)take(8ull * nt);
+    d.st_l = (unsigned long long *)take(8ull * nt);
+    d.st_r = (unsigned long long *)take(8ull * 4 * 256 * nt);
+    d.fill_bytes = off - fill0;
     d.nb = nb;
     d.nt = nt;
     d.tsize = T;
@@ -605,22 +758,18 @@ extern "C" int rsk_demux_batch(rsk_ctx *c, uint32_t n, const rsk_demux_in *in, u
     a.dst = in->dst;
     a.n = n;
     a.fields = fields;
-    hipError_t e = hipMemsetAsync(w.slots, 0xff, 12ull * w.tsize, s);  // slots + tmin (adjacent)
+    // one fill: the key table (slots, tmin) and every look-back state word start as all-ones
+    hipError_t e = hipMemsetAsync(w.slots, 0xff, w.fill_bytes, s);
     if (e != hipSuccess) { rsk::set_error("hipMemsetAsync(table)", e); return RSK_EDEVICE; }
     const uint32_t nb = w.nb;
-    hipLaunchKernelGGL(k_dm_flags, dim3(nb), dim3(kBlock), 0, s, a, w.mv, w.cv, w.mc, w.cc);
-    if ((r = rsk::launch_check("k_dm_flags"))) return r;
-    if ((r = scan_u32(w.cv, w.ov, nb, w.nv, w.scan, s))) return r;
-    if ((r = scan_u32(w.cc, w.oc, nb, nullptr, w.scan, s))) return r;
-    hipLaunchKernelGGL(k_dm_prep, dim3(nb), dim3(kBlock), 0, s, a, w.mv, w.ov, w.mc, w.oc, w.cidx, w.cep);
+    hipLaunchKernelGGL(k_dm_flags_prep, dim3(w.nt), dim3(kBlock), 0, s, a, w.st_v, w.st_c, w.cidx, w.cep, w.nv);
     hipLaunchKernelGGL(k_dm_insert, dim3((n + kInsTile - 1) / kInsTile), dim3(kBlock), 0, s, a, w.nv, w.cidx,
                        w.cep, w.slots, w.tmin, w.tsize - 1u, w.hslot);
-    hipLaunchKernelGGL(k_dm_leader, dim3(nb), dim3(kBlock), 0, s, w.nv, w.hslot, w.tmin, w.lead_of, w.ml, w.cl);
-    if ((r = rsk::launch_check("k_dm_leader"))) return r;
-    if ((r = scan_u32(w.cl, w.ol, nb, w.nseg, w.scan, s))) return r;
-    hipLaunchKernelGGL(k_dm_rank, dim3(nb), dim3(kBlock), 0, s, w.nv, w.ml, w.ol, w.cidx, w.rank_at, out->seg_first);
-    hipLaunchKernelGGL(k_dm_segof, dim3(nb), dim3(kBlock), 0, s, w.nv, w.lead_of, w.rank_at, w.cidx, w.kA, w.vA);
-    if ((r = rsk::launch_check("k_dm_segof"))) return r;
+    hipLaunchKernelGGL(k_dm_leader_rank, dim3(w.nt), dim3(kBlock), 0, s, w.nv, w.hslot, w.tmin, w.cidx, w.st_l,
+                       w.lead_of, w.rank_at, out->seg_first, w.nseg, w.ghist);
+    hipLaunchKernelGGL(k_dm_segof_hist, dim3(w.nt), dim3(kBlock), 0, s, w.nv, w.nseg, w.lead_of, w.rank_at, w.cidx,
+                       w.kA, w.vA, w.ghist);
+    if ((r = rsk::launch_check("k_dm_segof_hist"))) return r;
     // passes for the worst case (every packet its own segment); surplus passes return at once
     uint32_t maxbits = 1;
     while (maxbits < 32 && (1ull << maxbits) < n) ++maxbits;
@@ -628,11 +777,9 @@ extern "C" int rsk_demux_batch(rsk_ctx *c, uint32_t n, const rsk_demux_in *in, u
     for (uint32_t p = 0; p < passes; ++p) {
         const uint32_t *kin = (p & 1u) ? w.kB : w.kA, *vin = (p & 1u) ? w.vB : w.vA;
         uint32_t *kout = (p & 1u) ? w.kA : w.kB, *vout = (p & 1u) ? w.vA : w.vB;
-        hipLaunchKernelGGL(k_dm_hist, dim3(w.nt), dim3(kBlock), 0, s, p, w.nv, w.nseg, kin, w.hist, w.nt);
-        if ((r = scan_u32(w.hist, w.hoff, 256u * w.nt, nullptr, w.scan, s))) return r;
-        hipLaunchKernelGGL(k_dm_scatter, dim3(w.nt), dim3(kBlock), 0, s, p, w.nv, w.nseg, kin, vin, w.hoff, w.nt,
+        hipLaunchKernelGGL(k_dm_onesweep, dim3(w.nt), dim3(kBlock), 0, s, p, w.nv, w.nseg, kin, vin, w.ghist, w.st_r,
                            kout, vout);
-        if ((r = rsk::launch_check("k_dm_scatter"))) return r;
+        if ((r = rsk::launch_check("k_dm_onesweep"))) return r;
     }
     hipLaunchKernelGGL(k_dm_final, dim3(nb), dim3(kBlock), 0, s, w.nv, w.nseg, w.kA, w.vA, w.kB, w.vB,
                        out->perm, out->seg_off, out->n_seg, out->n_valid);
