@@ -39,6 +39,7 @@ struct rsk_ctx {
     int sq_scan_variant = 0;
     // single-packet shim buffers
     ShimIO *shim_dev = nullptr;
+    uint2 *tag_dev = nullptr;  // 256-entry tag table (rsk::KeySched::tab)
     ShimIO *shim_host = nullptr;
     hipStream_t shim_stream = nullptr;
     std::mutex shim_mu;

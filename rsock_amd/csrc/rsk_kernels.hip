@@ -71,6 +71,36 @@ __device__ __forceinline__ uint64_t rdl64(uint64_t v, uint32_t j) {
     return (uint64_t)rdl((uint32_t)v, j) | ((uint64_t)rdl((uint32_t)(v >> 32), j) << 32);
 }
 
+// ---- the tag (util/rhash.cpp:20-41): MD5(key || payload[0]) depends on one payload byte, so a key
+// has 256 possible tags.  k_tag_table computes them once per context with the MD5 compression of
+// rsk_md5.h; every kernel that frames or verifies stages the 2-KB table into LDS (one entry per
+// thread of the 256-thread block, before any early exit) and looks the tag up with one ds_read_b64.
+// RSK_TAG_INLINE (A/B build only) computes the MD5 per lane instead.
+#ifndef RSK_TAG_INLINE
+__shared__ uint2 s_tags[256];
+#endif
+
+__device__ __forceinline__ void stage_tags(const KeySched &ks) {
+    static_assert(kBlock == 256, "one tag-table entry per thread");
+#ifndef RSK_TAG_INLINE
+    s_tags[threadIdx.x] = ks.tab[threadIdx.x];
+    __syncthreads();
+#else
+    (void)ks;
+#endif
+}
+
+__device__ __forceinline__ void tag_of(const KeySched &ks, uint32_t b, uint32_t &t0, uint32_t &t1) {
+#ifndef RSK_TAG_INLINE
+    (void)ks;
+    const uint2 t = s_tags[b & 255u];
+    t0 = t.x;
+    t1 = t.y;
+#else
+    rsk::md5_tag(ks, b, t0, t1);
+#endif
+}
+
 // Frame bytes 8..31 as words H[2..7] (bean/EncHead.cpp:9-24 field order; byte 30 reserved = 0,
 // byte 31 = payload[0], which belongs to the payload but shares the word).
 __device__ __forceinline__ void head_words(uint32_t cmd, uint32_t id0, uint32_t id1, uint32_t conv,
@@ -110,7 +140,7 @@ __device__ __forceinline__ Lane1 encode_phase1(const EncArgs &a, const KeySched 
                       : (P > RSK_MAX_PAYLOAD ? RSK_SEND_OVERSIZE : (int32_t)(RSK_HEAD_SIZE + P));
         if (L.st > 0) {
             const uint32_t b0 = TAG ? a.payload[L.po] : 0u;
-            if (TAG) rsk::md5_tag(ks, b0, L.H[0], L.H[1]);
+            if (TAG) tag_of(ks, b0, L.H[0], L.H[1]);
             uint32_t id0 = a.id_lo, id1 = a.id_hi;
             if (a.id) {
                 const uint2 v = *reinterpret_cast<const uint2 *>(a.id + 8 * i);
@@ -130,7 +160,7 @@ __device__ __forceinline__ Lane1 encode_phase1(const EncArgs &a, const KeySched 
 __device__ __forceinline__ void encode_tag(const EncArgs &a, const KeySched &ks, Lane1 &L) {
     if (L.st > 0) {
         const uint32_t b0 = a.payload[L.po];
-        rsk::md5_tag(ks, b0, L.H[0], L.H[1]);
+        tag_of(ks, b0, L.H[0], L.H[1]);
         L.H[7] |= b0 << 24;
     }
 }
@@ -349,7 +379,7 @@ __device__ __forceinline__ void copy_pkt(const EncArgs &a, const KeySched &ks, c
         }
         uint32_t t0 = 0, t1 = 0;
         if constexpr (TAG) {
-            rsk::md5_tag(ks, my_b0, t0, t1);
+            tag_of(ks, my_b0, t0, t1);
         } else {
             // lane p stores the header chunks of its slot packet (store_head) beside the payload
             // chunks, so each frame's first line is written whole while it is in L2
@@ -530,6 +560,7 @@ template <int MODE, int PU, int U, int NT>
 __global__ __launch_bounds__(kBlock) void k_encode(EncArgs a, KeySched ks) {
     __shared__ CopyRec recs[kWavesPerBlock][64];
     __shared__ uint32_t cend[kWavesPerBlock][64];
+    stage_tags(ks);
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     const uint64_t base = ((uint64_t)blockIdx.x * kWavesPerBlock + w) * 64u;
     if (base >= a.n) return;  // wave-uniform; no block barriers below
@@ -795,7 +826,7 @@ __device__ __forceinline__ void copy_wire_pkt_dpp(const EncArgs &a, const KeySch
         uint32_t dsum = 0;  // TAG: lane p, checksum share of the bytes it adds to packet p's prefix image
         if constexpr (TAG) {
             uint32_t t0, t1;
-            rsk::md5_tag(ks, pw[0] & 0xffu, t0, t1);
+            tag_of(ks, pw[0] & 0xffu, t0, t1);
             uint32_t D[G::NPW];
 #pragma unroll
             for (int q = 0; q < G::NPW; ++q) D[q] = 0;
@@ -1106,6 +1137,7 @@ __device__ __forceinline__ void encode_wire_set(const EncArgs &a, const WireArgs
 
 template <int E, int MODE, int PU, int U>
 __global__ __launch_bounds__(kBlock) void k_encode_wire(EncArgs a, WireArgs wa, KeySched ks) {
+    stage_tags(ks);
     encode_wire_set<E, MODE, PU, U>(a, wa, ks);
 }
 
@@ -1114,6 +1146,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_wire(EncArgs a, WireArgs wa, 
 template <int E, int MODE, int PU, int U>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_encode_wire_w4(
     EncArgs a, WireArgs wa, KeySched ks) {
+    stage_tags(ks);
     encode_wire_set<E, MODE, PU, U>(a, wa, ks);
 }
 
@@ -1150,7 +1183,7 @@ __device__ __forceinline__ Dec decode_frame_t(const uint8_t *base, int nread, bo
         if ((int)len <= nread - 8 && dl > 0) {              // DecodeBuf ok, hash_equal len > 0
             const uint32_t b = (SLOT || len == (uint32_t)RSK_ENC_HEAD_SIZE) ? (w[7] >> 24) : base[8 + len];
             uint32_t t0, t1;
-            rsk::md5_tag(ks, b, t0, t1);
+            tag_of(ks, b, t0, t1);
             if (t0 == w[0] && t1 == w[1]) {
                 o.st = RSK_RECV_VALID;
                 o.hlen = len;
@@ -1222,6 +1255,7 @@ struct DecArgs {
 };
 
 __global__ __launch_bounds__(kBlock) void k_decode(DecArgs a, DecOut d, KeySched ks) {
+    stage_tags(ks);
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     bool valid = false;
     if (i < a.n) {
@@ -1235,6 +1269,7 @@ __global__ __launch_bounds__(kBlock) void k_decode(DecArgs a, DecOut d, KeySched
 
 // Header-only decode: 32-B slots (frame bytes [0, 31) + the hashed byte), one lane per frame.
 __global__ __launch_bounds__(kBlock) void k_decode_hdr(DecArgs a, DecOut d, KeySched ks) {
+    stage_tags(ks);
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     bool valid = false;
     if (i < a.n) {
@@ -1260,6 +1295,7 @@ struct EncHdrArgs {
 };
 
 __global__ __launch_bounds__(kBlock) void k_encode_hdr(EncHdrArgs a, KeySched ks) {
+    stage_tags(ks);
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= a.n) return;
     const uint32_t P = a.pay_len[i];
@@ -1267,7 +1303,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_hdr(EncHdrArgs a, KeySched ks
     uint32_t H[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (st > 0) {  // RConn.cpp:88-105
         const uint32_t b0 = a.b0[i];
-        rsk::md5_tag(ks, b0, H[0], H[1]);
+        tag_of(ks, b0, H[0], H[1]);
         uint32_t id0 = a.id_lo, id1 = a.id_hi;
         if (a.id) {
             const uint2 v = *reinterpret_cast<const uint2 *>(a.id + 8 * i);
@@ -1405,6 +1441,7 @@ __device__ __forceinline__ bool store_parse(const ParseArgs &a, const DecOut &d,
 
 template <int L, bool SLOT>
 __global__ __launch_bounds__(kBlock) void k_parse_decode(ParseArgs a, DecOut d, KeySched ks) {
+    stage_tags(ks);
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     bool valid = false;
     if (i < a.n) {
@@ -1437,6 +1474,7 @@ struct SyncArgs {
 };
 
 __global__ __launch_bounds__(kBlock) void k_syncinput_decode(SyncArgs a, DecOut d, KeySched ks) {
+    stage_tags(ks);
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     bool valid = false;
     if (i < a.n) {
@@ -1622,6 +1660,7 @@ __global__ __launch_bounds__(kBlock) void k_capture_filter(FiltArgs a, DecOut d,
 template <int L>
 __global__ __launch_bounds__(kBlock) void k_filter_parse_decode(ParseArgs a, DecOut d, KeySched ks, uint8_t *match,
                                                                 rsk_capture_filter f) {
+    stage_tags(ks);
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     bool valid = false;
     if (i < a.n) {
@@ -1789,6 +1828,13 @@ __global__ void k_shim(ShimIO *io, int op, int len_arg, KeySched ks) {
         for (int q = 0; q < 23; ++q) b[32 + q] = b[q];
         io->ret = (int)len;
     }
+}
+
+// The context's 256 tags (see stage_tags): lane b = MD5(key || b)[8..15].
+__global__ __launch_bounds__(256) void k_tag_table(KeySched ks, uint2 *tab) {
+    uint32_t t0, t1;
+    rsk::md5_tag(ks, threadIdx.x, t0, t1);
+    tab[threadIdx.x] = make_uint2(t0, t1);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1980,6 +2026,23 @@ rsk_ctx *rsk_create(const uint8_t *key, uint32_t key_len, int device) {
     c->device = device;
     c->key.assign(key, key + key_len);
     build_sched(c->key.data(), key_len, c->ks);
+    DeviceGuard g(device);
+    hipStream_t s = nullptr;
+    e = g.ok ? hipMalloc(&c->tag_dev, 256 * sizeof(uint2)) : hipErrorInvalidDevice;
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_tag_table, dim3(1), dim3(256), 0, s, c->ks, c->tag_dev);
+        e = hipGetLastError();
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+    }
+    if (s) (void)hipStreamDestroy(s);
+    if (e != hipSuccess) {
+        set_error("rsk_create: tag table", e);
+        if (c->tag_dev) (void)hipFree(c->tag_dev);
+        delete c;
+        return nullptr;
+    }
+    c->ks.tab = c->tag_dev;
     return c;
 }
 
@@ -1988,6 +2051,7 @@ void rsk_destroy(rsk_ctx *c) {
     DeviceGuard g(c->device);
     rsk::free_ws(c);
     if (c->shim_dev) (void)hipFree(c->shim_dev);
+    if (c->tag_dev) (void)hipFree(c->tag_dev);
     if (c->shim_host) (void)hipHostFree(c->shim_host);
     if (c->shim_stream) (void)hipStreamDestroy(c->shim_stream);
     delete c;

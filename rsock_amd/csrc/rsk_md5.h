@@ -81,6 +81,9 @@ struct KeySched {
     int32_t bshift;    // bit position of payload[0] inside that word
     int32_t two_blocks;
     int32_t _pad0;
+    // Device table of the 256 tags this key can produce (tag = f(key, payload[0]) only): entry b =
+    // (t0, t1) for payload[0] = b, built on the GPU by k_tag_table at rsk_create.
+    const uint2 *tab;
 };
 
 // Tag words (digest bytes 8..11 and 12..15, little-endian) for payload byte b.

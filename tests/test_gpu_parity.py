@@ -268,6 +268,29 @@ def test_all_first_bytes(codec, gpu, oracle):
         assert fr[b * 48: b * 48 + 8].tobytes() == oracle.tag(KEY, b)
 
 
+def test_tag_tables_per_context(gpu, oracle):
+    """Each context frames with its own key's tag table, with several contexts alive at once."""
+    from rsock_amd.codec import Codec
+
+    keys = [b"", b"k", b"hello135", bytes(range(60)), bytes(range(100, 230))]
+    cxs = [Codec(k, 0) for k in keys]
+    try:
+        n = 256
+        payload = np.arange(256, dtype=np.uint8).repeat(16)
+        pay_off = (np.arange(n) * 16).astype(np.uint64)
+        plen = np.full(n, 16, np.uint16)
+        frame_off = (np.arange(n) * 48).astype(np.uint64)
+        z = np.zeros(n, np.uint8)
+        for k, cx in reversed(list(zip(keys, cxs))):
+            fr, _ = run_encode(cx, gpu, payload, pay_off, plen, z, z.astype(np.uint32), z.astype(np.uint64),
+                               frame_off, n * 48)
+            for b in (0, 1, 127, 128, 255):
+                assert fr[b * 48: b * 48 + 8].tobytes() == oracle.tag(k, b)
+    finally:
+        for cx in cxs:
+            cx.close()
+
+
 @pytest.mark.parametrize("klen", [0, 1, 7, 8, 9, 53, 54, 55, 56, 62, 63, 64, 65, 100, 118, 119, 120, 127, 128, 200])
 def test_key_lengths(gpu, oracle, klen):
     """1-block, 2-block and midstate key schedules (util/rhash.cpp hashes key || payload[0])."""
@@ -282,6 +305,7 @@ def test_key_lengths(gpu, oracle, klen):
         pay_off = (np.arange(n) * 208).astype(np.uint64)
         frame_off = (np.arange(n) * 240).astype(np.uint64)
         payload = rng.integers(0, 256, n * 208, dtype=np.uint8)
+        payload[pay_off.astype(np.int64)] = np.arange(n) % 256  # every tag-table entry of this key
         cmd, conv, ckey = _rand_fields(rng, n)
         fr, st = run_encode(cx, gpu, payload, pay_off, plen, cmd, conv, ckey, frame_off, n * 240)
 
