@@ -45,9 +45,10 @@ def dec_bytes_per_pkt() -> int:
     return 32 + 8 + 2 + 1 + 1 + 8 + 4 + 8 + 2 + 2 + 1 + 4
 
 
-def load_traffic(cfg: str, n: int) -> dict | None:
+def load_traffic(cfg: str, n: int, frame_pitch: int) -> dict | None:
     """HBM traffic per k_encode launch measured by tools/pmc_traffic.py (separate rocprofv3 --pmc
-    passes, gfx950 FETCH_SIZE x2 correction) for this (config, packets), if profiles/ holds one."""
+    passes, gfx950 FETCH_SIZE x2 correction) for this (config, packets, frame slot pitch), if
+    profiles/ holds one."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     if not os.path.exists(path):
         return None
@@ -57,7 +58,10 @@ def load_traffic(cfg: str, n: int) -> dict | None:
         return None
     if "config" in table:  # single-record form
         table = {f"{table['config']}:{table['packets']}": table}
-    return table.get(f"{cfg}:{n}")
+    rec = table.get(f"{cfg}:{n}")
+    if rec is None or rec.get("frame_pitch") != frame_pitch:
+        return None  # measured on another layout (or before the layout was recorded)
+    return rec
 
 
 def _cpu_quota() -> float | None:
@@ -256,7 +260,8 @@ def main() -> None:
         if ev is not None:
             ev[0].record(stream)
         cx.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
-                        w.status, id_uniform=workload.ID_UNIFORM, pad16=True, stream=stream)
+                        w.status, id_uniform=workload.ID_UNIFORM, pad16=d.pad == 16, pad128=d.pad == 128,
+                        stream=stream)
         if ev is not None:
             ev[1].record(stream)
         cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, w.dec, stream=stream)
@@ -299,7 +304,7 @@ def main() -> None:
     achieved = enc_bytes / (enc_ms * 1e-3) / 1e9
 
     if rank == 0:
-        tr = load_traffic(cfg, d.n)
+        tr = load_traffic(cfg, d.n, d.frame_pitch)
         line = {
             "metric": METRIC,
             "value": round(mpkts, 2),
@@ -319,6 +324,8 @@ def main() -> None:
                 "packets_per_gpu": d.n,
                 "packets_total": n_total if strong else world * d.n,
                 "payload_bytes": p,
+                "frame_slot_bytes": d.frame_pitch,
+                "zero_pad": d.pad,
                 "key": "hello135",
                 "parallelism": f"shard{world} (no collective)",
             },

@@ -374,6 +374,9 @@ __device__ __forceinline__ void copy_pkt(const EncArgs &a, const KeySched &ks, c
             for (int q = 0; q < 2; ++q) {
                 const int32_t m = (int32_t)(lane + 64u * q) - 2;
                 A[p][q] = make_uint4(0u, 0u, 0u, 0u);
+                // slot 1 (chunks 64..127; lane 0's source chunk is chunk 63's funnel partner) only
+                // for frames of 64 chunks or more: a uniform branch
+                if (q == 1 && nst[p] < 64u) continue;
                 if (on[p] && m >= 0 && src_chunk_live(m, g.first_rel, g.last_rel)) A[p][q] = ld16<NT>(g.srcp + 16 * m);
             }
         }
@@ -394,10 +397,15 @@ __device__ __forceinline__ void copy_pkt(const EncArgs &a, const KeySched &ks, c
             if (!on[p]) continue;
             uint4 B[2];
             B[0] = make_uint4(wave_shl1(A[p][0].x), wave_shl1(A[p][0].y), wave_shl1(A[p][0].z), wave_shl1(A[p][0].w));
-            B[1] = make_uint4(wave_shl1(A[p][1].x), wave_shl1(A[p][1].y), wave_shl1(A[p][1].z), wave_shl1(A[p][1].w));
-            const uint4 l0 = make_uint4(rdl(A[p][1].x, 0), rdl(A[p][1].y, 0), rdl(A[p][1].z, 0),
-                                        rdl(A[p][1].w, 0));  // read in uniform flow (see k_encode)
-            if (lane == 63u) B[0] = l0;
+            B[1] = make_uint4(0u, 0u, 0u, 0u);
+            if (nst[p] >= 64u) {  // uniform: the frame reaches slot 1
+                const uint4 l0 = make_uint4(rdl(A[p][1].x, 0), rdl(A[p][1].y, 0), rdl(A[p][1].z, 0),
+                                            rdl(A[p][1].w, 0));  // read in uniform flow (see k_encode)
+                if (lane == 63u) B[0] = l0;
+                if (nst[p] > 64u)
+                    B[1] = make_uint4(wave_shl1(A[p][1].x), wave_shl1(A[p][1].y), wave_shl1(A[p][1].z),
+                                      wave_shl1(A[p][1].w));
+            }
             uint32_t Hj[8];  // TAG: the packet's header words (SGPRs), tag and payload[0] from lane p
             if constexpr (TAG) {
 #pragma unroll
@@ -409,6 +417,7 @@ __device__ __forceinline__ void copy_pkt(const EncArgs &a, const KeySched &ks, c
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
                 const uint32_t k = lane + 64u * q;
+                if (q == 1 && nst[p] <= 64u) continue;  // uniform
                 if (k >= nst[p] || (!TAG && k < 2u)) continue;
                 const uint4 V = rsk::funnel16(A[p][q], B[q], sh[p]);
                 if constexpr (TAG) {
@@ -422,6 +431,145 @@ __device__ __forceinline__ void copy_pkt(const EncArgs &a, const KeySched &ks, c
                 }
             }
         }
+    }
+}
+
+// ---- software-pipelined per-packet copy: the chunk loads of the next PU packets are issued before
+// the current PU packets are shifted and stored, so each wave keeps a batch of loads in flight
+// while it stores (copy_pkt waits for its own loads, then stores, then loads again).  Two register
+// buffers of PU packets, the roles swapped by a 2x unrolled loop.  Every load instruction runs with
+// all lanes (a dead lane reads the arena's first chunk, which stays cached) so the batch's load
+// count is static and the wait for the older batch leaves the newer one in flight.
+template <int PU>
+__device__ __forceinline__ uint64_t take_batch(uint64_t &vm) {
+    uint64_t m = 0;
+#pragma unroll
+    for (int p = 0; p < PU; ++p) {
+        const uint64_t b = vm & (~vm + 1ull);
+        m |= b;
+        vm ^= b;
+    }
+    return m;
+}
+
+template <int PU>
+__device__ __forceinline__ void batch_slots(uint64_t bm, uint32_t lane, uint32_t (&js)[PU], bool (&on)[PU],
+                                            uint32_t &myj, bool &mine) {
+    myj = 0;
+    mine = false;
+#pragma unroll
+    for (int p = 0; p < PU; ++p) {
+        on[p] = bm != 0ull;
+        js[p] = on[p] ? (uint32_t)__builtin_ctzll(bm) : 0u;
+        if (on[p]) bm &= bm - 1ull;
+        if (lane == (uint32_t)p) {
+            myj = js[p];
+            mine = on[p];
+        }
+    }
+}
+
+template <int PU, int NT, bool TAG>
+__device__ __forceinline__ void pkt_issue(const EncArgs &a, const Lane1 &L, uint32_t lane, uint64_t bm,
+                                          uint4 (&A)[PU][2], uint32_t &b0) {
+    uint32_t js[PU], myj;
+    bool on[PU], mine;
+    batch_slots<PU>(bm, lane, js, on, myj, mine);
+    if constexpr (TAG) {  // payload[0] of the lane's slot packet, ahead of the chunk loads
+        const uint64_t po = shfl64(L.po, myj);
+        b0 = rsk::gptr(a.payload)[mine ? po : 0u];
+    }
+#pragma unroll
+    for (int p = 0; p < PU; ++p) {
+        const uint32_t flen = on[p] ? rdl((uint32_t)L.st, js[p]) : 0u;
+        const uint8_t *src = a.payload + rdl64(L.po, js[p]);
+        const FrameGeo g = frame_geo(src, a.frame + rdl64(L.fo, js[p]), flen, a.pad);
+        // a dead lane reads the aligned chunk that holds the packet's payload[0] (mapped, cached)
+        const uint8_t *dummy = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(src) & ~(uintptr_t)15);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int32_t m = (int32_t)(lane + 64u * q) - 2;
+            const bool live = on[p] && m >= 0 && src_chunk_live(m, g.first_rel, g.last_rel);
+            const uint4 v = ld16<NT>(live ? g.srcp + 16 * m : dummy);
+            A[p][q] = live ? v : make_uint4(0u, 0u, 0u, 0u);
+        }
+    }
+}
+
+template <int PU, int NT, bool TAG>
+__device__ __forceinline__ void pkt_store(const EncArgs &a, const KeySched &ks, const Lane1 &L, uint32_t lane,
+                                          uint64_t bm, const uint4 (&A)[PU][2], uint32_t my_b0) {
+    uint32_t js[PU], myj;
+    bool on[PU], mine;
+    batch_slots<PU>(bm, lane, js, on, myj, mine);
+    uint32_t t0 = 0, t1 = 0;
+    if constexpr (TAG) {
+        tag_of(ks, my_b0, t0, t1);
+    } else {  // lane p: the header chunks of its slot packet (store_head)
+        uint32_t H[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) H[t] = (uint32_t)__shfl((int)L.H[t], (int)myj);
+        const uint64_t my_fo = shfl64(L.fo, myj);
+        if (mine) store_head(H, a.frame + my_fo);
+    }
+#pragma unroll
+    for (int p = 0; p < PU; ++p) {
+        if (!on[p]) continue;
+        const uint32_t fl = rdl((uint32_t)L.st, js[p]);
+        const FrameGeo g = frame_geo(a.payload + rdl64(L.po, js[p]), a.frame + rdl64(L.fo, js[p]), fl, a.pad);
+        const uint32_t flen = fl + g.r, nst = g.nst;
+        uint4 B[2];
+        B[0] = make_uint4(wave_shl1(A[p][0].x), wave_shl1(A[p][0].y), wave_shl1(A[p][0].z), wave_shl1(A[p][0].w));
+        B[1] = make_uint4(0u, 0u, 0u, 0u);
+        if (nst >= 64u) {  // uniform: the frame reaches slot 1
+            const uint4 l0 = make_uint4(rdl(A[p][1].x, 0), rdl(A[p][1].y, 0), rdl(A[p][1].z, 0), rdl(A[p][1].w, 0));
+            if (lane == 63u) B[0] = l0;
+            if (nst > 64u)
+                B[1] = make_uint4(wave_shl1(A[p][1].x), wave_shl1(A[p][1].y), wave_shl1(A[p][1].z),
+                                  wave_shl1(A[p][1].w));
+        }
+        uint32_t Hj[8];
+        if constexpr (TAG) {
+#pragma unroll
+            for (int t = 2; t < 8; ++t) Hj[t] = rdl(L.H[t], js[p]);
+            Hj[0] = rdl(t0, (uint32_t)p);
+            Hj[1] = rdl(t1, (uint32_t)p);
+            Hj[7] |= rdl(my_b0, (uint32_t)p) << 24;
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const uint32_t k = lane + 64u * q;
+            if (q == 1 && nst <= 64u) continue;  // uniform
+            if (k >= nst || (!TAG && k < 2u)) continue;
+            const uint4 V = rsk::funnel16(A[p][q], B[q], g.sh);
+            if constexpr (TAG) {
+                const uint4 v = k < (g.r >= 2u ? 3u : 2u) ? head_chunk(Hj, k, g.r, V) : V;
+                store_piece<NT>(g.d0 + 16u * k, v, k == 0u ? g.r : 0u, (int)flen - 16 * (int)k, a.pad != 0u);
+            } else {
+                store_piece<NT>(g.d0 + 16u * k, V, k == 2u ? chunk2_lo(g.r) : 0u, (int)flen - 16 * (int)k,
+                                a.pad != 0u);
+            }
+        }
+    }
+}
+
+template <int PU, int NT, bool TAG>
+__device__ __forceinline__ void copy_pkt_pipe(const EncArgs &a, const KeySched &ks, const Lane1 &L, uint32_t lane,
+                                              uint64_t vm) {
+    uint4 A0[PU][2], A1[PU][2];
+    uint32_t b0a = 0, b0b = 0;
+    uint64_t cur = take_batch<PU>(vm);
+    if (!cur) return;
+    pkt_issue<PU, NT, TAG>(a, L, lane, cur, A0, b0a);
+    while (true) {
+        const uint64_t nxt = take_batch<PU>(vm);
+        if (nxt) pkt_issue<PU, NT, TAG>(a, L, lane, nxt, A1, b0b);
+        pkt_store<PU, NT, TAG>(a, ks, L, lane, cur, A0, b0a);
+        if (!nxt) break;
+        cur = take_batch<PU>(vm);
+        if (cur) pkt_issue<PU, NT, TAG>(a, L, lane, cur, A0, b0a);
+        pkt_store<PU, NT, TAG>(a, ks, L, lane, nxt, A1, b0b);
+        if (!cur) break;
     }
 }
 
@@ -519,7 +667,8 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
     for (int off = 32; off; off >>= 1) fl += __shfl_xor(fl, off);
     const uint32_t cnt = (uint32_t)__popcll(vm);
     const bool flat = MODE == 7 ? true : MODE == 8 ? false : fl < kFlatBelowMeanBytes * cnt;
-    const bool defer = MODE != 3 && MODE != 7 && !flat && fl >= kDeferTagMeanBytes * cnt;
+    // MODE 10 (A/B): as 9 with the tag in the copy loop for every per-packet set
+    const bool defer = MODE != 3 && MODE != 7 && !flat && (MODE == 10 || fl >= kDeferTagMeanBytes * cnt);
     if constexpr (MODE != 3 && MODE != 7) {  // the tag now, except for the sets whose copy loop takes it
         if (!defer) encode_tag(a, ks, L);
     }
@@ -545,6 +694,16 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
     // first slot store (lanes 0..2, words by readlane); the others by the slot lane (store_head).
     // Measured (A/B, profiles/r02_ab_head.json): C3 2.34 vs 2.55 ms with the first; C4 0.389 vs
     // 0.420 ms with the second.
+    if constexpr (MODE == 9 || MODE == 10) {  // software-pipelined per-packet copy (shipped: 9)
+        if (defer) {
+            if (nt) copy_pkt_pipe<PU, 2, true>(a, ks, L, lane, vm);
+            else copy_pkt_pipe<PU, 0, true>(a, ks, L, lane, vm);
+        } else {
+            if (nt) copy_pkt_pipe<PU, 2, false>(a, ks, L, lane, vm);
+            else copy_pkt_pipe<PU, 0, false>(a, ks, L, lane, vm);
+        }
+        return;
+    }
     if (defer) {
         if (nt) copy_pkt<PU, 2, true>(a, ks, L, lane, vm);
         else copy_pkt<PU, 0, true>(a, ks, L, lane, vm);
@@ -553,6 +712,62 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
         else copy_pkt<PU, 0, false>(a, ks, L, lane, vm);
     }
 }
+
+#ifdef RSK_AB
+// A/B build only: memory-side ceiling of the encode access pattern.  Same arenas, same per-packet
+// chunk counts, same store policy as k_encode, but every frame chunk k is a plain copy of aligned
+// source chunk k (no funnel, no header, no partial stores; the frame bytes are NOT the encoding).
+template <int PU>
+__global__ __launch_bounds__(kBlock) void k_copy_probe(EncArgs a) {
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint64_t base = ((uint64_t)blockIdx.x * kWavesPerBlock + w) * 64u;
+    if (base >= a.n) return;
+    const uint64_t i = base + lane;
+    uint64_t po = 0, fo = 0;
+    uint32_t P = 0;
+    if (i < a.n) {
+        po = a.pay_off[i];
+        fo = a.frame_off[i];
+        P = a.pay_len[i];
+        a.status[i] = (int32_t)(RSK_HEAD_SIZE + P);
+    }
+    uint64_t vm = __ballot(i < a.n && P > 0u && P <= (uint32_t)RSK_MAX_PAYLOAD);
+    while (vm) {
+        uint4 A[PU][2];
+        uint32_t js[PU], nch[PU], nsrc[PU];
+        bool on[PU];
+#pragma unroll
+        for (int p = 0; p < PU; ++p) {
+            on[p] = vm != 0ull;
+            js[p] = on[p] ? (uint32_t)__builtin_ctzll(vm) : 0u;
+            if (on[p]) vm &= vm - 1ull;
+            const uint32_t Pj = on[p] ? rdl(P, js[p]) : 0u;
+            const uintptr_t s0 = reinterpret_cast<uintptr_t>(a.payload + rdl64(po, js[p]));
+            const uintptr_t d0 = reinterpret_cast<uintptr_t>(a.frame + rdl64(fo, js[p]));
+            // aligned source chunks holding payload bytes; aligned frame chunks up to the padded end
+            nsrc[p] = on[p] ? (uint32_t)(((s0 & 15u) + Pj + 15u) >> 4) : 0u;
+            nch[p] = on[p] ? (uint32_t)(((d0 & 15u) + Pj + RSK_HEAD_SIZE + 15u) >> 4) : 0u;
+            const uint8_t *src = reinterpret_cast<const uint8_t *>(s0 & ~(uintptr_t)15);
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const uint32_t k = lane + 64u * q;
+                A[p][q] = make_uint4(0u, 0u, 0u, 0u);
+                if (k < nsrc[p]) A[p][q] = ld16<0>(src + 16u * k);
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < PU; ++p) {
+            uint8_t *dst = reinterpret_cast<uint8_t *>(reinterpret_cast<uintptr_t>(a.frame + rdl64(fo, js[p])) &
+                                                       ~(uintptr_t)15);
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const uint32_t k = lane + 64u * q;
+                if (k < nch[p]) st16<2>(dst + 16u * k, A[p][q]);
+            }
+        }
+    }
+}
+#endif
 
 // Tiled mapping: wave t takes packets [64t, 64t + 64) (coalesced descriptor loads; the co-resident
 // waves each stream their own region of the arenas).
@@ -1988,12 +2203,17 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 
 #ifdef RSK_AB
 // A/B build only: selects the encode kernel variant for in-process A/B runs (tools/ab_encode.py).
-// k_encode<MODE, PU, U, NT> (see encode_set): 0 = the shipped <6, 12, 4, -1>; 1 = tag always in
-// phase 1; 2 / 3 = 8 / 16 packets per per-packet iteration; 4 = 2 chunks per lane per flat
-// iteration; 5 / 6 = normal / nontemporal stores on every per-packet set; 7 = flat path only;
-// 8 = per-packet path only.  v + 100 * cap (cap 1..4): the same kernel held to `cap` blocks per CU by unused LDS.
+// k_encode<MODE, PU, U, NT> (see encode_set): 0 = the shipped <9, 4, 4, -1> (software-pipelined
+// per-packet copy, 4 packets per batch); 17 = round 2's first form <6, 12, 4, -1> (12 packets per
+// iteration, no pipelining); 1 = as 17 with the tag always in phase 1; 2 / 3 = 17 with 8 / 16
+// packets per iteration; 4 = 2 chunks per lane per flat iteration; 5 / 6 = normal / nontemporal
+// stores on every per-packet set; 7 = flat path only; 8 = per-packet path only (unpipelined);
+// 9 / 10 / 14 / 15 / 16 = pipelined with 6 / 8 / 3 / 5 / 2 packets per batch (11 = 4, shipped);
+// 12 / 13 = k_copy_probe (memory-side ceiling probe, wrong bytes) with 12 / 4 packets per batch;
+// 18 = shipped with the tag in the copy loop for every per-packet set.
+// v + 100 * cap (cap 1..4): the same kernel held to `cap` blocks per CU by unused LDS.
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
-    if (!c || v < 0 || v % 100 > 8 || v / 100 > 4) return RSK_EINVAL;
+    if (!c || v < 0 || v % 100 > 18 || v / 100 > 4) return RSK_EINVAL;
     c->enc_variant = v;
     return RSK_OK;
 }
@@ -2104,13 +2324,23 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         case 6: hipLaunchKernelGGL((k_encode<6, 12, 4, 2>), gd, bd, lds, st, a, c->ks); break;
         case 7: hipLaunchKernelGGL((k_encode<7, 12, 4, -1>), gd, bd, lds, st, a, c->ks); break;
         case 8: hipLaunchKernelGGL((k_encode<8, 12, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        default: hipLaunchKernelGGL((k_encode<6, 12, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 9: hipLaunchKernelGGL((k_encode<9, 6, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 10: hipLaunchKernelGGL((k_encode<9, 8, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 11: hipLaunchKernelGGL((k_encode<9, 4, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 12: hipLaunchKernelGGL((k_copy_probe<12>), gd, bd, lds, st, a); break;
+        case 13: hipLaunchKernelGGL((k_copy_probe<4>), gd, bd, lds, st, a); break;
+        case 14: hipLaunchKernelGGL((k_encode<9, 3, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 15: hipLaunchKernelGGL((k_encode<9, 5, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 16: hipLaunchKernelGGL((k_encode<9, 2, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 17: hipLaunchKernelGGL((k_encode<6, 12, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 18: hipLaunchKernelGGL((k_encode<10, 4, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        default: hipLaunchKernelGGL((k_encode<9, 4, 4, -1>), gd, bd, lds, st, a, c->ks); break;
     }
 #else
-    // the shipped kernel: per-wave hybrid (flat chunk list for short frames, one-load DPP per-packet
-    // copy with 12 packets per iteration for the rest), tag in the copy loop for long-frame sets,
-    // per-set store policy
-    hipLaunchKernelGGL((k_encode<6, 12, 4, -1>), gd, bd, 0, st, a, c->ks);
+    // the shipped kernel: per-wave hybrid (flat chunk list for short frames, software-pipelined
+    // one-load DPP per-packet copy, 4 packets per batch, for the rest), tag in the copy loop for
+    // long-frame sets, per-set store policy
+    hipLaunchKernelGGL((k_encode<9, 4, 4, -1>), gd, bd, 0, st, a, c->ks);
 #endif
     return launch_check("k_encode");
 }

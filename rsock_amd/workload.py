@@ -57,6 +57,10 @@ def round16(x: int) -> int:
     return (x + 15) & ~15
 
 
+def round128(x: int) -> int:
+    return (x + 127) & ~127
+
+
 @dataclass
 class Descriptors:
     """Host SoA descriptors for packets [lo, hi) of a config."""
@@ -72,6 +76,7 @@ class Descriptors:
     corrupt: np.ndarray  # bool: flip a tag bit before decode
     pay_pitch: int
     frame_pitch: int
+    pad: int  # zero-pad granularity the slots allow: 128 (line-aligned slots) or 16
     payload_seed: int
     first: int  # global index of packet 0 of this shard
 
@@ -105,7 +110,12 @@ def describe(name: str, lo: int = 0, hi: int | None = None, n: int | None = None
     # control bodies: conv reset carries a 4-byte conv, the others an 8-byte key
     plen = np.where(cmd == 1, np.uint16(4), np.where(cmd >= 2, np.uint16(8), plen)).astype(np.uint16)
     pay_pitch = round16(pmax)
-    frame_pitch = round16(HEAD + pmax) if frame_pitch is None else int(frame_pitch)
+    # Frame slots: frames of one length tile densely at 16-B granularity (every line is written
+    # whole by neighbouring frames); frames of mixed lengths get 128-B-aligned slots, zero-padded to
+    # the line (RSK_ENC_ZERO_PAD128), so no frame leaves a partly written line behind.
+    if frame_pitch is None:
+        frame_pitch = round16(HEAD + pmax) if pmin == pmax else round128(HEAD + pmax)
+    frame_pitch = int(frame_pitch)
     assert frame_pitch % 16 == 0 and frame_pitch >= HEAD + pmax
     local = np.arange(cnt, dtype=np.uint64)
     corrupt = (gi % np.uint64(corrupt_every) == np.uint64(7)) if corrupt_every else np.zeros(cnt, bool)
@@ -121,6 +131,7 @@ def describe(name: str, lo: int = 0, hi: int | None = None, n: int | None = None
         corrupt=corrupt,
         pay_pitch=pay_pitch,
         frame_pitch=frame_pitch,
+        pad=128 if frame_pitch % 128 == 0 else 16,
         payload_seed=(seed ^ PAYLOAD_SALT) & 0xFFFFFFFFFFFFFFFF,
         first=lo,
     )

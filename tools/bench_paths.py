@@ -55,7 +55,7 @@ def main():
     common = (w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key)
     ops = {
         "encode": lambda: cx.output_batch(*common, w.frame, w.frame_off, w.status, id_uniform=workload.ID_UNIFORM,
-                                          pad16=True, stream=s),
+                                          pad16=d.pad == 16, pad128=d.pad == 128, stream=s),
         "encode_wire_raw4": lambda: cx.output_wire_batch(*common, src, dst, sp, dp, seq, ack, flag, ipid, wire4, off4,
                                                          st4, id_uniform=workload.ID_UNIFORM, pad16=True, stream=s),
         "encode_wire_eth": lambda: cx.output_wire_batch(*common, src, dst, sp, dp, seq, ack, flag, ipid, wiree, offe,

@@ -4,7 +4,7 @@ tools/profile_box.sh) into per-launch HBM bytes for a kernel, with the gfx950 co
 MI355X_MICROARCH.md §HBM: both counters are in KiB; FETCH_SIZE reads half the bytes of a wide
 coalesced stream, so it is doubled (the kernel's dominant reads are 16-B/lane streams); WRITE_SIZE
 is exact for 16-B/lane stores.
-    python tools/pmc_traffic.py gpurun_out/r01 --kernel k_encode --config c3 --packets 4194304 \
+    python tools/pmc_traffic.py gpurun_out/r01 --kernel k_encode --config c3 --packets 4194304 --frame-pitch 1440 \
         [--out profiles/traffic.json]
 """
 import argparse
@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--packets", type=int, default=4194304)
     ap.add_argument("--algorithmic", type=float, default=0.0, help="algorithmic bytes per launch")
+    ap.add_argument("--frame-pitch", type=int, required=True, help="frame slot pitch of the profiled run")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     f, nf = per_launch(os.path.join(a.dir, "pmc_fetch", "pmc_counter_collection.csv"), a.kernel, "FETCH_SIZE")
@@ -38,7 +39,7 @@ def main():
     read_b = 2.0 * f * 1024.0
     write_b = w * 1024.0
     rec = {
-        "kernel": a.kernel, "config": a.config, "packets": a.packets,
+        "kernel": a.kernel, "config": a.config, "packets": a.packets, "frame_pitch": a.frame_pitch,
         "fetch_size_kib_raw": f, "write_size_kib_raw": w, "launches": [nf, nw],
         "read_bytes_per_launch": read_b, "write_bytes_per_launch": write_b,
         "bytes_per_launch": read_b + write_b,
