@@ -14,7 +14,8 @@
 //                   MD5 verify, SoA field stores, per-wave ballot mask + per-block count.
 //   k_parse_decode  RawTcp::RawInput (conn/RawTcp.cpp:138-244) fused with k_decode's body.
 //   k_capture_filter the pcap predicate of BuildFilterStr (cap/cap_util.cpp:67-144), SURVEY §8f-4.
-//   k_scan/k_scatter order-stable compaction of the VALID indices from the ballot masks.
+//   k_compact       order-stable VALID index list from the decode launches' per-wave ballots, one
+//                   pass (decoupled look-back over 4096-packet tiles).
 //   k_tcpinfo_encode 21-B TcpInfo hand-off records (bean/TcpInfo.cpp:20-32), staged through LDS.
 //   k_shim          the single-call shims (reference signatures) on a batch of one.
 //   k_fill_splitmix synthetic workload generator (bench/tests only).
@@ -1428,8 +1429,7 @@ struct DecOut {
     uint64_t *key;
     uint16_t *pay_off, *pay_len;
     int8_t *status;
-    uint64_t *masks;   // workspace: one ballot mask per wave (null: no compaction)
-    uint32_t *counts;  // workspace: VALID count per block
+    uint64_t *masks;  // compaction workspace: one VALID ballot per wave (null: no compaction)
 };
 
 __device__ __forceinline__ void store_dec(const DecOut &d, uint64_t i, const Dec &o) {
@@ -1443,22 +1443,58 @@ __device__ __forceinline__ void store_dec(const DecOut &d, uint64_t i, const Dec
     d.status[i] = (int8_t)o.st;
 }
 
-// Per-wave ballot of VALID + per-block count, consumed by k_scan / k_scatter.
-__device__ __forceinline__ void compact_epilogue(const DecOut &d, bool valid) {
-    __shared__ uint32_t wc[kWavesPerBlock];
-    const uint64_t m = __ballot(valid);
-    const uint32_t w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63u) == 0) {
-        d.masks[(uint64_t)blockIdx.x * kWavesPerBlock + w] = m;
-        wc[w] = (uint32_t)__popcll(m);
+// ---- order-stable compaction: the decode launch writes one VALID ballot per wave; k_compact turns
+// them into the VALID index list in one pass.  k_compact tile t covers 64 masks (4096 packets):
+// it counts them, scans them in one wave, finds the tile's prefix by decoupled look-back over the
+// tiles before it, and its lanes write their indices at prefix + rank (valid_idx in index order).
+// Tiles are dispatched in index order, so a tile only waits for tiles that are resident or done.
+// State word per tile: bits 63..48 the call's epoch, bit 47 inclusive, bits 31..0 the count; a
+// word from another call is not ready, so the state needs no per-call reset.  Device-scope relaxed
+// atomics (acquire / release would add an L2 write-back / invalidate per access, rsk_demux.hip);
+// a spin that outlives kCmpSpinMax reads gives up (wrong list, no hang).  Round 1 used k_scan (one
+// workgroup) + k_scatter; a look-back inside the decode launch itself (one word per 256-packet
+// block) was measured slower than both (C2: 40 us vs 31): the block-granular chain is the cost.
+constexpr unsigned long long kCmpIncl = 1ull << 47;
+constexpr uint32_t kCmpSpinMax = 1u << 22;
+
+__device__ __forceinline__ unsigned long long cmp_wait(unsigned long long *s, uint32_t epoch) {
+    unsigned long long v;
+    uint32_t spins = 0;
+    do {
+        v = __hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } while ((uint32_t)(v >> 48) != epoch && ++spins < kCmpSpinMax);
+    return (uint32_t)(v >> 48) == epoch ? v : kCmpIncl;
+}
+
+// all 64 lanes of one wave of tile b; agg uniform; returns b's exclusive prefix (uniform)
+__device__ uint32_t cmp_lookback(unsigned long long *st, uint32_t b, uint32_t agg, uint32_t lane, uint32_t epoch) {
+    const unsigned long long tag = (unsigned long long)epoch << 48;
+    if (b == 0u) {
+        if (lane == 0u) __hip_atomic_store(st, tag | kCmpIncl | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return 0u;
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t s = 0;
+    if (lane == 0u) __hip_atomic_store(st + b, tag | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t excl = 0;
+    for (int64_t top = (int64_t)b - 1;; top -= 64) {
+        const int64_t j = top - (int64_t)lane;
+        const unsigned long long v = j >= 0 ? cmp_wait(st + j, epoch) : kCmpIncl;  // before tile 0: 0
+        const uint64_t im = __ballot((v & kCmpIncl) != 0ull);
+        uint32_t val = (uint32_t)v;
+        if (im && lane > (uint32_t)__builtin_ctzll(im)) val = 0u;  // beyond the nearest inclusive word
 #pragma unroll
-        for (int q = 0; q < kWavesPerBlock; ++q) s += wc[q];
-        d.counts[blockIdx.x] = s;
+        for (int off = 32; off; off >>= 1) val += __shfl_xor(val, off);
+        excl += val;
+        if (im) break;
     }
+    if (lane == 0u)
+        __hip_atomic_store(st + b, tag | kCmpIncl | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return excl;
+}
+
+// The decode launches' epilogue: every thread calls it (no early exit before); i = its packet.
+__device__ __forceinline__ void compact_epilogue(const DecOut &d, bool valid, uint64_t i) {
+    const uint64_t m = __ballot(valid);
+    if ((threadIdx.x & 63u) == 0u) d.masks[i >> 6] = m;
 }
 
 struct DecArgs {
@@ -1479,7 +1515,7 @@ __global__ __launch_bounds__(kBlock) void k_decode(DecArgs a, DecOut d, KeySched
         store_dec(d, i, o);
         valid = o.st == RSK_RECV_VALID;
     }
-    if (d.masks) compact_epilogue(d, valid);
+    if (d.masks) compact_epilogue(d, valid, i);
 }
 
 // Header-only decode: 32-B slots (frame bytes [0, 31) + the hashed byte), one lane per frame.
@@ -1493,7 +1529,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_hdr(DecArgs a, DecOut d, KeyS
         store_dec(d, i, o);
         valid = o.st == RSK_RECV_VALID;
     }
-    if (d.masks) compact_epilogue(d, valid);
+    if (d.masks) compact_epilogue(d, valid, i);
 }
 
 // Header-only encode: frame bytes [0, 32) (tag, EncHead, payload[0]) per packet into 32-B slots.
@@ -1666,7 +1702,7 @@ __global__ __launch_bounds__(kBlock) void k_parse_decode(ParseArgs a, DecOut d, 
         uint32_t hw[16];
         valid = store_parse(a, d, i, parse_one<L, SLOT, false>(a, pkt, wl, cl, av, hw, ks));
     }
-    if (d.masks) compact_epilogue(d, valid);
+    if (d.masks) compact_epilogue(d, valid, i);
 }
 
 // ---- RawTcp::syncInput (conn/RawTcp.cpp:262-276) + RConn::OnRecv: the loop thread's side of
@@ -1717,7 +1753,7 @@ __global__ __launch_bounds__(kBlock) void k_syncinput_decode(SyncArgs a, DecOut 
         store_dec(d, i, o);
         valid = o.st == RSK_RECV_VALID;
     }
-    if (d.masks) compact_epilogue(d, valid);
+    if (d.masks) compact_epilogue(d, valid, i);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1866,7 +1902,7 @@ __global__ __launch_bounds__(kBlock) void k_capture_filter(FiltArgs a, DecOut d,
         m = filter_eval(k, f);
         a.match[i] = m ? 1 : 0;
     }
-    if (d.masks) compact_epilogue(d, m);
+    if (d.masks) compact_epilogue(d, m, i);
 }
 
 // Capture filter, then RawTcp::RawInput + RConn::OnRecv on the packets it passes, in one pass: the
@@ -1889,57 +1925,42 @@ __global__ __launch_bounds__(kBlock) void k_filter_parse_decode(ParseArgs a, Dec
         if (m) r = parse_one<L, false, true>(a, pkt, wl, cl, cl, k.w, ks);
         valid = store_parse(a, d, i, r);
     }
-    if (d.masks) compact_epilogue(d, valid);
+    if (d.masks) compact_epilogue(d, valid, i);
 }
 
-__global__ __launch_bounds__(1024) void k_scan(const uint32_t *counts, uint32_t *offsets, uint32_t nb,
-                                               uint32_t *n_valid) {
-    __shared__ uint32_t wsum[16];
-    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
-    uint32_t carry = 0;
-    for (uint32_t base = 0; base < nb; base += 4096u) {
-        const uint32_t idx = base + 4u * t;
-        uint32_t c[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) c[k] = idx + k < nb ? counts[idx + k] : 0u;
-        const uint32_t tsum = c[0] + c[1] + c[2] + c[3];
-        uint32_t inc = tsum;
+__global__ __launch_bounds__(kBlock) void k_compact(const uint64_t *masks, uint32_t nw, unsigned long long *st,
+                                                    uint32_t epoch, uint32_t *valid_idx, uint32_t *n_valid) {
+    __shared__ uint64_t ms[64];
+    __shared__ uint32_t mex[64];
+    __shared__ uint32_t pre;
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    const uint64_t mb = (uint64_t)blockIdx.x * 64u;
+    if (w == 0u) {
+        const uint64_t m = mb + lane < nw ? masks[mb + lane] : 0ull;
+        const uint32_t c = (uint32_t)__popcll(m);
+        uint32_t inc = c;
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
             const uint32_t v = __shfl_up(inc, off);
             if (lane >= (uint32_t)off) inc += v;
         }
-        if (lane == 63u) wsum[wv] = inc;
-        __syncthreads();
-        uint32_t wpre = 0, total = 0;
-#pragma unroll
-        for (uint32_t q = 0; q < 16; ++q) {
-            const uint32_t v = wsum[q];
-            wpre += q < wv ? v : 0u;
-            total += v;
+        ms[lane] = m;
+        mex[lane] = inc - c;
+        const uint32_t agg = (uint32_t)__shfl((int)inc, 63);
+        const uint32_t p = cmp_lookback(st, blockIdx.x, agg, lane, epoch);
+        if (lane == 0u) {
+            pre = p;
+            if (n_valid && blockIdx.x == gridDim.x - 1u) *n_valid = p + agg;
         }
-        uint32_t run = carry + wpre + inc - tsum;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (idx + k < nb) offsets[idx + k] = run;
-            run += c[k];
-        }
-        carry += total;
-        __syncthreads();  // wsum reused next pass
     }
-    if (t == 0 && n_valid) *n_valid = carry;
-}
-
-__global__ __launch_bounds__(kBlock) void k_scatter(const uint64_t *masks, const uint32_t *offsets,
-                                                    uint32_t *valid_idx) {
-    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    const uint64_t *mb = masks + (uint64_t)blockIdx.x * kWavesPerBlock;
-    uint32_t pos = offsets[blockIdx.x];
-    for (uint32_t q = 0; q < w; ++q) pos += (uint32_t)__popcll(mb[q]);
-    const uint64_t m = mb[w];
-    if ((m >> lane) & 1ull) {
-        pos += (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-        valid_idx[pos] = blockIdx.x * (uint32_t)kBlock + threadIdx.x;
+    __syncthreads();
+    if (!valid_idx) return;
+#pragma unroll 4
+    for (uint32_t r = 0; r < 16u; ++r) {
+        const uint32_t j = 4u * r + w;  // wave w takes masks w, w + 4, ... of the tile
+        const uint64_t m = ms[j];
+        if ((m >> lane) & 1ull)
+            valid_idx[pre + mex[j] + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)((mb + j) * 64u + lane);
     }
 }
 
@@ -2127,35 +2148,29 @@ thread_local char rsk::g_last_error[256] = "";
 
 namespace {
 
-size_t ws_bytes(uint32_t n) {
-    const uint64_t nb = (n + kBlock - 1ull) / kBlock;
-    return nb * kWavesPerBlock * sizeof(uint64_t) + 2 * nb * sizeof(uint32_t) + 256;
-}
+// compaction workspace of stream s for n packets: one ballot mask per wave of the decode grid
+// (grid_for(n) blocks of 4 waves), then one look-back word per k_compact tile of 64 masks
+struct Compact {
+    uint64_t *masks = nullptr;
+    unsigned long long *st = nullptr;
+    uint32_t nw = 0, ntiles = 0, epoch = 0;
+};
 
-// compaction scratch of stream s for n packets: masks | counts | offsets
-int ensure_ws(rsk_ctx *c, uint32_t n, hipStream_t s, uint64_t *&masks, uint32_t *&counts, uint32_t *&offsets) {
-    void *p = nullptr;
-    int r = rsk::stream_ws(c, s, rsk::WS_COMPACT, ws_bytes(n), &p);
+int ensure_compact(rsk_ctx *c, uint32_t n, hipStream_t s, Compact &k) {
+    k.nw = (uint32_t)(((n + kBlock - 1ull) / kBlock) * kWavesPerBlock);
+    k.ntiles = (k.nw + 63u) / 64u;
+    unsigned long long *p = nullptr;
+    int r = rsk::stream_compact(c, s, (size_t)k.nw + k.ntiles, &p, &k.epoch);
     if (r) return r;
-    const uint64_t nb = (n + kBlock - 1ull) / kBlock;
-    masks = reinterpret_cast<uint64_t *>(p);
-    counts = reinterpret_cast<uint32_t *>(masks + nb * kWavesPerBlock);
-    offsets = counts + nb;
+    k.masks = reinterpret_cast<uint64_t *>(p);
+    k.st = p + k.nw;
     return RSK_OK;
 }
 
-int run_compaction(rsk_ctx *c, uint32_t n, uint64_t *masks, uint32_t *counts, uint32_t *offsets,
-                   const rsk_decode_out *out, hipStream_t s) {
-    const uint32_t nb = (uint32_t)((n + kBlock - 1ull) / kBlock);
-    (void)c;
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, counts, offsets, nb, out->n_valid);
-    int r = launch_check("k_scan");
-    if (r) return r;
-    if (out->valid_idx) {
-        hipLaunchKernelGGL(k_scatter, dim3(nb), dim3(kBlock), 0, s, masks, offsets, out->valid_idx);
-        r = launch_check("k_scatter");
-    }
-    return r;
+int run_compaction(const Compact &k, uint32_t *valid_idx, uint32_t *n_valid, hipStream_t s) {
+    hipLaunchKernelGGL(k_compact, dim3(k.ntiles), dim3(kBlock), 0, s, k.masks, k.nw, k.st, k.epoch, valid_idx,
+                       n_valid);
+    return launch_check("k_compact");
 }
 
 bool filter_ports_bad(const rsk_capture_filter *f) {
@@ -2182,11 +2197,11 @@ bool dec_out_ok(const rsk_decode_out *o) {
            o->status && ((reinterpret_cast<uintptr_t>(o->id) & 7u) == 0);
 }
 
-DecOut make_dec_out(const rsk_decode_out *o, uint64_t *masks, uint32_t *counts) {
+DecOut make_dec_out(const rsk_decode_out *o, uint64_t *masks) {
     DecOut d;
     d.hlen = o->hlen; d.cmd = o->cmd; d.id = o->id; d.conv = o->conv; d.key = o->conn_key;
     d.pay_off = o->pay_off; d.pay_len = o->pay_len; d.status = o->status;
-    d.masks = masks; d.counts = counts;
+    d.masks = masks;
     return d;
 }
 
@@ -2283,9 +2298,8 @@ int rsk_reserve_stream(rsk_ctx *c, uint32_t n_max, void *stream) {
     if (!c) return RSK_EINVAL;
     DeviceGuard g(c->device);
     if (!g.ok) return RSK_EDEVICE;
-    uint64_t *m;
-    uint32_t *cn, *o;
-    return ensure_ws(c, n_max, (hipStream_t)stream, m, cn, o);
+    Compact ck;
+    return ensure_compact(c, n_max, (hipStream_t)stream, ck);
 }
 
 int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_encode_out *out,
@@ -2420,18 +2434,17 @@ int rsk_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *frame_arena, const u
     DeviceGuard g(c->device);
     if (!g.ok) return RSK_EDEVICE;
     const bool compact = out->valid_idx || out->n_valid;
-    uint64_t *masks = nullptr;
-    uint32_t *counts = nullptr, *offsets = nullptr;
+    Compact ck;
     if (compact) {
-        int r = ensure_ws(c, n, (hipStream_t)stream, masks, counts, offsets);
+        int r = ensure_compact(c, n, (hipStream_t)stream, ck);
         if (r) return r;
     }
     DecArgs a{frame_arena, frame_off, frame_len, is_tcp_close, n};
-    DecOut d = make_dec_out(out, masks, counts);
+    DecOut d = make_dec_out(out, ck.masks);
     hipLaunchKernelGGL(k_decode, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, a, d, c->ks);
     int r = launch_check("k_decode");
     if (r || !compact) return r;
-    return run_compaction(c, n, masks, counts, offsets, out, (hipStream_t)stream);
+    return run_compaction(ck, out->valid_idx, out->n_valid, (hipStream_t)stream);
 }
 
 int rsk_encode_headers_batch(rsk_ctx *c, uint32_t n, const rsk_encode_hdr_in *in, uint8_t *hdr, int32_t *status,
@@ -2462,18 +2475,17 @@ int rsk_decode_headers_batch(rsk_ctx *c, uint32_t n, const uint8_t *hdr, const u
     DeviceGuard g(c->device);
     if (!g.ok) return RSK_EDEVICE;
     const bool compact = out->valid_idx || out->n_valid;
-    uint64_t *masks = nullptr;
-    uint32_t *counts = nullptr, *offsets = nullptr;
+    Compact ck;
     if (compact) {
-        int r = ensure_ws(c, n, (hipStream_t)stream, masks, counts, offsets);
+        int r = ensure_compact(c, n, (hipStream_t)stream, ck);
         if (r) return r;
     }
     DecArgs a{hdr, nullptr, frame_len, is_tcp_close, n};
-    DecOut d = make_dec_out(out, masks, counts);
+    DecOut d = make_dec_out(out, ck.masks);
     hipLaunchKernelGGL(k_decode_hdr, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, a, d, c->ks);
     int r = launch_check("k_decode_hdr");
     if (r || !compact) return r;
-    return run_compaction(c, n, masks, counts, offsets, out, (hipStream_t)stream);
+    return run_compaction(ck, out->valid_idx, out->n_valid, (hipStream_t)stream);
 }
 
 // Host: the 32-B decode slot of one received frame (EncHead::DecodeBuf reads frame[8] = len; the
@@ -2502,10 +2514,9 @@ int parse_decode(rsk_ctx *c, uint32_t n, const uint8_t *cap_arena, const uint64_
     DeviceGuard g(c->device);
     if (!g.ok) return RSK_EDEVICE;
     const bool compact = dec->valid_idx || dec->n_valid;
-    uint64_t *masks = nullptr;
-    uint32_t *counts = nullptr, *offsets = nullptr;
+    Compact ck;
     if (compact) {
-        int r = ensure_ws(c, n, (hipStream_t)stream, masks, counts, offsets);
+        int r = ensure_compact(c, n, (hipStream_t)stream, ck);
         if (r) return r;
     }
     ParseArgs a;
@@ -2513,7 +2524,7 @@ int parse_decode(rsk_ctx *c, uint32_t n, const uint8_t *cap_arena, const uint64_
     a.src = tcp->src; a.dst = tcp->dst; a.sp = tcp->sp; a.dp = tcp->dp; a.seq = tcp->seq; a.ack = tcp->ack;
     a.flag = tcp->flag; a.pst = tcp->parse_status; a.cpo = tcp->cap_pay_off; a.cpl = tcp->cap_pay_len;
     a.datalink = datalink; a.flags = flags; a.n = n;
-    DecOut d = make_dec_out(dec, masks, counts);
+    DecOut d = make_dec_out(dec, ck.masks);
     a.slot = slot;
     const bool sl = slot != 0;
     const hipStream_t st = (hipStream_t)stream;
@@ -2527,7 +2538,7 @@ int parse_decode(rsk_ctx *c, uint32_t n, const uint8_t *cap_arena, const uint64_
     }
     int r = launch_check("k_parse_decode");
     if (r || !compact) return r;
-    return run_compaction(c, n, masks, counts, offsets, dec, (hipStream_t)stream);
+    return run_compaction(ck, dec->valid_idx, dec->n_valid, (hipStream_t)stream);
 }
 }  // namespace
 
@@ -2556,10 +2567,9 @@ int rsk_syncinput_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *rec_arena,
     DeviceGuard g(c->device);
     if (!g.ok) return RSK_EDEVICE;
     const bool compact = dec->valid_idx || dec->n_valid;
-    uint64_t *masks = nullptr;
-    uint32_t *counts = nullptr, *offsets = nullptr;
+    Compact ck;
     if (compact) {
-        int r = ensure_ws(c, n, (hipStream_t)stream, masks, counts, offsets);
+        int r = ensure_compact(c, n, (hipStream_t)stream, ck);
         if (r) return r;
     }
     SyncArgs a;
@@ -2567,11 +2577,11 @@ int rsk_syncinput_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *rec_arena,
     a.src = tcp->src; a.dst = tcp->dst; a.sp = tcp->sp; a.dp = tcp->dp; a.seq = tcp->seq; a.ack = tcp->ack;
     a.flag = tcp->flag; a.pst = tcp->parse_status; a.cpo = tcp->cap_pay_off; a.cpl = tcp->cap_pay_len;
     a.n = n;
-    const DecOut d = make_dec_out(dec, masks, counts);
+    const DecOut d = make_dec_out(dec, ck.masks);
     hipLaunchKernelGGL(k_syncinput_decode, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, a, d, c->ks);
     int r = launch_check("k_syncinput_decode");
     if (r || !compact) return r;
-    return run_compaction(c, n, masks, counts, offsets, dec, (hipStream_t)stream);
+    return run_compaction(ck, dec->valid_idx, dec->n_valid, (hipStream_t)stream);
 }
 
 int rsk_filter_parse_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *cap_arena, const uint64_t *cap_off,
@@ -2589,10 +2599,9 @@ int rsk_filter_parse_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *cap_are
     DeviceGuard g(c->device);
     if (!g.ok) return RSK_EDEVICE;
     const bool compact = dec->valid_idx || dec->n_valid;
-    uint64_t *masks = nullptr;
-    uint32_t *counts = nullptr, *offsets = nullptr;
+    Compact ck;
     if (compact) {
-        int r = ensure_ws(c, n, (hipStream_t)stream, masks, counts, offsets);
+        int r = ensure_compact(c, n, (hipStream_t)stream, ck);
         if (r) return r;
     }
     ParseArgs a;
@@ -2600,7 +2609,7 @@ int rsk_filter_parse_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *cap_are
     a.src = tcp->src; a.dst = tcp->dst; a.sp = tcp->sp; a.dp = tcp->dp; a.seq = tcp->seq; a.ack = tcp->ack;
     a.flag = tcp->flag; a.pst = tcp->parse_status; a.cpo = tcp->cap_pay_off; a.cpl = tcp->cap_pay_len;
     a.datalink = datalink; a.flags = flags; a.n = n; a.slot = 0;
-    DecOut d = make_dec_out(dec, masks, counts);
+    DecOut d = make_dec_out(dec, ck.masks);
     const hipStream_t st = (hipStream_t)stream;
     if (datalink == RSK_DLT_EN10MB)
         hipLaunchKernelGGL(k_filter_parse_decode<14>, dim3(grid_for(n)), dim3(kBlock), 0, st, a, d, c->ks, match, *f);
@@ -2608,7 +2617,7 @@ int rsk_filter_parse_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *cap_are
         hipLaunchKernelGGL(k_filter_parse_decode<4>, dim3(grid_for(n)), dim3(kBlock), 0, st, a, d, c->ks, match, *f);
     int r = launch_check("k_filter_parse_decode");
     if (r || !compact) return r;
-    return run_compaction(c, n, masks, counts, offsets, dec, st);
+    return run_compaction(ck, dec->valid_idx, dec->n_valid, (hipStream_t)stream);
 }
 
 int rsk_capture_filter_batch(rsk_ctx *c, uint32_t n, const uint8_t *cap_arena, const uint64_t *cap_off,
@@ -2621,29 +2630,23 @@ int rsk_capture_filter_batch(rsk_ctx *c, uint32_t n, const uint8_t *cap_arena, c
     DeviceGuard g(c->device);
     if (!g.ok) return RSK_EDEVICE;
     const bool compact = match_idx || n_match;
-    uint64_t *masks = nullptr;
-    uint32_t *counts = nullptr, *offsets = nullptr;
+    Compact ck;
     if (compact) {
-        int r = ensure_ws(c, n, (hipStream_t)stream, masks, counts, offsets);
+        int r = ensure_compact(c, n, (hipStream_t)stream, ck);
         if (r) return r;
     }
     FiltArgs a;
     a.cap = cap_arena; a.cap_off = cap_off; a.cap_len = cap_len; a.match = match; a.n = n;
     DecOut d;
     std::memset(&d, 0, sizeof d);
-    d.masks = masks;
-    d.counts = counts;
+    d.masks = ck.masks;
     if (datalink == RSK_DLT_EN10MB)
         hipLaunchKernelGGL(k_capture_filter<14>, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, a, d, *f);
     else
         hipLaunchKernelGGL(k_capture_filter<4>, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, a, d, *f);
     int r = launch_check("k_capture_filter");
     if (r || !compact) return r;
-    rsk_decode_out o;
-    std::memset(&o, 0, sizeof o);
-    o.valid_idx = match_idx;
-    o.n_valid = n_match;
-    return run_compaction(c, n, masks, counts, offsets, &o, (hipStream_t)stream);
+    return run_compaction(ck, match_idx, n_match, (hipStream_t)stream);
 }
 
 // BuildFilterStr (cap/cap_util.cpp:67-144) with proto "tcp" (cap/RCap.cpp:64)

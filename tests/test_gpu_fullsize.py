@@ -105,7 +105,7 @@ def _roundtrip(codec, gpu, oracle, d, pad16):
 
 
 def test_compaction_large_random(codec, gpu, oracle):
-    """n > 4096 scan blocks x 256 (multi-pass k_scan): random validity pattern, order-stable."""
+    """n > 4096 scan blocks x 256 (many k_compact tiles): random validity pattern, order-stable."""
     import torch
 
     n = 5_000_003

@@ -1,7 +1,8 @@
-"""GPU: one context driven from two streams at once.  The compaction scratch (ballot masks, block
-counts, offsets) is per stream (rsk_ctx.h stream_ws), so two compacting decodes issued back to back
-on different streams — overlapping on the device — each give their own batch's VALID list
-(include/rsk_codec.h, "Streams")."""
+"""GPU: one context driven from two streams at once.  The compaction's look-back state is per
+stream (rsk_ctx.h stream_compact), so two compacting decodes issued back to back on different
+streams — overlapping on the device — each give their own batch's VALID list (include/rsk_codec.h,
+"Streams").  The state words carry a per-call epoch instead of being reset per call; the epoch
+wraps after 65535 calls (the state is zeroed then)."""
 from __future__ import annotations
 
 import numpy as np
@@ -61,3 +62,40 @@ def test_reserve_stream(codec, gpu):
     s = torch.cuda.Stream(gpu)
     codec.reserve(1 << 16, stream=s)
     codec.reserve(1 << 10)
+
+
+def test_compaction_epochs_wrap(codec, gpu):
+    """65 540 compacting decodes on one stream: two batches alternate (different VALID lists and
+    block counts), so a state word left by the previous call that were taken as this call's would
+    show up as a wrong prefix; checked around the epoch wrap (call 65 535 -> zeroed state)."""
+    import torch
+
+    from rsock_amd.codec import DecodeBuffers
+
+    n = 5000  # 20 blocks, the last one partial
+    d = workload.describe("c2", 0, n, n=n)
+    w = workload.DeviceWorkload(d, gpu)
+    codec.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
+                       w.status, id_uniform=workload.ID_UNIFORM)
+    torch.cuda.synchronize()
+    good = w.frame.clone()
+    bad_rows = np.nonzero(np.arange(n) % 3 == 1)[0]
+    w.frame[w.frame_off[torch.from_numpy(bad_rows).to(gpu)]] ^= 1
+    bad = w.frame.clone()
+    keep = [np.ones(n, bool), np.arange(n) % 3 != 1]
+    exp = [np.nonzero(k)[0].astype(np.int32) for k in keep]
+    s = torch.cuda.Stream(gpu)
+    outs = [DecodeBuffers.alloc(n, gpu) for _ in range(2)]
+    frames = [good, bad]
+    checked = 0
+    with torch.cuda.stream(s):
+        for call in range(65540):
+            k = call & 1
+            codec.onrecv_batch(frames[k], w.frame_off, w.frame_len, outs[k], stream=s)
+            if call in (0, 1, 9, 65533, 65534, 65535, 65536, 65537, 65539):
+                s.synchronize()
+                nv = int(outs[k].n_valid.item())
+                assert nv == exp[k].size, call
+                assert np.array_equal(outs[k].valid_idx[:nv].cpu().numpy(), exp[k]), call
+                checked += 1
+    assert checked == 9
