@@ -1,10 +1,13 @@
 #!/usr/bin/env python3
 """Benchmark: device-resident EncHead+MD5 encode then decode+verify+compact (BASELINE.json metric).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4|c5] [--no-cpu-baseline]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4|c5] [--no-cpu-baseline] [--eager]
 
 One step = one pass of the hot path over one batch: k_encode (RConn::Output framing of every
-packet) followed by k_decode + compaction (RConn::OnRecv of every frame), inputs resident in HBM.
+packet) followed by k_decode + k_compact (RConn::OnRecv of every frame), inputs resident in HBM.
+The timed region replays a HIP graph of the step (one host launch per step; --eager: the three
+library calls per step instead); the per-kernel times behind `roofline` come from HIP events on
+the step's stream around the same launches issued one by one right after the timed region.
 
 Workload: N = 1 defaults to C3 (4M x 1400-B packets, the metric's target config); N > 1 defaults
 to C5 (BASELINE configs[4]: 64M x 1400-B packets in total, contiguous shards, strong scaling), so
@@ -213,6 +216,9 @@ def main() -> None:
     ap.add_argument("--cpu-sample", type=int, default=1 << 20)
     ap.add_argument("--cpu-seconds", type=float, default=6.0)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal)")
+    ap.add_argument("--eager", action="store_true",
+                    help="launch the step's kernels one by one in the timed region instead of replaying a "
+                         "captured HIP graph of the step")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal only: every rank uses GPU 0 (N ranks on a 1-GPU box)")
     args = ap.parse_args()
@@ -253,8 +259,11 @@ def main() -> None:
         d = workload.describe(cfg, rank * n, (rank + 1) * n, n=world * n)
     w = workload.DeviceWorkload(d, dev)
     cx = rc.Codec(b"hello135", gpu)
-    cx.reserve(d.n)
-    stream = torch.cuda.current_stream()
+    graph_mode = not args.eager
+    # graph capture needs a stream other than the null stream; the codec's per-stream workspaces are
+    # sized on it by the warmup, before the capture
+    stream = torch.cuda.Stream(dev) if graph_mode else torch.cuda.current_stream()
+    cx.reserve(d.n, stream=stream)
 
     def step(ev=None):
         if ev is not None:
@@ -268,14 +277,30 @@ def main() -> None:
         if ev is not None:
             ev[2].record(stream)
 
-    for _ in range(args.warmup):
-        step()
+    with torch.cuda.stream(stream):
+        for _ in range(args.warmup):
+            step()
     torch.cuda.synchronize()
     # correctness gate on the measured data: every packet must verify
-    nv = int(w.dec.n_valid.item())
     expect_valid = int(((d.pay_len >= 1) & (d.pay_len <= 1469)).sum())
-    if nv != expect_valid:
-        raise SystemExit(f"bench: decode verified {nv} of {expect_valid} packets")
+
+    def gate(when):
+        nv = int(w.dec.n_valid.item())
+        if nv != expect_valid:
+            raise SystemExit(f"bench: decode verified {nv} of {expect_valid} packets ({when})")
+
+    gate("warmup")
+    graph = None
+    if graph_mode:
+        # the whole step (k_encode, k_decode, k_compact) as one HIP graph: one launch per step from
+        # the host instead of three library calls, so the timed region measures the GPU, not Python
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=stream):
+            step()
+        w.dec.n_valid.zero_()
+        graph.replay()
+        torch.cuda.synchronize()
+        gate("graph replay")
 
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
     if world > 1:
@@ -283,11 +308,22 @@ def main() -> None:
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(evs[k])
+        if graph is not None:
+            graph.replay()
+        else:
+            step(evs[k])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    gate("timed region")
+    if graph is not None:
+        # per-kernel durations for the roofline: HIP events on the step's stream around the same
+        # launches, issued one by one (the graph replays the identical kernels and arguments)
+        with torch.cuda.stream(stream):
+            for k in range(args.steps):
+                step(evs[k])
+        torch.cuda.synchronize()
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -331,6 +367,9 @@ def main() -> None:
             },
             "gib_per_s": round(world * bytes_step * args.steps / elapsed_max / 2**30, 2),
             "kernels_ms": {"k_encode": round(enc_ms, 4), "decode+compact": round(dec_ms, 4)},
+            "launch": ("hipGraph replay of the step (k_encode, k_decode, k_compact); kernel times: HIP events "
+                       "around the same launches issued one by one after the timed region") if graph_mode else
+                      "eager launches; kernel times: HIP events in the timed region",
             "roofline": {
                 "kernel": "k_encode",
                 "bound": "hbm",

@@ -22,7 +22,7 @@ enum WsKind { WS_COMPACT = 0, WS_SEQ = 1, WS_DEMUX = 2, WS_KINDS = 3 };
 struct WsBuf {
     void *p = nullptr;
     size_t bytes = 0;
-    uint32_t epoch = 0;  // WS_COMPACT: the look-back state's call epoch (see stream_compact)
+    bool zeroed = false;  // WS_COMPACT: zero-filled since (re)allocation (see stream_compact)
 };
 }  // namespace rsk
 
@@ -98,29 +98,28 @@ inline int stream_ws(rsk_ctx *c, hipStream_t s, int kind, size_t need, void **ou
         hipError_t e = hipMalloc(&b.p, need);
         if (e != hipSuccess) { set_error("hipMalloc(workspace)", e); b.p = nullptr; return RSK_ENOMEM; }
         b.bytes = need;
-        b.epoch = 0;  // fresh memory: stream_compact zeroes it before the first epoch
+        b.zeroed = false;  // fresh memory: stream_compact zeroes it before first use
     }
     *out = b.p;
     return RSK_OK;
 }
 
-// Look-back state of the single-pass compaction for stream s: `words` 64-bit words and this
-// call's epoch (1..0xFFFF).  A state word is ready for a call only when its top 16 bits hold the
-// call's epoch, so no per-call reset is needed; a fresh buffer, and every 65535th call, zeroes the
-// words first (epoch 0 is never handed out).
-inline int stream_compact(rsk_ctx *c, hipStream_t s, size_t words, unsigned long long **out, uint32_t *epoch) {
+// Workspace of the compaction for stream s: `words` 64-bit words, zeroed when (re)allocated.  Its
+// first word is the device-side call counter k_compact keeps (see rsk_kernels.hip), so the state
+// needs no host-side reset per call and a captured graph replays correctly.
+inline int stream_compact(rsk_ctx *c, hipStream_t s, size_t words, unsigned long long **out, size_t *cap) {
     void *p = nullptr;
     int r = stream_ws(c, s, WS_COMPACT, words * sizeof(unsigned long long), &p);
     if (r) return r;
     std::lock_guard<std::mutex> lk(c->ws_mu);
     WsBuf &b = c->ws[s][WS_COMPACT];
-    if (b.epoch == 0 || b.epoch >= 0xFFFFu) {
+    if (!b.zeroed) {
         hipError_t e = hipMemsetAsync(b.p, 0, b.bytes, s);
         if (e != hipSuccess) { set_error("hipMemsetAsync(compaction state)", e); return RSK_EDEVICE; }
-        b.epoch = 0;
+        b.zeroed = true;
     }
-    *epoch = ++b.epoch;
     *out = reinterpret_cast<unsigned long long *>(p);
+    *cap = b.bytes / sizeof(unsigned long long);
     return RSK_OK;
 }
 

@@ -1448,13 +1448,17 @@ __device__ __forceinline__ void store_dec(const DecOut &d, uint64_t i, const Dec
 // it counts them, scans them in one wave, finds the tile's prefix by decoupled look-back over the
 // tiles before it, and its lanes write their indices at prefix + rank (valid_idx in index order).
 // Tiles are dispatched in index order, so a tile only waits for tiles that are resident or done.
-// State word per tile: bits 63..48 the call's epoch, bit 47 inclusive, bits 31..0 the count; a
-// word from another call is not ready, so the state needs no per-call reset.  Device-scope relaxed
+// State word per tile: bits 63..33 the call's epoch, bit 32 inclusive, bits 31..0 the count; a
+// word from another call is not ready, so the state needs no per-call reset.  The epoch is a
+// device-side counter (workspace word 0) that every tile reads first and the last tile advances
+// when it is done — by then every tile has published (the inclusive chain reaches tile 0), so all
+// read the same value; the next call on the stream, or the next replay of a captured graph, sees
+// the next epoch.  Epochs run 1 .. 2^31 - 1 (0 is the zeroed state).  Device-scope relaxed
 // atomics (acquire / release would add an L2 write-back / invalidate per access, rsk_demux.hip);
 // a spin that outlives kCmpSpinMax reads gives up (wrong list, no hang).  Round 1 used k_scan (one
 // workgroup) + k_scatter; a look-back inside the decode launch itself (one word per 256-packet
 // block) was measured slower than both (C2: 40 us vs 31): the block-granular chain is the cost.
-constexpr unsigned long long kCmpIncl = 1ull << 47;
+constexpr unsigned long long kCmpIncl = 1ull << 32;
 constexpr uint32_t kCmpSpinMax = 1u << 22;
 
 __device__ __forceinline__ unsigned long long cmp_wait(unsigned long long *s, uint32_t epoch) {
@@ -1462,13 +1466,13 @@ __device__ __forceinline__ unsigned long long cmp_wait(unsigned long long *s, ui
     uint32_t spins = 0;
     do {
         v = __hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } while ((uint32_t)(v >> 48) != epoch && ++spins < kCmpSpinMax);
-    return (uint32_t)(v >> 48) == epoch ? v : kCmpIncl;
+    } while ((uint32_t)(v >> 33) != epoch && ++spins < kCmpSpinMax);
+    return (uint32_t)(v >> 33) == epoch ? v : kCmpIncl;
 }
 
 // all 64 lanes of one wave of tile b; agg uniform; returns b's exclusive prefix (uniform)
 __device__ uint32_t cmp_lookback(unsigned long long *st, uint32_t b, uint32_t agg, uint32_t lane, uint32_t epoch) {
-    const unsigned long long tag = (unsigned long long)epoch << 48;
+    const unsigned long long tag = (unsigned long long)epoch << 33;
     if (b == 0u) {
         if (lane == 0u) __hip_atomic_store(st, tag | kCmpIncl | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return 0u;
@@ -1928,14 +1932,17 @@ __global__ __launch_bounds__(kBlock) void k_filter_parse_decode(ParseArgs a, Dec
     if (d.masks) compact_epilogue(d, valid, i);
 }
 
+// st[0]: the epoch counter; st[1 + t]: tile t's look-back word
 __global__ __launch_bounds__(kBlock) void k_compact(const uint64_t *masks, uint32_t nw, unsigned long long *st,
-                                                    uint32_t epoch, uint32_t *valid_idx, uint32_t *n_valid) {
+                                                    uint32_t *valid_idx, uint32_t *n_valid) {
     __shared__ uint64_t ms[64];
     __shared__ uint32_t mex[64];
     __shared__ uint32_t pre;
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     const uint64_t mb = (uint64_t)blockIdx.x * 64u;
     if (w == 0u) {
+        const uint32_t e0 = (uint32_t)__hip_atomic_load(st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t epoch = e0 % 0x7fffffffu + 1u;
         const uint64_t m = mb + lane < nw ? masks[mb + lane] : 0ull;
         const uint32_t c = (uint32_t)__popcll(m);
         uint32_t inc = c;
@@ -1947,10 +1954,13 @@ __global__ __launch_bounds__(kBlock) void k_compact(const uint64_t *masks, uint3
         ms[lane] = m;
         mex[lane] = inc - c;
         const uint32_t agg = (uint32_t)__shfl((int)inc, 63);
-        const uint32_t p = cmp_lookback(st, blockIdx.x, agg, lane, epoch);
+        const uint32_t p = cmp_lookback(st + 1, blockIdx.x, agg, lane, epoch);
         if (lane == 0u) {
             pre = p;
-            if (n_valid && blockIdx.x == gridDim.x - 1u) *n_valid = p + agg;
+            if (blockIdx.x == gridDim.x - 1u) {  // every tile has read the epoch (see above)
+                if (n_valid) *n_valid = p + agg;
+                __hip_atomic_store(st, (unsigned long long)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
     }
     __syncthreads();
@@ -2148,28 +2158,31 @@ thread_local char rsk::g_last_error[256] = "";
 
 namespace {
 
-// compaction workspace of stream s for n packets: one ballot mask per wave of the decode grid
-// (grid_for(n) blocks of 4 waves), then one look-back word per k_compact tile of 64 masks
+// Compaction workspace of stream s for n packets.  Layout, fixed by the buffer's capacity (not by
+// n, so a call never reads another call's masks as look-back words): word 0 the epoch counter,
+// words 1 .. T the look-back words of up to T tiles, then the per-wave ballot masks (T = (cap - 1)
+// / 65: room for 64 T masks).  The decode grid has grid_for(n) blocks of 4 waves, one mask each.
 struct Compact {
     uint64_t *masks = nullptr;
     unsigned long long *st = nullptr;
-    uint32_t nw = 0, ntiles = 0, epoch = 0;
+    uint32_t nw = 0, ntiles = 0;
 };
 
 int ensure_compact(rsk_ctx *c, uint32_t n, hipStream_t s, Compact &k) {
     k.nw = (uint32_t)(((n + kBlock - 1ull) / kBlock) * kWavesPerBlock);
     k.ntiles = (k.nw + 63u) / 64u;
     unsigned long long *p = nullptr;
-    int r = rsk::stream_compact(c, s, (size_t)k.nw + k.ntiles, &p, &k.epoch);
+    size_t cap = 0;
+    int r = rsk::stream_compact(c, s, 1u + 65ull * k.ntiles, &p, &cap);
     if (r) return r;
-    k.masks = reinterpret_cast<uint64_t *>(p);
-    k.st = p + k.nw;
+    const size_t T = (cap - 1u) / 65u;
+    k.st = p;
+    k.masks = reinterpret_cast<uint64_t *>(p + 1u + T);
     return RSK_OK;
 }
 
 int run_compaction(const Compact &k, uint32_t *valid_idx, uint32_t *n_valid, hipStream_t s) {
-    hipLaunchKernelGGL(k_compact, dim3(k.ntiles), dim3(kBlock), 0, s, k.masks, k.nw, k.st, k.epoch, valid_idx,
-                       n_valid);
+    hipLaunchKernelGGL(k_compact, dim3(k.ntiles), dim3(kBlock), 0, s, k.masks, k.nw, k.st, valid_idx, n_valid);
     return launch_check("k_compact");
 }
 

@@ -1,8 +1,8 @@
 """GPU: one context driven from two streams at once.  The compaction's look-back state is per
 stream (rsk_ctx.h stream_compact), so two compacting decodes issued back to back on different
 streams — overlapping on the device — each give their own batch's VALID list (include/rsk_codec.h,
-"Streams").  The state words carry a per-call epoch instead of being reset per call; the epoch
-wraps after 65535 calls (the state is zeroed then)."""
+"Streams").  The look-back words carry a per-call epoch kept on the device instead of being reset
+per call, which also makes a captured graph replay correctly."""
 from __future__ import annotations
 
 import numpy as np
@@ -64,15 +64,9 @@ def test_reserve_stream(codec, gpu):
     codec.reserve(1 << 10)
 
 
-def test_compaction_epochs_wrap(codec, gpu):
-    """65 540 compacting decodes on one stream: two batches alternate (different VALID lists and
-    block counts), so a state word left by the previous call that were taken as this call's would
-    show up as a wrong prefix; checked around the epoch wrap (call 65 535 -> zeroed state)."""
+def _alt_batches(codec, gpu, n):
     import torch
 
-    from rsock_amd.codec import DecodeBuffers
-
-    n = 5000  # 20 blocks, the last one partial
     d = workload.describe("c2", 0, n, n=n)
     w = workload.DeviceWorkload(d, gpu)
     codec.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
@@ -82,20 +76,61 @@ def test_compaction_epochs_wrap(codec, gpu):
     bad_rows = np.nonzero(np.arange(n) % 3 == 1)[0]
     w.frame[w.frame_off[torch.from_numpy(bad_rows).to(gpu)]] ^= 1
     bad = w.frame.clone()
-    keep = [np.ones(n, bool), np.arange(n) % 3 != 1]
-    exp = [np.nonzero(k)[0].astype(np.int32) for k in keep]
+    exp = [np.arange(n, dtype=np.int32), np.nonzero(np.arange(n) % 3 != 1)[0].astype(np.int32)]
+    return w, [good, bad], exp
+
+
+def _check(out, exp, what):
+    nv = int(out.n_valid.item())
+    assert nv == exp.size, what
+    assert np.array_equal(out.valid_idx[:nv].cpu().numpy(), exp), what
+
+
+def test_compaction_state_across_calls(codec, gpu):
+    """Compaction look-back words are tagged with a device-side call epoch, never reset per call:
+    batches of two sizes (different tile counts) and two VALID patterns alternate on one stream, so
+    a word left by an earlier call taken as this call's would show up as a wrong prefix."""
+    import torch
+
+    from rsock_amd.codec import DecodeBuffers
+
+    wa, fa, ea = _alt_batches(codec, gpu, 300_000)  # 74 tiles
+    wb, fb, eb = _alt_batches(codec, gpu, 5000)     # 2 tiles, the last partial
     s = torch.cuda.Stream(gpu)
-    outs = [DecodeBuffers.alloc(n, gpu) for _ in range(2)]
-    frames = [good, bad]
-    checked = 0
+    oa, ob = DecodeBuffers.alloc(300_000, gpu), DecodeBuffers.alloc(5000, gpu)
     with torch.cuda.stream(s):
-        for call in range(65540):
-            k = call & 1
-            codec.onrecv_batch(frames[k], w.frame_off, w.frame_len, outs[k], stream=s)
-            if call in (0, 1, 9, 65533, 65534, 65535, 65536, 65537, 65539):
+        for call in range(400):
+            k = (call >> 1) & 1
+            if call & 1:
+                codec.onrecv_batch(fb[k], wb.frame_off, wb.frame_len, ob, stream=s)
+            else:
+                codec.onrecv_batch(fa[k], wa.frame_off, wa.frame_len, oa, stream=s)
+            if call % 37 in (0, 1):
                 s.synchronize()
-                nv = int(outs[k].n_valid.item())
-                assert nv == exp[k].size, call
-                assert np.array_equal(outs[k].valid_idx[:nv].cpu().numpy(), exp[k]), call
-                checked += 1
-    assert checked == 9
+                _check(ob if call & 1 else oa, (eb if call & 1 else ea)[k], call)
+
+
+def test_compaction_in_captured_graph(codec, gpu):
+    """A compacting decode captured in a HIP graph and replayed: the epoch advances on the device, so
+    every replay's VALID list is right while the frames alternate between two patterns."""
+    import torch
+
+    from rsock_amd.codec import DecodeBuffers
+
+    n = 100_000
+    w, frames, exp = _alt_batches(codec, gpu, n)
+    out = DecodeBuffers.alloc(n, gpu)
+    s = torch.cuda.Stream(gpu)
+    with torch.cuda.stream(s):
+        codec.onrecv_batch(w.frame, w.frame_off, w.frame_len, out, stream=s)  # workspace sized before capture
+    s.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        codec.onrecv_batch(w.frame, w.frame_off, w.frame_len, out, stream=torch.cuda.current_stream())
+    for r in range(12):
+        k = r % 2 if r < 8 else 1
+        w.frame.copy_(frames[k])
+        out.n_valid.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        _check(out, exp[k], r)
