@@ -578,9 +578,27 @@ __device__ __forceinline__ void copy_pkt_pipe(const EncArgs &a, const KeySched &
 // lane l of iteration t takes chunk g = 64(U t + u) + l and finds its packet by a 6-step binary
 // search over the set's prefix sums in this wave's LDS slice.  Wave-local: no block barrier, so
 // waves of one block may take different copy paths.
-template <int U>
-__device__ __forceinline__ void copy_flat(const EncArgs &a, const Lane1 &L, uint32_t lane, bool mine,
-                                          CopyRec *recs, uint32_t *cend) {
+// TAGQ: phase 1 left the tag; `payload[0]` is loaded right after the first iteration's chunk loads
+// (both depend only on the descriptors) and the packet's lane then stores its header chunks, so
+// the set pays one dependent global round trip less than with the tag before the copy.
+template <int U, bool TAGQ = false>
+__device__ __forceinline__ void flat_head(const EncArgs &a, const KeySched &ks, const Lane1 &L, bool mine) {
+    if constexpr (TAGQ) {
+        if (mine) {
+            const uint32_t b0 = rsk::gptr(a.payload)[L.po];
+            uint32_t H[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) H[q] = L.H[q];
+            tag_of(ks, b0, H[0], H[1]);
+            H[7] |= b0 << 24;
+            store_head(H, a.frame + L.fo);
+        }
+    }
+}
+
+template <int U, bool TAGQ = false>
+__device__ __forceinline__ void copy_flat(const EncArgs &a, const KeySched &ks, const Lane1 &L, uint32_t lane,
+                                          bool mine, CopyRec *recs, uint32_t *cend) {
     uint32_t cc = 0;
     CopyRec r;
     r.src_al = nullptr; r.dst = nullptr; r.cstart = 0; r.sh = 0; r.last_rel = 0; r.flen = 0;
@@ -638,10 +656,12 @@ __device__ __forceinline__ void copy_flat(const EncArgs &a, const Lane1 &L, uint
                 lims[u] = (int32_t)rr.flen - 32 - 16 * m;
             }
         }
+        if (TAGQ && g0 == 0u) flat_head<U, TAGQ>(a, ks, L, mine);
 #pragma unroll
         for (int u = 0; u < U; ++u)
             if (act[u]) store_piece<0>(dsts[u], funnel16_lane(A[u], B[u], shs[u]), los[u], lims[u], a.pad != 0u);
     }
+    if (TAGQ && C == 0u) flat_head<U, TAGQ>(a, ks, L, mine);
     wave_lds_sync();  // LDS slice reusable by the caller afterwards
 }
 
@@ -653,9 +673,12 @@ constexpr uint32_t kFlatBelowMeanBytes = 256;
 // carries fewer bytes per MD5 (C4: +10 % with the tag deferred).
 constexpr uint32_t kDeferTagMeanBytes = 1024;
 
-// One 64-packet set per wave: phase 1, then the chosen copy path.  MODE 6 (shipped): per-wave
-// choice of path, tag deferred into the copy loop for sets of long frames; A/B build only: 3 = tag
-// always in phase 1, 7 = flat path only, 8 = per-packet path only.  NT < 0: store policy per set.
+// One 64-packet set per wave: phase 1, then the chosen copy path.  MODE 11 (shipped): per-wave
+// choice of path, tag deferred into the copy loop for sets of long frames and behind the first
+// chunk loads for flat sets, pipelined per-packet copy; A/B build only: 6 = unpipelined, 9 = 11
+// with the flat sets' tag in phase 1, 10 = 9 with the tag in the copy loop for every per-packet
+// set, 3 = tag always in phase 1, 7 = flat path only, 8 = per-packet path only.  NT < 0: store
+// policy per set.
 template <int MODE, int PU, int U, int NT>
 __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks, uint64_t i, uint32_t lane,
                                            CopyRec *recs, uint32_t *cend) {
@@ -670,12 +693,14 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
     const bool flat = MODE == 7 ? true : MODE == 8 ? false : fl < kFlatBelowMeanBytes * cnt;
     // MODE 10 (A/B): as 9 with the tag in the copy loop for every per-packet set
     const bool defer = MODE != 3 && MODE != 7 && !flat && (MODE == 10 || fl >= kDeferTagMeanBytes * cnt);
+    // MODE 11 (A/B): as 9 with the flat sets' tag and header stores behind the first chunk loads
+    constexpr bool kFlatTagQ = MODE == 11;
     if constexpr (MODE != 3 && MODE != 7) {  // the tag now, except for the sets whose copy loop takes it
-        if (!defer) encode_tag(a, ks, L);
+        if (!defer && !(kFlatTagQ && flat)) encode_tag(a, ks, L);
     }
     if (flat) {
-        if (vec) store_head(L.H, a.frame + L.fo);
-        copy_flat<U>(a, L, lane, vec, recs, cend);
+        if (!kFlatTagQ && vec) store_head(L.H, a.frame + L.fo);
+        copy_flat<U, kFlatTagQ>(a, ks, L, lane, vec, recs, cend);
         return;
     }
     bool nt = NT == 2;
@@ -695,7 +720,7 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
     // first slot store (lanes 0..2, words by readlane); the others by the slot lane (store_head).
     // Measured (A/B, profiles/r02_ab_head.json): C3 2.34 vs 2.55 ms with the first; C4 0.389 vs
     // 0.420 ms with the second.
-    if constexpr (MODE == 9 || MODE == 10) {  // software-pipelined per-packet copy (shipped: 9)
+    if constexpr (MODE == 9 || MODE == 10 || MODE == 11) {  // software-pipelined per-packet copy (shipped: 9)
         if (defer) {
             if (nt) copy_pkt_pipe<PU, 2, true>(a, ks, L, lane, vm);
             else copy_pkt_pipe<PU, 0, true>(a, ks, L, lane, vm);
@@ -2231,17 +2256,19 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 
 #ifdef RSK_AB
 // A/B build only: selects the encode kernel variant for in-process A/B runs (tools/ab_encode.py).
-// k_encode<MODE, PU, U, NT> (see encode_set): 0 = the shipped <9, 4, 4, -1> (software-pipelined
-// per-packet copy, 4 packets per batch); 17 = round 2's first form <6, 12, 4, -1> (12 packets per
+// k_encode<MODE, PU, U, NT> (see encode_set): 0 = the shipped <11, 4, 4, -1> (software-pipelined
+// per-packet copy, 4 packets per batch; flat sets' tag behind the first chunk loads); 22 = the same
+// with the flat sets' tag in phase 1 (<9, 4, 4, -1>); 17 = round 2's first form <6, 12, 4, -1> (12 packets per
 // iteration, no pipelining); 1 = as 17 with the tag always in phase 1; 2 / 3 = 17 with 8 / 16
 // packets per iteration; 4 = 2 chunks per lane per flat iteration; 5 / 6 = normal / nontemporal
 // stores on every per-packet set; 7 = flat path only; 8 = per-packet path only (unpipelined);
-// 9 / 10 / 14 / 15 / 16 = pipelined with 6 / 8 / 3 / 5 / 2 packets per batch (11 = 4, shipped);
+// 9 / 10 / 14 / 15 / 16 = pipelined with 6 / 8 / 3 / 5 / 2 packets per batch (11 = 4);
 // 12 / 13 = k_copy_probe (memory-side ceiling probe, wrong bytes) with 12 / 4 packets per batch;
-// 18 = shipped with the tag in the copy loop for every per-packet set.
+// 18 = shipped with the tag in the copy loop for every per-packet set; 19 / 20 / 21 = shipped with
+// the flat sets' tag behind the first chunk loads, 4 / 2 / 8 chunk rows per flat iteration.
 // v + 100 * cap (cap 1..4): the same kernel held to `cap` blocks per CU by unused LDS.
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
-    if (!c || v < 0 || v % 100 > 18 || v / 100 > 4) return RSK_EINVAL;
+    if (!c || v < 0 || v % 100 > 22 || v / 100 > 4) return RSK_EINVAL;
     c->enc_variant = v;
     return RSK_OK;
 }
@@ -2361,13 +2388,17 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         case 16: hipLaunchKernelGGL((k_encode<9, 2, 4, -1>), gd, bd, lds, st, a, c->ks); break;
         case 17: hipLaunchKernelGGL((k_encode<6, 12, 4, -1>), gd, bd, lds, st, a, c->ks); break;
         case 18: hipLaunchKernelGGL((k_encode<10, 4, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        default: hipLaunchKernelGGL((k_encode<9, 4, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 19: hipLaunchKernelGGL((k_encode<11, 4, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 20: hipLaunchKernelGGL((k_encode<11, 4, 2, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 21: hipLaunchKernelGGL((k_encode<11, 4, 8, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 22: hipLaunchKernelGGL((k_encode<9, 4, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        default: hipLaunchKernelGGL((k_encode<11, 4, 4, -1>), gd, bd, lds, st, a, c->ks); break;
     }
 #else
-    // the shipped kernel: per-wave hybrid (flat chunk list for short frames, software-pipelined
-    // one-load DPP per-packet copy, 4 packets per batch, for the rest), tag in the copy loop for
-    // long-frame sets, per-set store policy
-    hipLaunchKernelGGL((k_encode<9, 4, 4, -1>), gd, bd, 0, st, a, c->ks);
+    // the shipped kernel: per-wave hybrid (flat chunk list for short frames, with the tag behind the
+    // first chunk loads; software-pipelined one-load DPP per-packet copy, 4 packets per batch, for
+    // the rest), tag in the copy loop for long-frame sets, per-set store policy
+    hipLaunchKernelGGL((k_encode<11, 4, 4, -1>), gd, bd, 0, st, a, c->ks);
 #endif
     return launch_check("k_encode");
 }
