@@ -2,22 +2,24 @@
 //
 // Kernels (DESIGN.md §4 has the roofline and the algorithmic bytes of each):
 //   k_encode        RConn::Output framing (conn/RConn.cpp:87-105): per 64-packet set, one lane per
-//                   packet computes status, the MD5 tag and the 31 header bytes; then, per wave, the
-//                   per-packet path (the wave streams 16 frames at a time as 16-B chunks, one aligned
-//                   payload load per chunk, funnel partner from the next lane by DPP) or the flat
-//                   chunk list for short frames.  k_encode_blk and the two-load copy: A/B variants.
+//                   packet computes status and the 31 header bytes (the tag from the key's 256-entry
+//                   table, staged in LDS); then, per wave, the software-pipelined per-packet copy
+//                   (4-packet batches of 16-B chunks, one aligned payload load per chunk, funnel
+//                   partner from the next lane by DPP) or the flat chunk list for short frames.
+//                   The unpipelined copy and k_copy_probe: A/B build only.
 //   k_encode_wire   RConn::Output + RawTcp::SendRawTcp (conn/RawTcp.cpp:280-341): frames plus the
 //                   IPv4/TCP headers and checksums libnet writes, two-launch hybrid.
 //   k_encode_hdr /  header-only framing / verification on 32-B slots (host-resident deployments:
 //   k_decode_hdr    the payload never crosses PCIe).
 //   k_decode        RConn::OnRecv (conn/RConn.cpp:64-85): one lane per frame, 32-B header window,
-//                   MD5 verify, SoA field stores, per-wave ballot mask + per-block count.
+//                   tag verify (LDS table), SoA field stores, per-wave VALID ballot for k_compact.
 //   k_parse_decode  RawTcp::RawInput (conn/RawTcp.cpp:138-244) fused with k_decode's body.
 //   k_capture_filter the pcap predicate of BuildFilterStr (cap/cap_util.cpp:67-144), SURVEY §8f-4.
 //   k_compact       order-stable VALID index list from the decode launches' per-wave ballots, one
 //                   pass (decoupled look-back over 4096-packet tiles).
 //   k_tcpinfo_encode 21-B TcpInfo hand-off records (bean/TcpInfo.cpp:20-32), staged through LDS.
 //   k_shim          the single-call shims (reference signatures) on a batch of one.
+//   k_tag_table     the key's 256 tags (MD5(key || b)[8..15], b = 0..255), once per context.
 //   k_fill_splitmix synthetic workload generator (bench/tests only).
 // The receive demux is in rsk_demux.hip; host batch helpers in rsk_host.cpp.
 #include <hip/hip_runtime.h>
