@@ -294,16 +294,19 @@ class Codec:
 
     def output_wire_batch(self, payload, pay_off, pay_len, cmd, conv, conn_key, src, dst, sp, dp, seq, ack, flag,
                           ip_id, wire, wire_off, status, eth: bytes | None = None, id=None,
-                          id_uniform: bytes = b"\0" * 8, pad16: bool = False, stream=None) -> None:
+                          id_uniform: bytes = b"\0" * 8, pad16: bool = False, pad128: bool = False,
+                          stream=None) -> None:
         """RConn::Output + RawTcp::SendRawTcp (libnet IPv4/TCP build with checksums) for n packets
-        (rsk_encode_wire_batch).  eth=None: LIBNET_RAW4 layout; else a 14-byte link header."""
+        (rsk_encode_wire_batch).  eth=None: LIBNET_RAW4 layout; else a 14-byte link header.  pad16 /
+        pad128 set RSK_ENC_ZERO_PAD16 / RSK_ENC_ZERO_PAD128."""
         n = pay_len.numel()
         ein = _abi.EncodeIn(_ptr(payload), _ptr(pay_off), _ptr(pay_len), _ptr(cmd), _ptr(conv),
                             _ptr(conn_key), _ptr(id),
                             (ctypes.c_uint8 * 8)(*bytes(id_uniform)[:8].ljust(8, b"\0")))
         win = _abi.WireIn(_ptr(src), _ptr(dst), _ptr(sp), _ptr(dp), _ptr(seq), _ptr(ack), _ptr(flag), _ptr(ip_id),
                           (ctypes.c_uint8 * 14)(*(bytes(eth or b"")[:14].ljust(14, b"\0"))), 1 if eth else 0)
-        eout = _abi.EncodeOut(_ptr(wire), _ptr(wire_off), _ptr(status), _abi.ENC_ZERO_PAD16 if pad16 else 0)
+        eout = _abi.EncodeOut(_ptr(wire), _ptr(wire_off), _ptr(status),
+                              (_abi.ENC_ZERO_PAD16 if pad16 else 0) | (_abi.ENC_ZERO_PAD128 if pad128 else 0))
         _check(lib().rsk_encode_wire_batch(self._ctx, n, ctypes.byref(ein), ctypes.byref(win), ctypes.byref(eout),
                                            _stream(stream)), "rsk_encode_wire_batch")
 

@@ -20,14 +20,14 @@ KEY = b"hello135"
 
 @pytest.mark.parametrize("eth", [False, True])
 @pytest.mark.parametrize("layout", ["aligned", "odd_payload", "odd_wire"])
-@pytest.mark.parametrize("pad16", [False, True])
+@pytest.mark.parametrize("pad", [0, 16, 128])
 @pytest.mark.parametrize("mix", ["mixed", "short", "bimodal", "long"])
 # shipped kernel only; RSK_LIB=librsk_ab.so RSK_WIRE_VARIANTS=0,1,...,9 covers the A/B build
 @pytest.mark.parametrize("variant", [int(v) for v in os.environ.get("RSK_WIRE_VARIANTS", "0").split(",")])
-def test_wire_batch(codec, gpu, oracle, eth, layout, pad16, mix, variant):
+def test_wire_batch(codec, gpu, oracle, eth, layout, pad, mix, variant):
     import torch
 
-    rng = np.random.default_rng(hash((eth, layout, pad16, mix)) & 0xFFFF)
+    rng = np.random.default_rng(hash((eth, layout, pad, mix)) & 0xFFFF)
     lens = [0, 1, 2, 8, 9, 10, 11, 12, 15, 16, 17, 31, 32, 33, 100, 1000, 1400, 1468, 1469, 1470] + \
         list(rng.integers(1200 if mix == "long" else 1, 1470 if mix in ("mixed", "long") else 160, 400))
     # "long": every set's mean frame >= 1024 B, so the deferred-tag copy also meets the 20 edge lengths
@@ -38,7 +38,7 @@ def test_wire_batch(codec, gpu, oracle, eth, layout, pad16, mix, variant):
     pitch_p = 1504
     pay_off = (np.arange(n) * pitch_p + (np.arange(n) % 13 if layout == "odd_payload" else 0)).astype(np.uint64)
     payload = rng.integers(0, 256, n * pitch_p + 64, dtype=np.uint8)
-    pitch_w = 1600
+    pitch_w = 1664 if pad == 128 else 1600  # PAD128 needs every slot's padded end inside the slot
     wire_off = (np.arange(n) * pitch_w + (5 if layout == "odd_wire" else 0)).astype(np.uint64)
     cmd = rng.integers(0, 5, n).astype(np.uint8)
     conv = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
@@ -62,7 +62,7 @@ def test_wire_batch(codec, gpu, oracle, eth, layout, pad16, mix, variant):
                             dev(dst, gpu, np.int32), dev(sp, gpu, np.int16), dev(dp, gpu, np.int16),
                             dev(seq, gpu, np.int32), dev(ack, gpu, np.int32), dev(flag, gpu), dev(ipid, gpu, np.int16),
                             wire, dev(wire_off, gpu, np.int64), status, eth=ethb, id_uniform=workload.ID_UNIFORM,
-                            pad16=pad16)
+                            pad16=pad == 16, pad128=pad == 128)
     if variant:
         codec.set_wire_variant(0)
     torch.cuda.synchronize()
@@ -80,9 +80,9 @@ def test_wire_batch(codec, gpu, oracle, eth, layout, pad16, mix, variant):
         assert st[i] == len(w), i
         o = int(wire_off[i])
         exp[o: o + len(w)] = np.frombuffer(w, np.uint8)
-        if pad16:
+        if pad:
             e = o + len(w)
-            exp[e: (e + 15) // 16 * 16] = 0
+            exp[e: (e + pad - 1) // pad * pad] = 0
         g = got[o: o + len(w)].tobytes()
         assert py_csum(g[L: L + 20]) == 0, i                      # IPv4 header checksum verifies
         pseudo = g[L + 12: L + 20] + struct.pack("!BBH", 0, 6, len(w) - L - 20)

@@ -19,7 +19,9 @@ def main():
     ap.add_argument("--packets", type=int, default=0)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--wire-align", type=int, default=16, help="wire packet pitch alignment (bytes)")
+    ap.add_argument("--wire-align", type=int, default=0,
+                    help="wire packet pitch alignment (bytes); 0 = the frame slot rule (128 with PAD128 for "
+                         "mixed lengths, else 16)")
     ap.add_argument("--wire-variants", default="", help="also time these rsk__set_wire_variant values (A/B)")
     args = ap.parse_args()
     import torch
@@ -41,7 +43,8 @@ def main():
     sp, dp, ipid = ri(2**15, torch.int16) + 1, ri(2**15, torch.int16) + 1, ri(2**15, torch.int16)
     flag = torch.full((n,), 0x18, dtype=torch.uint8, device=dev)
     pmax = workload.CONFIGS[args.config][3]
-    al = args.wire_align
+    al = args.wire_align or (128 if d.pad == 128 else 16)
+    wpad = dict(pad16=al != 128, pad128=al == 128)
     p4, pe = (40 + 31 + pmax + al - 1) // al * al, (54 + 31 + pmax + al - 1) // al * al
     wire4 = torch.empty(n * p4, dtype=torch.uint8, device=dev)
     wiree = torch.empty(n * pe, dtype=torch.uint8, device=dev)
@@ -57,10 +60,10 @@ def main():
         "encode": lambda: cx.output_batch(*common, w.frame, w.frame_off, w.status, id_uniform=workload.ID_UNIFORM,
                                           pad16=d.pad == 16, pad128=d.pad == 128, stream=s),
         "encode_wire_raw4": lambda: cx.output_wire_batch(*common, src, dst, sp, dp, seq, ack, flag, ipid, wire4, off4,
-                                                         st4, id_uniform=workload.ID_UNIFORM, pad16=True, stream=s),
+                                                         st4, id_uniform=workload.ID_UNIFORM, stream=s, **wpad),
         "encode_wire_eth": lambda: cx.output_wire_batch(*common, src, dst, sp, dp, seq, ack, flag, ipid, wiree, offe,
-                                                        ste, eth=eth, id_uniform=workload.ID_UNIFORM, pad16=True,
-                                                        stream=s),
+                                                        ste, eth=eth, id_uniform=workload.ID_UNIFORM, stream=s,
+                                                        **wpad),
         "decode": lambda: cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, w.dec, stream=s),
         "parse_decode": lambda: cx.rawinput_batch(wiree, offe, ste, ste, 1, 0, tcp, pdec, stream=s),
     }
@@ -69,10 +72,10 @@ def main():
     for v in ([1, 2, 3] if ab else []) + [int(x) for x in args.wire_variants.split(",") if x]:
         ops[f"encode_wire_raw4_v{v}"] = (lambda v=v: (cx.set_wire_variant(v), cx.output_wire_batch(
             *common, src, dst, sp, dp, seq, ack, flag, ipid, wire4, off4, st4, id_uniform=workload.ID_UNIFORM,
-            pad16=True, stream=s), cx.set_wire_variant(0)))
+            stream=s, **wpad), cx.set_wire_variant(0)))
         ops[f"encode_wire_eth_v{v}"] = (lambda v=v: (cx.set_wire_variant(v), cx.output_wire_batch(
             *common, src, dst, sp, dp, seq, ack, flag, ipid, wiree, offe, ste, eth=eth, id_uniform=workload.ID_UNIFORM,
-            pad16=True, stream=s), cx.set_wire_variant(0)))
+            stream=s, **wpad), cx.set_wire_variant(0)))
     # fake-TCP connection state: seq / IP id of a send batch over 64 connections, ack of a receive batch
     conn64 = (torch.arange(n, device=dev, dtype=torch.int64) % 64).to(torch.int32)
     cseq, cack = torch.zeros(64, dtype=torch.int32, device=dev), torch.zeros(64, dtype=torch.int32, device=dev)
