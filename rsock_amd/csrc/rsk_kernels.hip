@@ -825,6 +825,15 @@ struct WireArgs {
 // one's-complement sum of the little-endian 16-bit halves of w (RFC 1071 is byte-order agnostic:
 // summing LE halfwords and storing ~sum little-endian gives the big-endian checksum bytes)
 __device__ __forceinline__ uint32_t hsum(uint32_t w) { return (w & 0xffffu) + (w >> 16); }
+// acc + the four words' 16-bit halves: one v_dot2_u32_u16 (halves x (1, 1)) per word
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t hsum4(const uint4 &v, uint32_t acc) {
+    const u16x2 one = {1, 1};
+    acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, v.x), one, acc, false);
+    acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, v.y), one, acc, false);
+    acc = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, v.z), one, acc, false);
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, v.w), one, acc, false);
+}
 __device__ __forceinline__ uint32_t fold16(uint32_t s) {
     s = (s & 0xffffu) + (s >> 16);
     s = (s & 0xffffu) + (s >> 16);
@@ -984,7 +993,7 @@ __device__ __forceinline__ void copy_wire_pkt(const EncArgs &a, const Lane1 &L, 
                 const int lim = (int)wlen[p] - 16 * (int)k;
                 if (k < nch) {
                     if (lim < 16) v[p][q] = rsk::keep_bytes16(v[p][q], lim);
-                    part += hsum(v[p][q].x) + hsum(v[p][q].y) + hsum(v[p][q].z) + hsum(v[p][q].w);
+                    part = hsum4(v[p][q], part);
                 }
             }
             ck[p] = part;
@@ -1104,7 +1113,7 @@ __device__ __forceinline__ void copy_wire_pkt_dpp(const EncArgs &a, const KeySch
                 const int lim = (int)wlen[p] - 16 * (int)k;
                 if (k < nch) {
                     if (lim < 16) v[p][q] = rsk::keep_bytes16(v[p][q], lim);
-                    part += hsum(v[p][q].x) + hsum(v[p][q].y) + hsum(v[p][q].z) + hsum(v[p][q].w);
+                    part = hsum4(v[p][q], part);
                 }
             }
             ck[p] = part;
@@ -1207,7 +1216,7 @@ __device__ __forceinline__ void copy_wire_flat(const EncArgs &a, const Lane1 &L,
             if (!act[u]) continue;
             uint4 v = funnel16_lane(A[u], B[u], shs[u]);
             if (lims[u] < 16) v = lims[u] > 0 ? rsk::keep_bytes16(v, lims[u]) : make_uint4(0u, 0u, 0u, 0u);
-            const uint32_t s = hsum(v.x) + hsum(v.y) + hsum(v.z) + hsum(v.w);
+            const uint32_t s = hsum4(v, 0u);
             if (s) atomicAdd(&psum[pk[u]], s);
             store_last16<0>(dsts[u], v, lims[u], a.pad != 0u);
         }
