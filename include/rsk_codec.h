@@ -109,18 +109,20 @@ extern "C" {
 typedef struct rsk_ctx rsk_ctx;
 
 /* Create a codec context bound to HIP device `device` for hash key `key` (host pointer, key_len
- * bytes, any length; rsock's default is "hello135", bean/RConfig.h:44).  The key's MD5 message
- * schedule is precomputed here (chaining state of the whole-key blocks, the constant words of the
- * block that carries the payload byte, and the padding block when one is needed), so the kernels
- * compress 1 block per tag for key_len <= 54 and 2 blocks otherwise.  Returns NULL on failure. */
+ * bytes, any length; rsock's default is "hello135", bean/RConfig.h:44).  The tag is
+ * MD5(key || payload[0])[8..15] (util/rhash.cpp:20-41), so a key has 256 tags: the key's MD5
+ * message schedule is precomputed here (chaining state of the whole-key blocks, the constant words
+ * of the block that carries the payload byte, the padding block when one is needed) and one GPU
+ * launch (k_tag_table) compresses the 256 tags into a 2-KB device table that the framing and
+ * verifying kernels stage in LDS.  Synchronous; returns NULL on failure (rsk_last_error). */
 rsk_ctx *rsk_create(const uint8_t *key, uint32_t key_len, int device);
 void rsk_destroy(rsk_ctx *ctx);
 
 /* Streams: a context may be used from several streams at once.  Its device scratch (compaction
- * masks and counts, demux and send-seq tables) is kept per stream, so calls on different streams
+ * ballots and look-back state, demux and send-seq tables) is kept per stream, so calls on different streams
  * never share it; calls on ONE stream must be issued in the order the caller wants them to run
  * (from one host thread at a time, as with any hipStream_t).  The only per-context state the
- * kernels read is the immutable key schedule.
+ * kernels read is the immutable key schedule and tag table.
  *
  * Pre-size the compaction scratch of `stream` (rsk_reserve: the legacy default stream, NULL) for
  * batches of up to n packets.  Batch calls grow it on demand, which waits for that stream to
