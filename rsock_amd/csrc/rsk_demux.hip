@@ -15,16 +15,18 @@
 //   k_dm_flags_prep per-wave ballots of VALID and VALID-control packets, block offsets by look-back;
 //                   cidx[j] = packet of compacted slot j, cep[j] = its epoch (CTRL for singletons)
 //   k_dm_insert     open-addressing table: a slot holds a key fingerprint and the compacted index of
-//                   one packet of its key, so key confirmation reads the immutable input arrays (no
-//                   lane ever waits on another lane's write); atomicMin leaves each key's first
-//                   packet in tmin
-//   k_dm_leader_rank leader of j = tab_min[slot] (or j for a control packet); leader ranks = dense
-//                   segment ids in first-occurrence order by look-back; rank_at, seg_first, n_seg
-//   k_dm_segof_hist radix keys = segment id of each compacted packet, values = its packet index,
-//                   global digit histograms of every pass
-//   k_dm_onesweep   stable LSD pass by segment id (8-bit or narrower digits, as many passes as the
-//                   segment count needs; passes beyond that return at once), per-digit look-back
-//   k_dm_final      perm = sorted values, seg_off from the key boundaries, n_seg / n_valid
+//                   its key's first packet (lowered by CAS), so key confirmation reads the immutable
+//                   input arrays (no lane ever waits on another lane's write)
+//   k_dm_leader_rank leader of j = the slot's index (or j for a control packet); leader ranks = dense
+//                   segment ids in first-occurrence order by look-back; rank_at, seg_first, n_seg;
+//                   the followers (non-leaders) compacted with their leader
+//   k_dm_segof_hist radix keys = segment id of each follower, global digit histograms of every pass
+//   k_dm_onesweep   stable LSD pass of the FOLLOWERS by segment id (8-bit or narrower digits, as many
+//                   passes as the segment count needs; passes beyond that, and tiles past the
+//                   follower count, return at once), per-digit look-back
+//   k_dm_final      leaders merged with the sorted followers: perm, seg_off, n_seg / n_valid
+// (round 3: only followers are sorted — leaders already stand in segment order — so a batch of
+// mostly single-packet segments skips the sort's work)
 #include <hip/hip_runtime.h>
 
 #include <cstring>
@@ -238,8 +240,12 @@ __device__ __forceinline__ uint64_t key_hash(const Key &k) {
 }
 
 // Global table probe: a slot is one u64, fingerprint (hash bits 32..63) << 32 | the compacted index
-// of the packet that claimed it; a slot with another fingerprint is skipped without touching that
-// packet's fields, a matching fingerprint is confirmed on the full key.
+// of the key's first packet so far.  A slot with another fingerprint is skipped without touching that
+// packet's fields, a matching fingerprint is confirmed on the full key, and the index is lowered by
+// compare-and-swap (the fingerprint half never changes once claimed).  The first access is the CAS
+// itself: it claims an empty slot and returns an occupied one's word, so a new key costs one atomic
+// at the memory side (round 2: a load, a CAS and a separate atomicMin word cost four; the table's
+// atomic request rate is what bounds this kernel).
 __device__ __forceinline__ uint32_t global_probe(const DmIn &a, const uint32_t *cidx, const uint32_t *cep,
                                                  unsigned long long *slots, uint32_t mask, const Key &k,
                                                  uint64_t hv, uint32_t j) {
@@ -247,14 +253,18 @@ __device__ __forceinline__ uint32_t global_probe(const DmIn &a, const uint32_t *
     const unsigned long long mine = ((unsigned long long)fp << 32) | j;
     uint32_t h = (uint32_t)hv & mask;
     for (;;) {
-        unsigned long long e = __hip_atomic_load(slots + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (e == ~0ull) {
-            e = atomicCAS(slots + h, ~0ull, mine);
-            if (e == ~0ull) return h;  // claimed
-        }
+        unsigned long long e = atomicCAS(slots + h, ~0ull, mine);
+        if (e == ~0ull) return h;  // claimed
         if ((uint32_t)(e >> 32) == fp) {
             const uint32_t o = (uint32_t)e;
-            if (key_eq(load_key(a, cidx[o], cep[o]), k)) return h;
+            if (key_eq(load_key(a, cidx[o], cep[o]), k)) {
+                while ((uint32_t)e > j) {  // lower the key's first index to j
+                    const unsigned long long f = atomicCAS(slots + h, e, mine);
+                    if (f == e) break;
+                    e = f;
+                }
+                return h;
+            }
         }
         h = (h + 1u) & mask;
     }
@@ -262,7 +272,7 @@ __device__ __forceinline__ uint32_t global_probe(const DmIn &a, const uint32_t *
 
 // One block = kInsTile consecutive compacted packets.  Phase 1 groups them by key in an LDS table
 // (same fingerprint scheme, confirmed on the full key) and takes each key's block-minimum index
-// with LDS atomics; phase 2: that minimum packet alone probes the global table and lowers tmin,
+// with LDS atomics; phase 2: that minimum packet alone probes the global table and lowers its index,
 // so a hot key costs one global atomic per block, not one per packet (a single hot word takes
 // ~88 atomics/us: MI355X_MICROARCH.md, dequeue row); phase 3 hands every packet its key's slot.
 constexpr uint32_t kInsItems = 4;
@@ -271,7 +281,7 @@ constexpr uint32_t kLtab = 2 * kInsTile;           // LDS table slots (power of 
 
 __global__ __launch_bounds__(kBlock) void k_dm_insert(DmIn a, const uint32_t *nvp, const uint32_t *cidx,
                                                       const uint32_t *cep, unsigned long long *slots,
-                                                      uint32_t *tmin, uint32_t mask, uint32_t *hslot) {
+                                                      uint32_t mask, uint32_t *hslot) {
     __shared__ unsigned long long ltab[kLtab];
     __shared__ uint32_t lmin[kLtab];  // block-minimum index per key, then (phase 2b) the key's global slot
     const uint32_t nv = *nvp;
@@ -326,9 +336,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_insert(DmIn a, const uint32_t *nv
         if (!((rep >> it) & 1u)) continue;
         const uint32_t j = base + it * kBlock + t;
         const Key &k = kr[it];
-        const uint32_t gh = global_probe(a, cidx, cep, slots, mask, k, key_hash(k), j);
-        if (__hip_atomic_load(tmin + gh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > j) atomicMin(tmin + gh, j);
-        lmin[lpos[it]] = gh;
+        lmin[lpos[it]] = global_probe(a, cidx, cep, slots, mask, k, key_hash(k), j);
     }
     __syncthreads();
 #pragma unroll
@@ -439,13 +447,15 @@ __global__ __launch_bounds__(kBlock) void k_dm_flags_prep(DmIn a, unsigned long 
     }
 }
 
-// leader + scan + rank in one pass: lead_of[j] = the first packet of j's key (tmin of its slot, or j
-// for a control packet); the leaders' dense ranks (segment ids in first-occurrence order) by
-// decoupled look-back; rank_at[leader], seg_first[rank]; the last tile writes the segment count.
-// Block 0 also clears the radix digit histograms the next launch accumulates.
+// leader + scan + rank in one pass: the leader of compacted packet j is the first packet of its key
+// (the index half of its table slot, or j for a control packet); the leaders' dense ranks (segment
+// ids in first-occurrence order) by decoupled look-back; rank_at[leader], seg_first[rank]; the last
+// tile writes the segment count.  Followers (every other packet) are compacted by the same count:
+// follower f = j - (leaders before j) gets fkey[f] = its leader, fval[f] = its packet index.  Block 0
+// also clears the radix digit histograms the next launch accumulates.
 __global__ __launch_bounds__(kBlock) void k_dm_leader_rank(const uint32_t *nvp, const uint32_t *hslot,
-                                                           const uint32_t *tmin, const uint32_t *cidx,
-                                                           unsigned long long *st_l, uint32_t *lead_of,
+                                                           const unsigned long long *slots, const uint32_t *cidx,
+                                                           unsigned long long *st_l, uint32_t *fkey, uint32_t *fval,
                                                            uint32_t *rank_at, uint32_t *seg_first, uint32_t *nsegp,
                                                            uint32_t *ghist) {
     __shared__ uint64_t ml[kRows][kWaves];
@@ -455,7 +465,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_leader_rank(const uint32_t *nvp, 
     if (b == 0u)
         for (uint32_t q = t; q < 4u * 256u; q += kBlock) ghist[q] = 0u;
     uint32_t isl = 0;  // bit r: row r's item is its key's leader
-    uint32_t hs[kRows];
+    uint32_t hs[kRows], lead[kRows];
 #pragma unroll
     for (uint32_t r = 0; r < kRows; ++r) {
         const uint32_t j = b * kTile + r * kBlock + t;
@@ -464,12 +474,12 @@ __global__ __launch_bounds__(kBlock) void k_dm_leader_rank(const uint32_t *nvp, 
 #pragma unroll
     for (uint32_t r = 0; r < kRows; ++r) {
         const uint32_t j = b * kTile + r * kBlock + t;
-        bool l = false;
-        if (j < nv) {
-            const uint32_t lead = hs[r] == kNone ? j : tmin[hs[r]];
-            lead_of[j] = lead;
-            l = lead == j;
-        }
+        lead[r] = hs[r] == kNone ? j : (uint32_t)slots[hs[r]];
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < kRows; ++r) {
+        const uint32_t j = b * kTile + r * kBlock + t;
+        const bool l = j < nv && lead[r] == j;
         const uint64_t bl = __ballot(l);
         if (lane == 0u) ml[r][w] = bl;
         isl |= l ? 1u << r : 0u;
@@ -488,52 +498,55 @@ __global__ __launch_bounds__(kBlock) void k_dm_leader_rank(const uint32_t *nvp, 
     const uint64_t lt = lanemask_lt(lane);
 #pragma unroll
     for (uint32_t r = 0; r < kRows; ++r) {
-        if (!((isl >> r) & 1u)) continue;
         const uint32_t j = b * kTile + r * kBlock + t;
-        const uint32_t rk = pre + ol[r] + (uint32_t)__popcll(ml[r][w] & lt);
-        rank_at[j] = rk;
-        seg_first[rk] = cidx[j];
+        if (j >= nv) continue;
+        const uint32_t before = pre + ol[r] + (uint32_t)__popcll(ml[r][w] & lt);  // leaders before j
+        const uint32_t pk = cidx[j];
+        if ((isl >> r) & 1u) {
+            rank_at[j] = before;
+            seg_first[before] = pk;
+        } else {
+            fkey[j - before] = lead[r];
+            fval[j - before] = pk;
+        }
     }
 }
 
-// segof + the global digit histograms of every radix pass: keys[j] = segment id of compacted packet
-// j, vals[j] = its packet index; one tile of kTile packets per block, LDS histograms per pass, one
-// global atomic per non-empty bin.
+// The followers' radix keys + the global digit histograms of every radix pass: fkey[f] (its leader,
+// written by k_dm_leader_rank) becomes the leader's segment id in place; one tile of kTile followers
+// per block, LDS histograms per pass, one global atomic per non-empty bin.  Leaders are not sorted:
+// they already stand in segment order (k_dm_final).
 __global__ __launch_bounds__(kBlock) void k_dm_segof_hist(const uint32_t *nvp, const uint32_t *nsegp,
-                                                          const uint32_t *lead_of, const uint32_t *rank_at,
-                                                          const uint32_t *cidx, uint32_t *keys, uint32_t *vals,
+                                                          const uint32_t *rank_at, uint32_t *keys,
                                                           uint32_t *ghist) {
     __shared__ uint32_t lh[4][256];
-    const uint32_t nv = *nvp, ns = *nsegp, t = threadIdx.x, lane = t & 63u;
+    const uint32_t ns = *nsegp, nf = *nvp - ns, t = threadIdx.x, lane = t & 63u;
     const uint32_t base = blockIdx.x * kTile;
-    if (base >= nv) return;  // block-uniform
+    if (base >= nf) return;  // block-uniform
     const uint32_t np = n_passes(ns), width = digit_width(ns), dm = (1u << width) - 1u;
 #pragma unroll
     for (int p = 0; p < 4; ++p) lh[p][t] = 0u;
     __syncthreads();
-    uint32_t kk[kItems], ld[kItems];  // all lead_of loads, then all rank_at gathers, in flight at once
+    uint32_t kk[kItems], ld[kItems];  // all leader loads, then all rank_at gathers, in flight at once
 #pragma unroll
     for (uint32_t r = 0; r < kItems; ++r) {
-        const uint32_t j = base + r * kBlock + t;
-        ld[r] = j < nv ? lead_of[j] : 0u;
+        const uint32_t f = base + r * kBlock + t;
+        ld[r] = f < nf ? keys[f] : 0u;
     }
 #pragma unroll
     for (uint32_t r = 0; r < kItems; ++r) {
-        const uint32_t j = base + r * kBlock + t;
-        kk[r] = j < nv ? rank_at[ld[r]] : 0u;
+        const uint32_t f = base + r * kBlock + t;
+        kk[r] = f < nf ? rank_at[ld[r]] : 0u;
     }
 #pragma unroll
     for (uint32_t r = 0; r < kItems; ++r) {
-        const uint32_t j = base + r * kBlock + t;
-        if (j < nv) {
-            keys[j] = kk[r];
-            vals[j] = cidx[j];  // the packet index rides through the sort
-        }
+        const uint32_t f = base + r * kBlock + t;
+        if (f < nf) keys[f] = kk[r];
     }
     for (uint32_t p = 0; p < np; ++p) {  // np is block-uniform
 #pragma unroll
         for (uint32_t r = 0; r < kItems; ++r) {
-            const bool v = base + r * kBlock + t < nv;
+            const bool v = base + r * kBlock + t < nf;
             const uint32_t d = (kk[r] >> (width * p)) & dm;
             const uint64_t peers = digit_peers(v, d, width);
             if (v && (peers & lanemask_lt(lane)) == 0) atomicAdd(&lh[p][d], (uint32_t)__popcll(peers));
@@ -554,7 +567,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_onesweep(uint32_t pass, const uin
     __shared__ uint32_t run[256], lbase[256], dbase[256];
     __shared__ uint32_t wcnt[kWaves][256];
     __shared__ uint32_t sk[kTile], sv[kTile];
-    const uint32_t nv = *nvp, ns = *nsegp, tile = blockIdx.x;
+    const uint32_t ns = *nsegp, nv = *nvp - ns, tile = blockIdx.x;  // nv: the followers being sorted
     if (pass >= n_passes(ns) || tile * kTile >= nv) return;  // block-uniform; no later tile waits on these
     const uint32_t width = digit_width(ns), sh = width * pass, dm = (1u << width) - 1u;
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
@@ -645,11 +658,15 @@ __global__ __launch_bounds__(kBlock) void k_dm_onesweep(uint32_t pass, const uin
     }
 }
 
+// Merge of the leaders (segment order already) with the sorted followers (segment id, arrival order):
+// segment s starts at s + (followers of segments before s), a lower bound in the sorted keys, and its
+// leader goes there; the follower at sorted position p with segment id r lands at r + 1 + p (r
+// leaders up to and including its own, p followers before it).
 __global__ __launch_bounds__(kBlock) void k_dm_final(const uint32_t *nvp, const uint32_t *nsegp, const uint32_t *kA,
                                                      const uint32_t *vA, const uint32_t *kB, const uint32_t *vB,
-                                                     uint32_t *perm, uint32_t *seg_off,
+                                                     const uint32_t *seg_first, uint32_t *perm, uint32_t *seg_off,
                                                      uint32_t *n_seg, uint32_t *n_valid) {
-    const uint32_t nv = *nvp, ns = *nsegp;
+    const uint32_t nv = *nvp, ns = *nsegp, nf = nv - ns;
     const uint32_t passes = n_passes(ns);  // effective passes; pass p writes B when p is even
     const bool inB = ((passes - 1u) & 1u) == 0u;
     const uint32_t *keys = inB ? kB : kA;
@@ -660,19 +677,25 @@ __global__ __launch_bounds__(kBlock) void k_dm_final(const uint32_t *nvp, const 
         *n_valid = nv;
         seg_off[ns] = nv;
     }
-    if (k >= nv) return;
-    perm[k] = vals[k];
-    const uint32_t key = keys[k];
-    if (k == 0 || keys[k - 1] != key) seg_off[key] = k;
+    if (k < ns) {
+        uint32_t lo = 0, hi = nf;  // followers with segment id < k
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (keys[mid] < k) lo = mid + 1u;
+            else hi = mid;
+        }
+        seg_off[k] = k + lo;
+        perm[k + lo] = seg_first[k];
+    }
+    if (k < nf) perm[keys[k] + 1u + k] = vals[k];
 }
 
 // ---- workspace ------------------------------------------------------------------------------
 struct DmWs {
-    uint32_t *cidx, *cep, *hslot, *lead_of, *rank_at;
+    uint32_t *cidx, *cep, *hslot, *rank_at;
     uint32_t *kA, *vA, *kB, *vB;
     uint32_t *ghist;
-    unsigned long long *slots;  // slots | tmin | look-back states: one 0xff fill per call
-    uint32_t *tmin;
+    unsigned long long *slots;  // slots | look-back states: one 0xff fill per call
     unsigned long long *st_v, *st_c, *st_l, *st_r;
     size_t fill_bytes;
     uint32_t *nv, *nseg;
@@ -697,7 +720,6 @@ size_t dm_layout(uint32_t n, uint8_t *base, DmWs *w) {
     d.cidx = (uint32_t *)take(4ull * n);
     d.cep = (uint32_t *)take(4ull * n);
     d.hslot = (uint32_t *)take(4ull * n);
-    d.lead_of = (uint32_t *)take(4ull * n);
     d.rank_at = (uint32_t *)take(4ull * n);
     d.kA = (uint32_t *)take(4ull * n);
     d.vA = (uint32_t *)take(4ull * n);
@@ -708,7 +730,6 @@ size_t dm_layout(uint32_t n, uint8_t *base, DmWs *w) {
     d.nseg = (uint32_t *)take(8);
     const size_t fill0 = off;
     d.slots = (unsigned long long *)take(8ull * T);
-    d.tmin = (uint32_t *)take(4ull * T);
     d.st_v = (unsigned long long *)take(8ull * nt);
     d.st_c = (unsigned long long *)take(8ull * nt);
     d.st_l = (unsigned long long *)take(8ull * nt);
@@ -758,19 +779,18 @@ extern "C" int rsk_demux_batch(rsk_ctx *c, uint32_t n, const rsk_demux_in *in, u
     a.dst = in->dst;
     a.n = n;
     a.fields = fields;
-    // one fill: the key table (slots, tmin) and every look-back state word start as all-ones
+    // one fill: the key table and every look-back state word start as all-ones
     hipError_t e = hipMemsetAsync(w.slots, 0xff, w.fill_bytes, s);
     if (e != hipSuccess) { rsk::set_error("hipMemsetAsync(table)", e); return RSK_EDEVICE; }
     const uint32_t nb = w.nb;
     hipLaunchKernelGGL(k_dm_flags_prep, dim3(w.nt), dim3(kBlock), 0, s, a, w.st_v, w.st_c, w.cidx, w.cep, w.nv);
     hipLaunchKernelGGL(k_dm_insert, dim3((n + kInsTile - 1) / kInsTile), dim3(kBlock), 0, s, a, w.nv, w.cidx,
-                       w.cep, w.slots, w.tmin, w.tsize - 1u, w.hslot);
-    hipLaunchKernelGGL(k_dm_leader_rank, dim3(w.nt), dim3(kBlock), 0, s, w.nv, w.hslot, w.tmin, w.cidx, w.st_l,
-                       w.lead_of, w.rank_at, out->seg_first, w.nseg, w.ghist);
-    hipLaunchKernelGGL(k_dm_segof_hist, dim3(w.nt), dim3(kBlock), 0, s, w.nv, w.nseg, w.lead_of, w.rank_at, w.cidx,
-                       w.kA, w.vA, w.ghist);
+                       w.cep, w.slots, w.tsize - 1u, w.hslot);
+    hipLaunchKernelGGL(k_dm_leader_rank, dim3(w.nt), dim3(kBlock), 0, s, w.nv, w.hslot, w.slots, w.cidx, w.st_l,
+                       w.kA, w.vA, w.rank_at, out->seg_first, w.nseg, w.ghist);
+    hipLaunchKernelGGL(k_dm_segof_hist, dim3(w.nt), dim3(kBlock), 0, s, w.nv, w.nseg, w.rank_at, w.kA, w.ghist);
     if ((r = rsk::launch_check("k_dm_segof_hist"))) return r;
-    // passes for the worst case (every packet its own segment); surplus passes return at once
+    // passes for the largest possible segment count (n); surplus passes return at once
     uint32_t maxbits = 1;
     while (maxbits < 32 && (1ull << maxbits) < n) ++maxbits;
     const uint32_t passes = (maxbits + 7) / 8;
@@ -782,7 +802,7 @@ extern "C" int rsk_demux_batch(rsk_ctx *c, uint32_t n, const rsk_demux_in *in, u
         if ((r = rsk::launch_check("k_dm_onesweep"))) return r;
     }
     hipLaunchKernelGGL(k_dm_final, dim3(nb), dim3(kBlock), 0, s, w.nv, w.nseg, w.kA, w.vA, w.kB, w.vB,
-                       out->perm, out->seg_off, out->n_seg, out->n_valid);
+                       out->seg_first, out->perm, out->seg_off, out->n_seg, out->n_valid);
     return rsk::launch_check("k_dm_final");
 }
 

@@ -798,16 +798,23 @@ __global__ __launch_bounds__(kBlock) void k_copy_probe(EncArgs a) {
 #endif
 
 // Tiled mapping: wave t takes packets [64t, 64t + 64) (coalesced descriptor loads; the co-resident
-// waves each stream their own region of the arenas).
-template <int MODE, int PU, int U, int NT>
+// waves each stream their own region of the arenas).  SET < 64 (A/B build only): wave t takes
+// [SET t, SET t + SET), lanes SET.. idle in phase 1, so each wave streams a smaller region.
+template <int MODE, int PU, int U, int NT, int SET = 64>
 __global__ __launch_bounds__(kBlock) void k_encode(EncArgs a, KeySched ks) {
     __shared__ CopyRec recs[kWavesPerBlock][64];
     __shared__ uint32_t cend[kWavesPerBlock][64];
     stage_tags(ks);
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    const uint64_t base = ((uint64_t)blockIdx.x * kWavesPerBlock + w) * 64u;
+    const uint64_t base = ((uint64_t)blockIdx.x * kWavesPerBlock + w) * (uint64_t)SET;
     if (base >= a.n) return;  // wave-uniform; no block barriers below
-    encode_set<MODE, PU, U, NT>(a, ks, base + lane, lane, recs[w], cend[w]);
+    if constexpr (SET < 64) {
+        EncArgs b = a;
+        b.n = (uint32_t)(base + SET < a.n ? base + SET : a.n);
+        encode_set<MODE, PU, U, NT>(b, ks, lane < (uint32_t)SET ? base + lane : b.n, lane, recs[w], cend[w]);
+    } else {
+        encode_set<MODE, PU, U, NT>(a, ks, base + lane, lane, recs[w], cend[w]);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2276,10 +2283,11 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 // 9 / 10 / 14 / 15 / 16 = pipelined with 6 / 8 / 3 / 5 / 2 packets per batch (11 = 4);
 // 12 / 13 = k_copy_probe (memory-side ceiling probe, wrong bytes) with 12 / 4 packets per batch;
 // 18 = shipped with the tag in the copy loop for every per-packet set; 19 / 20 / 21 = shipped with
-// the flat sets' tag behind the first chunk loads, 4 / 2 / 8 chunk rows per flat iteration.
+// the flat sets' tag behind the first chunk loads, 4 / 2 / 8 chunk rows per flat iteration;
+// 23 / 24 / 25 / 26 = shipped with 32 / 16 / 8 / 4 packets per wave (smaller region per wave).
 // v + 100 * cap (cap 1..4): the same kernel held to `cap` blocks per CU by unused LDS.
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
-    if (!c || v < 0 || v % 100 > 22 || v / 100 > 4) return RSK_EINVAL;
+    if (!c || v < 0 || v % 100 > 26 || v / 100 > 4) return RSK_EINVAL;
     c->enc_variant = v;
     return RSK_OK;
 }
@@ -2403,6 +2411,10 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         case 20: hipLaunchKernelGGL((k_encode<11, 4, 2, -1>), gd, bd, lds, st, a, c->ks); break;
         case 21: hipLaunchKernelGGL((k_encode<11, 4, 8, -1>), gd, bd, lds, st, a, c->ks); break;
         case 22: hipLaunchKernelGGL((k_encode<9, 4, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 23: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 32>), dim3(grid * 2), bd, lds, st, a, c->ks); break;
+        case 24: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 16>), dim3(grid * 4), bd, lds, st, a, c->ks); break;
+        case 25: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8>), dim3(grid * 8), bd, lds, st, a, c->ks); break;
+        case 26: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 4>), dim3(grid * 16), bd, lds, st, a, c->ks); break;
         default: hipLaunchKernelGGL((k_encode<11, 4, 4, -1>), gd, bd, lds, st, a, c->ks); break;
     }
 #else
