@@ -275,7 +275,13 @@ __device__ __forceinline__ uint32_t global_probe(const DmIn &a, const uint32_t *
 // with LDS atomics; phase 2: that minimum packet alone probes the global table and lowers its index,
 // so a hot key costs one global atomic per block, not one per packet (a single hot word takes
 // ~88 atomics/us: MI355X_MICROARCH.md, dequeue row); phase 3 hands every packet its key's slot.
+// Epoch-local keys (round 3): with CMD_BARRIER the epoch is part of the key and epochs only grow
+// with the packet index, so a key whose epoch lies strictly between the epochs of the tile's first
+// and last data packets cannot occur outside the tile: its block minimum IS its first packet and it
+// never touches the global table (hslot = kLeadTag | leader).  Only the tile's first and last epochs
+// go to the table: C4 (5 % control packets) sends ~2 % of its keys there instead of all of them.
 constexpr uint32_t kInsItems = 4;
+constexpr uint32_t kLeadTag = 0x80000000u;  // hslot: leader index (table slots are < 2^31)
 constexpr uint32_t kInsTile = kBlock * kInsItems;  // 1024 packets (24 KB LDS: 6 waves per SIMD)
 constexpr uint32_t kLtab = 2 * kInsTile;           // LDS table slots (power of 2)
 
@@ -284,12 +290,17 @@ __global__ __launch_bounds__(kBlock) void k_dm_insert(DmIn a, const uint32_t *nv
                                                       uint32_t mask, uint32_t *hslot) {
     __shared__ unsigned long long ltab[kLtab];
     __shared__ uint32_t lmin[kLtab];  // block-minimum index per key, then (phase 2b) the key's global slot
+    __shared__ uint32_t elo, ehi;     // epochs of the tile's first and last data packets
     const uint32_t nv = *nvp;
     const uint32_t base = blockIdx.x * kInsTile, t = threadIdx.x;
     if (base >= nv) return;  // block-uniform
     for (uint32_t q = t; q < kLtab; q += kBlock) {
         ltab[q] = ~0ull;
         lmin[q] = kNone;
+    }
+    if (t == 0) {
+        elo = kNone;
+        ehi = 0u;
     }
     __syncthreads();
     // (keys stay in registers; confirming another packet's key reads the immutable inputs: keeping
@@ -325,6 +336,24 @@ __global__ __launch_bounds__(kBlock) void k_dm_insert(DmIn a, const uint32_t *nv
         lpos[it] = h;
         atomicMin(&lmin[h], j);
     }
+    {  // the tile's epoch range (data packets only; control packets carry kCtrl)
+        uint32_t lo = kNone, hi = 0u;
+#pragma unroll
+        for (uint32_t it = 0; it < kInsItems; ++it)
+            if (lpos[it] != kNone) {
+                lo = min(lo, kr[it].ep);
+                hi = max(hi, kr[it].ep);
+            }
+#pragma unroll
+        for (int off = 32; off; off >>= 1) {
+            lo = min(lo, (uint32_t)__shfl_xor((int)lo, off));
+            hi = max(hi, (uint32_t)__shfl_xor((int)hi, off));
+        }
+        if ((t & 63u) == 0u && lo != kNone) {
+            atomicMin(&elo, lo);
+            atomicMax(&ehi, hi);
+        }
+    }
     __syncthreads();
     uint32_t rep = 0;  // bit it: this thread's item `it` is its key's first packet in the block
 #pragma unroll
@@ -336,7 +365,8 @@ __global__ __launch_bounds__(kBlock) void k_dm_insert(DmIn a, const uint32_t *nv
         if (!((rep >> it) & 1u)) continue;
         const uint32_t j = base + it * kBlock + t;
         const Key &k = kr[it];
-        lmin[lpos[it]] = global_probe(a, cidx, cep, slots, mask, k, key_hash(k), j);
+        lmin[lpos[it]] = k.ep == elo || k.ep == ehi ? global_probe(a, cidx, cep, slots, mask, k, key_hash(k), j)
+                                                    : kLeadTag | j;
     }
     __syncthreads();
 #pragma unroll
@@ -474,7 +504,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_leader_rank(const uint32_t *nvp, 
 #pragma unroll
     for (uint32_t r = 0; r < kRows; ++r) {
         const uint32_t j = b * kTile + r * kBlock + t;
-        lead[r] = hs[r] == kNone ? j : (uint32_t)slots[hs[r]];
+        lead[r] = hs[r] == kNone ? j : (hs[r] & kLeadTag) ? hs[r] & ~kLeadTag : (uint32_t)slots[hs[r]];
     }
 #pragma unroll
     for (uint32_t r = 0; r < kRows; ++r) {
@@ -516,13 +546,52 @@ __global__ __launch_bounds__(kBlock) void k_dm_leader_rank(const uint32_t *nvp, 
 // written by k_dm_leader_rank) becomes the leader's segment id in place; one tile of kTile followers
 // per block, LDS histograms per pass, one global atomic per non-empty bin.  Leaders are not sorted:
 // they already stand in segment order (k_dm_final).
+// At most kSmallF followers (a batch of mostly single-packet segments): block 0 sorts them alone, in
+// place, by counting for each follower the followers that precede it in (segment id, arrival) order,
+// and the radix passes return at once.
+constexpr uint32_t kSmallF = 1024;
 __global__ __launch_bounds__(kBlock) void k_dm_segof_hist(const uint32_t *nvp, const uint32_t *nsegp,
-                                                          const uint32_t *rank_at, uint32_t *keys,
+                                                          const uint32_t *rank_at, uint32_t *keys, uint32_t *vals,
                                                           uint32_t *ghist) {
     __shared__ uint32_t lh[4][256];
+    __shared__ uint32_t sk[kSmallF], sv[kSmallF];
     const uint32_t ns = *nsegp, nf = *nvp - ns, t = threadIdx.x, lane = t & 63u;
     const uint32_t base = blockIdx.x * kTile;
     if (base >= nf) return;  // block-uniform
+    if (nf <= kSmallF) {  // block 0 only (base = 0)
+        constexpr uint32_t kPer = kSmallF / kBlock;
+        uint32_t ld[kPer], kk[kPer], vv[kPer];
+#pragma unroll
+        for (uint32_t r = 0; r < kPer; ++r) {
+            const uint32_t f = r * kBlock + t;
+            ld[r] = f < nf ? keys[f] : 0u;
+            vv[r] = f < nf ? vals[f] : 0u;
+        }
+#pragma unroll
+        for (uint32_t r = 0; r < kPer; ++r) {
+            const uint32_t f = r * kBlock + t;
+            kk[r] = f < nf ? rank_at[ld[r]] : 0u;
+            if (f < nf) {  // every global read is consumed before the barrier: the writes below are in place
+                sk[f] = kk[r];
+                sv[f] = vv[r];
+            }
+        }
+        __syncthreads();
+        uint32_t pos[kPer] = {};
+        for (uint32_t g = 0; g < nf; ++g) {  // sk[g] is an LDS broadcast
+            const uint32_t kg = sk[g];
+#pragma unroll
+            for (uint32_t r = 0; r < kPer; ++r) pos[r] += kg < kk[r] || (kg == kk[r] && g < r * kBlock + t);
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t r = 0; r < kPer; ++r) {
+            if (r * kBlock + t >= nf) continue;
+            keys[pos[r]] = kk[r];
+            vals[pos[r]] = sv[r * kBlock + t];
+        }
+        return;
+    }
     const uint32_t np = n_passes(ns), width = digit_width(ns), dm = (1u << width) - 1u;
 #pragma unroll
     for (int p = 0; p < 4; ++p) lh[p][t] = 0u;
@@ -568,7 +637,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_onesweep(uint32_t pass, const uin
     __shared__ uint32_t wcnt[kWaves][256];
     __shared__ uint32_t sk[kTile], sv[kTile];
     const uint32_t ns = *nsegp, nv = *nvp - ns, tile = blockIdx.x;  // nv: the followers being sorted
-    if (pass >= n_passes(ns) || tile * kTile >= nv) return;  // block-uniform; no later tile waits on these
+    if (pass >= n_passes(ns) || tile * kTile >= nv || nv <= kSmallF) return;  // block-uniform; no later tile waits
     const uint32_t width = digit_width(ns), sh = width * pass, dm = (1u << width) - 1u;
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     const uint32_t base = tile * kTile;
@@ -668,7 +737,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_final(const uint32_t *nvp, const 
                                                      uint32_t *n_seg, uint32_t *n_valid) {
     const uint32_t nv = *nvp, ns = *nsegp, nf = nv - ns;
     const uint32_t passes = n_passes(ns);  // effective passes; pass p writes B when p is even
-    const bool inB = ((passes - 1u) & 1u) == 0u;
+    const bool inB = nf > kSmallF && ((passes - 1u) & 1u) == 0u;  // small: sorted in place in A
     const uint32_t *keys = inB ? kB : kA;
     const uint32_t *vals = inB ? vB : vA;
     const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
@@ -788,7 +857,8 @@ extern "C" int rsk_demux_batch(rsk_ctx *c, uint32_t n, const rsk_demux_in *in, u
                        w.cep, w.slots, w.tsize - 1u, w.hslot);
     hipLaunchKernelGGL(k_dm_leader_rank, dim3(w.nt), dim3(kBlock), 0, s, w.nv, w.hslot, w.slots, w.cidx, w.st_l,
                        w.kA, w.vA, w.rank_at, out->seg_first, w.nseg, w.ghist);
-    hipLaunchKernelGGL(k_dm_segof_hist, dim3(w.nt), dim3(kBlock), 0, s, w.nv, w.nseg, w.rank_at, w.kA, w.ghist);
+    hipLaunchKernelGGL(k_dm_segof_hist, dim3(w.nt), dim3(kBlock), 0, s, w.nv, w.nseg, w.rank_at, w.kA, w.vA,
+                       w.ghist);
     if ((r = rsk::launch_check("k_dm_segof_hist"))) return r;
     // passes for the largest possible segment count (n); surplus passes return at once
     uint32_t maxbits = 1;

@@ -817,6 +817,26 @@ __global__ __launch_bounds__(kBlock) void k_encode(EncArgs a, KeySched ks) {
     }
 }
 
+#ifdef RSK_AB
+// A/B build only: persistent form of the SET mapping — the grid holds only resident blocks and each
+// wave strides over SET-packet sets (set w, w + W, ...), so the tag table is staged once per block
+// and the resident waves still sweep the arenas as one compact window.
+template <int MODE, int PU, int U, int NT, int SET>
+__global__ __launch_bounds__(kBlock) void k_encode_gs(EncArgs a, KeySched ks) {
+    __shared__ CopyRec recs[kWavesPerBlock][64];
+    __shared__ uint32_t cend[kWavesPerBlock][64];
+    stage_tags(ks);
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint64_t nsets = ((uint64_t)a.n + SET - 1) / SET, stride = (uint64_t)gridDim.x * kWavesPerBlock;
+    for (uint64_t sidx = (uint64_t)blockIdx.x * kWavesPerBlock + w; sidx < nsets; sidx += stride) {
+        const uint64_t base = sidx * SET;
+        EncArgs b = a;
+        b.n = (uint32_t)(base + SET < a.n ? base + SET : a.n);
+        encode_set<MODE, PU, U, NT>(b, ks, lane < (uint32_t)SET ? base + lane : b.n, lane, recs[w], cend[w]);
+    }
+}
+#endif
+
 // ---------------------------------------------------------------------------------------------
 // Encode straight to wire packets (RConn::Output + RawTcp::SendRawTcp / libnet)
 // ---------------------------------------------------------------------------------------------
@@ -2284,10 +2304,11 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 // 12 / 13 = k_copy_probe (memory-side ceiling probe, wrong bytes) with 12 / 4 packets per batch;
 // 18 = shipped with the tag in the copy loop for every per-packet set; 19 / 20 / 21 = shipped with
 // the flat sets' tag behind the first chunk loads, 4 / 2 / 8 chunk rows per flat iteration;
-// 23 / 24 / 25 / 26 = shipped with 32 / 16 / 8 / 4 packets per wave (smaller region per wave).
+// 23 / 24 / 25 / 26 = shipped with 32 / 16 / 8 / 4 packets per wave (smaller region per wave);
+// 27 / 28 / 29 / 30 = persistent k_encode_gs: SET 16 on 1024 blocks / 8 on 1024 / 16 on 2048 / 32 on 1024.
 // v + 100 * cap (cap 1..4): the same kernel held to `cap` blocks per CU by unused LDS.
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
-    if (!c || v < 0 || v % 100 > 26 || v / 100 > 4) return RSK_EINVAL;
+    if (!c || v < 0 || v % 100 > 30 || v / 100 > 4) return RSK_EINVAL;
     c->enc_variant = v;
     return RSK_OK;
 }
@@ -2415,6 +2436,10 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         case 24: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 16>), dim3(grid * 4), bd, lds, st, a, c->ks); break;
         case 25: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8>), dim3(grid * 8), bd, lds, st, a, c->ks); break;
         case 26: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 4>), dim3(grid * 16), bd, lds, st, a, c->ks); break;
+        case 27: hipLaunchKernelGGL((k_encode_gs<11, 4, 4, -1, 16>), dim3(std::min(grid * 4u, 1024u)), bd, lds, st, a, c->ks); break;
+        case 28: hipLaunchKernelGGL((k_encode_gs<11, 4, 4, -1, 8>), dim3(std::min(grid * 8u, 1024u)), bd, lds, st, a, c->ks); break;
+        case 29: hipLaunchKernelGGL((k_encode_gs<11, 4, 4, -1, 16>), dim3(std::min(grid * 4u, 2048u)), bd, lds, st, a, c->ks); break;
+        case 30: hipLaunchKernelGGL((k_encode_gs<11, 4, 4, -1, 32>), dim3(std::min(grid * 2u, 1024u)), bd, lds, st, a, c->ks); break;
         default: hipLaunchKernelGGL((k_encode<11, 4, 4, -1>), gd, bd, lds, st, a, c->ks); break;
     }
 #else

@@ -63,6 +63,46 @@ def test_demux_many_segments(codec, gpu, oracle, n, fields):
     assert got[0] == exp[0]
 
 
+@pytest.mark.parametrize("n_follow", [0, 1, 17, 1023, 1024, 1025, 5000])
+@pytest.mark.parametrize("fields", [A.DEMUX_CONN_KEY, A.DEMUX_CONN_KEY | A.DEMUX_CMD_BARRIER])
+def test_demux_follower_counts(codec, gpu, oracle, n_follow, fields):
+    """Distinct keys plus exactly `n_follow` repeats of earlier keys (near and far back, across the
+    insert kernel's 1024-packet tiles): the one-block sort of <= 1024 followers, the radix passes
+    above it, and no followers at all."""
+    n = 30000
+    rng = np.random.default_rng(n_follow * 7 + fields)
+    status = np.ones(n, np.int8)
+    cmd = np.zeros(n, np.uint8)
+    ckey = (rng.permutation(n).astype(np.uint64) + 1) * 0x9E3779B1
+    rep = np.sort(rng.choice(np.arange(1, n), n_follow, replace=False))
+    for i in rep:  # a follower of a key seen up to 3000 packets earlier
+        ckey[i] = ckey[max(0, i - 1 - int(rng.integers(0, 3000)))]
+    if fields & A.DEMUX_CMD_BARRIER:  # sparse barriers: epochs of ~2000 packets cross the tiles
+        cmd[rng.choice(n, 15, replace=False)] = 3
+    ids = np.zeros(8 * n, np.uint8)
+    conv = np.zeros(n, np.uint32)
+    dst = np.zeros(n, np.uint32)
+    got = run_gpu(codec, gpu, status, cmd, fields, ids, conv, ckey, dst)
+    exp = oracle.demux_batch(status, cmd, fields, ids, conv, ckey, dst)
+    assert got[1] == exp[1] and len(got[0]) == len(exp[0])
+    assert got[0] == exp[0]
+
+
+@pytest.mark.parametrize("shape", [(50000, 20000, 0.05, 0.95), (50000, 500, 0.05, 0.95), (200000, 50, 0.01, 0.9),
+                                   (100000, 3, 0.3, 1.0)])
+def test_demux_epoch_local(codec, gpu, oracle, shape):
+    """Dense barriers (C4-like 5 % control packets and denser): keys whose epoch lies inside one
+    insert tile never reach the global table; the tiles' first and last epochs do."""
+    n, nkeys, p_ctrl, p_valid = shape
+    rng = np.random.default_rng(n + nkeys)
+    case = make_case(rng, n, nkeys, p_ctrl, p_valid)
+    for fields in (ALL | A.DEMUX_CMD_BARRIER, A.DEMUX_CONN_KEY | A.DEMUX_CMD_BARRIER):
+        got = run_gpu(codec, gpu, *case[:2], fields, *case[2:])
+        exp = oracle.demux_batch(case[0], case[1], fields, *case[2:])
+        assert got[1] == exp[1]
+        assert got[0] == exp[0]
+
+
 def test_demux_empty_and_errors(codec, gpu):
     import torch
 
