@@ -16,17 +16,19 @@
 //                   cidx[j] = packet of compacted slot j, cep[j] = its epoch (CTRL for singletons)
 //   k_dm_insert     open-addressing table: a slot holds a key fingerprint and the compacted index of
 //                   its key's first packet (lowered by CAS), so key confirmation reads the immutable
-//                   input arrays (no lane ever waits on another lane's write)
+//                   input arrays (no lane ever waits on another lane's write); keys whose epoch lies
+//                   inside one tile are grouped in LDS only
 //   k_dm_leader_rank leader of j = the slot's index (or j for a control packet); leader ranks = dense
 //                   segment ids in first-occurrence order by look-back; rank_at, seg_first, n_seg;
 //                   the followers (non-leaders) compacted with their leader
 //   k_dm_segof_hist radix keys = segment id of each follower, global digit histograms of every pass
+//                   (<= 1024 followers: sorted here by one block)
 //   k_dm_onesweep   stable LSD pass of the FOLLOWERS by segment id (8-bit or narrower digits, as many
 //                   passes as the segment count needs; passes beyond that, and tiles past the
 //                   follower count, return at once), per-digit look-back
 //   k_dm_final      leaders merged with the sorted followers: perm, seg_off, n_seg / n_valid
-// (round 3: only followers are sorted — leaders already stand in segment order — so a batch of
-// mostly single-packet segments skips the sort's work)
+// (round 2, second half: only followers are sorted — leaders already stand in segment order — so a
+// batch of mostly single-packet segments skips the sort's work)
 #include <hip/hip_runtime.h>
 
 #include <cstring>
@@ -275,7 +277,7 @@ __device__ __forceinline__ uint32_t global_probe(const DmIn &a, const uint32_t *
 // with LDS atomics; phase 2: that minimum packet alone probes the global table and lowers its index,
 // so a hot key costs one global atomic per block, not one per packet (a single hot word takes
 // ~88 atomics/us: MI355X_MICROARCH.md, dequeue row); phase 3 hands every packet its key's slot.
-// Epoch-local keys (round 3): with CMD_BARRIER the epoch is part of the key and epochs only grow
+// Epoch-local keys (round 2, second half): with CMD_BARRIER the epoch is part of the key and epochs only grow
 // with the packet index, so a key whose epoch lies strictly between the epochs of the tile's first
 // and last data packets cannot occur outside the tile: its block minimum IS its first packet and it
 // never touches the global table (hslot = kLeadTag | leader).  Only the tile's first and last epochs

@@ -1,12 +1,13 @@
 // rsk_kernels.hip — MI355X (gfx950) HIP implementation of the rsock framing codec + its C ABI.
 //
 // Kernels (DESIGN.md §4 has the roofline and the algorithmic bytes of each):
-//   k_encode        RConn::Output framing (conn/RConn.cpp:87-105): per 64-packet set, one lane per
-//                   packet computes status and the 31 header bytes (the tag from the key's 256-entry
-//                   table, staged in LDS); then, per wave, the software-pipelined per-packet copy
-//                   (4-packet batches of 16-B chunks, one aligned payload load per chunk, funnel
-//                   partner from the next lane by DPP) or the flat chunk list for short frames.
-//                   The unpipelined copy and k_copy_probe: A/B build only.
+//   k_encode        RConn::Output framing (conn/RConn.cpp:87-105): per 64-packet set (8 groups of 8
+//                   consecutive packets, interleaved across 1024 waves), one lane per packet computes
+//                   status and the 31 header bytes (the tag from the key's 256-entry table, staged in
+//                   LDS); then, per wave, the software-pipelined per-packet copy (4-packet batches of
+//                   16-B chunks, one aligned payload load per chunk, funnel partner from the next lane
+//                   by DPP) or the flat chunk list for short frames.  The tiled mapping, the
+//                   unpipelined copy and k_copy_probe: A/B build only.
 //   k_encode_wire   RConn::Output + RawTcp::SendRawTcp (conn/RawTcp.cpp:280-341): frames plus the
 //                   IPv4/TCP headers and checksums libnet writes, two-launch hybrid.
 //   k_encode_hdr /  header-only framing / verification on 32-B slots (host-resident deployments:
@@ -681,7 +682,7 @@ constexpr uint32_t kDeferTagMeanBytes = 1024;
 // with the flat sets' tag in phase 1, 10 = 9 with the tag in the copy loop for every per-packet
 // set, 3 = tag always in phase 1, 7 = flat path only, 8 = per-packet path only.  NT < 0: store
 // policy per set.
-template <int MODE, int PU, int U, int NT>
+template <int MODE, int PU, int U, int NT, int GRP = 64>
 __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks, uint64_t i, uint32_t lane,
                                            CopyRec *recs, uint32_t *cend) {
     Lane1 L = encode_phase1<MODE == 3 || MODE == 7>(a, ks, i);
@@ -716,7 +717,8 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
         const uint64_t nfo = (uint64_t)(uint32_t)__shfl_down((int)(uint32_t)L.fo, 1) |
                              ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(L.fo >> 32), 1) << 32);
         const bool nvec = __shfl_down((int)vec, 1) != 0;
-        nt = __ballot(vec && nvec && lane != 63u && end != nfo) != 0ull;
+        // (lanes of the last packet of a group: the next lane's packet is not the next frame)
+        nt = __ballot(vec && nvec && lane % GRP != GRP - 1u && end != nfo) != 0ull;
     }
     // Header chunks: sets with the tag in the copy loop (long frames) store them in the packet's
     // first slot store (lanes 0..2, words by readlane); the others by the slot lane (store_head).
@@ -797,11 +799,13 @@ __global__ __launch_bounds__(kBlock) void k_copy_probe(EncArgs a) {
 }
 #endif
 
-// Tiled mapping: wave t takes packets [64t, 64t + 64) (coalesced descriptor loads; the co-resident
-// waves each stream their own region of the arenas).  SET < 64 (A/B build only): wave t takes
-// [SET t, SET t + SET), lanes SET.. idle in phase 1, so each wave streams a smaller region.
+#ifdef RSK_AB
+// A/B build only: the tiled mapping (round 1 and 2's shipped form): wave t takes packets
+// [64t, 64t + 64) (coalesced descriptor loads; the co-resident waves each stream their own region of
+// the arenas, 64 packets apart).  SET < 64: wave t takes [SET t, SET t + SET), lanes SET.. idle in
+// phase 1, so each wave streams a smaller region.
 template <int MODE, int PU, int U, int NT, int SET = 64>
-__global__ __launch_bounds__(kBlock) void k_encode(EncArgs a, KeySched ks) {
+__global__ __launch_bounds__(kBlock) void k_encode_tiled(EncArgs a, KeySched ks) {
     __shared__ CopyRec recs[kWavesPerBlock][64];
     __shared__ uint32_t cend[kWavesPerBlock][64];
     stage_tags(ks);
@@ -817,7 +821,64 @@ __global__ __launch_bounds__(kBlock) void k_encode(EncArgs a, KeySched ks) {
     }
 }
 
+#endif  // RSK_AB
+
+// Grouped-interleave mapping (shipped: GRP 8, SBW 1024).  A super-block of SBW consecutive waves owns
+// SBW * 64 consecutive packets; wave wl of it takes groups of GRP consecutive packets strided by
+// SBW * GRP (lane l: group (l / GRP) * SBW + wl, packet l % GRP in it).  Each wave still frames 64
+// packets (descriptor loads coalesced per 8-packet group), but the resident waves copy one compact
+// stretch of the arenas at a time (SBW * GRP packets per super-block) instead of each its own region
+// 64 packets from the next wave's: C3 -3.7 %, C4 -4.1 %, C2 within 1 % against the tiled mapping
+// (profiles/r02_ab_encode_mapping.json).  The grid holds only waves that own a packet (enc_grid).
+template <int MODE, int PU, int U, int NT, int GRP, int SBW>
+__global__ __launch_bounds__(kBlock) void k_encode(EncArgs a, KeySched ks) {
+    __shared__ CopyRec recs[kWavesPerBlock][64];
+    __shared__ uint32_t cend[kWavesPerBlock][64];
+    stage_tags(ks);
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint64_t wg = (uint64_t)blockIdx.x * kWavesPerBlock + w;
+    const uint64_t sb = wg / SBW, wl = wg % SBW;
+    const uint64_t first = sb * SBW * 64u + wl * GRP;  // the wave's smallest packet
+    if (first >= a.n) return;  // wave-uniform
+    const uint64_t i = sb * SBW * 64u + ((uint64_t)(lane / GRP) * SBW + wl) * GRP + lane % GRP;
+    encode_set<MODE, PU, U, NT, GRP>(a, ks, i < a.n ? i : a.n, lane, recs[w], cend[w]);
+}
+
 #ifdef RSK_AB
+// A/B build only: the mapping chosen on the device per launch.  Every block reads the same sample
+// (pay_len of the first 256 packets) beside its tag-table stage and takes the same decision: mean
+// payload >= LONGP bytes -> 8 packets per wave (tiled, the grid's every block); otherwise the
+// grouped interleave <8, 1024> over the first grid / 8 blocks, the rest exit.  The grid is sized for
+// the 8-packet mapping.
+template <int MODE, int PU, int U, int NT, uint32_t LONGP>
+__global__ __launch_bounds__(kBlock) void k_encode_ad(EncArgs a, KeySched ks) {
+    __shared__ CopyRec recs[kWavesPerBlock][64];
+    __shared__ uint32_t cend[kWavesPerBlock][64];
+    __shared__ uint32_t wsum[kWavesPerBlock];
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    uint32_t p = threadIdx.x < a.n ? a.pay_len[threadIdx.x] : 0u;
+#pragma unroll
+    for (int off = 32; off; off >>= 1) p += __shfl_xor(p, off);
+    if (lane == 0u) wsum[w] = p;
+    stage_tags(ks);  // its barrier publishes wsum too
+    const uint32_t cnt = a.n < (uint32_t)kBlock ? a.n : (uint32_t)kBlock;
+    const bool lng = wsum[0] + wsum[1] + wsum[2] + wsum[3] >= LONGP * cnt;
+    const uint64_t wg = (uint64_t)blockIdx.x * kWavesPerBlock + w;
+    if (lng) {
+        const uint64_t base = wg * 8u;
+        if (base >= a.n) return;
+        EncArgs b = a;
+        b.n = (uint32_t)(base + 8u < a.n ? base + 8u : a.n);
+        encode_set<MODE, PU, U, NT>(b, ks, lane < 8u ? base + lane : b.n, lane, recs[w], cend[w]);
+        return;
+    }
+    const uint64_t sb = wg / 1024u, wl = wg % 1024u;
+    const uint64_t first = sb * 1024u * 64u + wl * 8u;
+    if (first >= a.n) return;
+    const uint64_t i = sb * 1024u * 64u + ((uint64_t)(lane / 8u) * 1024u + wl) * 8u + lane % 8u;
+    encode_set<MODE, PU, U, NT, 8>(a, ks, i < a.n ? i : a.n, lane, recs[w], cend[w]);
+}
+
 // A/B build only: persistent form of the SET mapping — the grid holds only resident blocks and each
 // wave strides over SET-packet sets (set w, w + W, ...), so the tag table is staged once per block
 // and the resident waves still sweep the arenas as one compact window.
@@ -2286,6 +2347,16 @@ DecOut make_dec_out(const rsk_decode_out *o, uint64_t *masks) {
 // =============================================================================================
 // C ABI
 // =============================================================================================
+namespace {
+// Blocks of k_encode<.., GRP, SBW>: every wave that owns at least one packet (the last super-block
+// may be partial: its wave wl owns packets iff wl * GRP < the packets left).
+unsigned enc_grid(uint64_t n, uint32_t grp, uint32_t sbw) {
+    const uint64_t per_sb = (uint64_t)sbw * 64u, rest = n % per_sb;
+    const uint64_t waves = n / per_sb * sbw + std::min<uint64_t>(sbw, (rest + grp - 1) / grp);
+    return (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
+}
+}  // namespace
+
 extern "C" {
 
 const char *rsk_last_error(void) { return g_last_error; }
@@ -2294,8 +2365,9 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 
 #ifdef RSK_AB
 // A/B build only: selects the encode kernel variant for in-process A/B runs (tools/ab_encode.py).
-// k_encode<MODE, PU, U, NT> (see encode_set): 0 = the shipped <11, 4, 4, -1> (software-pipelined
-// per-packet copy, 4 packets per batch; flat sets' tag behind the first chunk loads); 22 = the same
+// 0 = the shipped k_encode<11, 4, 4, -1, 8, 1024> (grouped interleave; software-pipelined per-packet
+// copy, 4 packets per batch; flat sets' tag behind the first chunk loads).  The others are the tiled
+// mapping k_encode_tiled<MODE, PU, U, NT> (see encode_set) unless named: 37 = the tiled form of 0, 22 = the same
 // with the flat sets' tag in phase 1 (<9, 4, 4, -1>); 17 = round 2's first form <6, 12, 4, -1> (12 packets per
 // iteration, no pipelining); 1 = as 17 with the tag always in phase 1; 2 / 3 = 17 with 8 / 16
 // packets per iteration; 4 = 2 chunks per lane per flat iteration; 5 / 6 = normal / nontemporal
@@ -2305,10 +2377,13 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 // 18 = shipped with the tag in the copy loop for every per-packet set; 19 / 20 / 21 = shipped with
 // the flat sets' tag behind the first chunk loads, 4 / 2 / 8 chunk rows per flat iteration;
 // 23 / 24 / 25 / 26 = shipped with 32 / 16 / 8 / 4 packets per wave (smaller region per wave);
-// 27 / 28 / 29 / 30 = persistent k_encode_gs: SET 16 on 1024 blocks / 8 on 1024 / 16 on 2048 / 32 on 1024.
+// 27 / 28 / 29 / 30 = persistent k_encode_gs: SET 16 on 1024 blocks / 8 on 1024 / 16 on 2048 / 32 on 1024;
+// 31 / 32 / 33 / 34 = grouped interleave k_encode_gi <GRP, SBW> = <8, 1024> / <8, 4096> / <16, 1024> / <4, 1024>;
+// 35 / 36 = k_encode_ad (mapping chosen on the device from a pay_len sample), long at >= 1024 / 512 B;
+// 37 = the tiled mapping with the shipped copy (the form shipped before the grouped interleave).
 // v + 100 * cap (cap 1..4): the same kernel held to `cap` blocks per CU by unused LDS.
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
-    if (!c || v < 0 || v % 100 > 30 || v / 100 > 4) return RSK_EINVAL;
+    if (!c || v < 0 || v % 100 > 37 || v / 100 > 4) return RSK_EINVAL;
     c->enc_variant = v;
     return RSK_OK;
 }
@@ -2410,43 +2485,51 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
     const int cap = c->enc_variant / 100;
     const size_t lds = cap ? (size_t)(163840 / cap) - 16384 : 0;
     switch (c->enc_variant % 100) {
-        case 1: hipLaunchKernelGGL((k_encode<3, 12, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 2: hipLaunchKernelGGL((k_encode<6, 8, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 3: hipLaunchKernelGGL((k_encode<6, 16, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 4: hipLaunchKernelGGL((k_encode<6, 12, 2, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 5: hipLaunchKernelGGL((k_encode<6, 12, 4, 0>), gd, bd, lds, st, a, c->ks); break;
-        case 6: hipLaunchKernelGGL((k_encode<6, 12, 4, 2>), gd, bd, lds, st, a, c->ks); break;
-        case 7: hipLaunchKernelGGL((k_encode<7, 12, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 8: hipLaunchKernelGGL((k_encode<8, 12, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 9: hipLaunchKernelGGL((k_encode<9, 6, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 10: hipLaunchKernelGGL((k_encode<9, 8, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 11: hipLaunchKernelGGL((k_encode<9, 4, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 1: hipLaunchKernelGGL((k_encode_tiled<3, 12, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 2: hipLaunchKernelGGL((k_encode_tiled<6, 8, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 3: hipLaunchKernelGGL((k_encode_tiled<6, 16, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 4: hipLaunchKernelGGL((k_encode_tiled<6, 12, 2, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 5: hipLaunchKernelGGL((k_encode_tiled<6, 12, 4, 0>), gd, bd, lds, st, a, c->ks); break;
+        case 6: hipLaunchKernelGGL((k_encode_tiled<6, 12, 4, 2>), gd, bd, lds, st, a, c->ks); break;
+        case 7: hipLaunchKernelGGL((k_encode_tiled<7, 12, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 8: hipLaunchKernelGGL((k_encode_tiled<8, 12, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 9: hipLaunchKernelGGL((k_encode_tiled<9, 6, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 10: hipLaunchKernelGGL((k_encode_tiled<9, 8, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 11: hipLaunchKernelGGL((k_encode_tiled<9, 4, 4, -1>), gd, bd, lds, st, a, c->ks); break;
         case 12: hipLaunchKernelGGL((k_copy_probe<12>), gd, bd, lds, st, a); break;
         case 13: hipLaunchKernelGGL((k_copy_probe<4>), gd, bd, lds, st, a); break;
-        case 14: hipLaunchKernelGGL((k_encode<9, 3, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 15: hipLaunchKernelGGL((k_encode<9, 5, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 16: hipLaunchKernelGGL((k_encode<9, 2, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 17: hipLaunchKernelGGL((k_encode<6, 12, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 18: hipLaunchKernelGGL((k_encode<10, 4, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 19: hipLaunchKernelGGL((k_encode<11, 4, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 20: hipLaunchKernelGGL((k_encode<11, 4, 2, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 21: hipLaunchKernelGGL((k_encode<11, 4, 8, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 22: hipLaunchKernelGGL((k_encode<9, 4, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 23: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 32>), dim3(grid * 2), bd, lds, st, a, c->ks); break;
-        case 24: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 16>), dim3(grid * 4), bd, lds, st, a, c->ks); break;
-        case 25: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8>), dim3(grid * 8), bd, lds, st, a, c->ks); break;
-        case 26: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 4>), dim3(grid * 16), bd, lds, st, a, c->ks); break;
+        case 14: hipLaunchKernelGGL((k_encode_tiled<9, 3, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 15: hipLaunchKernelGGL((k_encode_tiled<9, 5, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 16: hipLaunchKernelGGL((k_encode_tiled<9, 2, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 17: hipLaunchKernelGGL((k_encode_tiled<6, 12, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 18: hipLaunchKernelGGL((k_encode_tiled<10, 4, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 19: hipLaunchKernelGGL((k_encode_tiled<11, 4, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 20: hipLaunchKernelGGL((k_encode_tiled<11, 4, 2, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 21: hipLaunchKernelGGL((k_encode_tiled<11, 4, 8, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 22: hipLaunchKernelGGL((k_encode_tiled<9, 4, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 23: hipLaunchKernelGGL((k_encode_tiled<11, 4, 4, -1, 32>), dim3(grid * 2), bd, lds, st, a, c->ks); break;
+        case 24: hipLaunchKernelGGL((k_encode_tiled<11, 4, 4, -1, 16>), dim3(grid * 4), bd, lds, st, a, c->ks); break;
+        case 25: hipLaunchKernelGGL((k_encode_tiled<11, 4, 4, -1, 8>), dim3(grid * 8), bd, lds, st, a, c->ks); break;
+        case 26: hipLaunchKernelGGL((k_encode_tiled<11, 4, 4, -1, 4>), dim3(grid * 16), bd, lds, st, a, c->ks); break;
         case 27: hipLaunchKernelGGL((k_encode_gs<11, 4, 4, -1, 16>), dim3(std::min(grid * 4u, 1024u)), bd, lds, st, a, c->ks); break;
         case 28: hipLaunchKernelGGL((k_encode_gs<11, 4, 4, -1, 8>), dim3(std::min(grid * 8u, 1024u)), bd, lds, st, a, c->ks); break;
         case 29: hipLaunchKernelGGL((k_encode_gs<11, 4, 4, -1, 16>), dim3(std::min(grid * 4u, 2048u)), bd, lds, st, a, c->ks); break;
         case 30: hipLaunchKernelGGL((k_encode_gs<11, 4, 4, -1, 32>), dim3(std::min(grid * 2u, 1024u)), bd, lds, st, a, c->ks); break;
-        default: hipLaunchKernelGGL((k_encode<11, 4, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 31: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
+        case 32: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 4096>), dim3(enc_grid(n, 8, 4096)), bd, lds, st, a, c->ks); break;
+        case 33: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 16, 1024>), dim3(enc_grid(n, 16, 1024)), bd, lds, st, a, c->ks); break;
+        case 34: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 4, 1024>), dim3(enc_grid(n, 4, 1024)), bd, lds, st, a, c->ks); break;
+        case 35: hipLaunchKernelGGL((k_encode_ad<11, 4, 4, -1, 1024>), dim3(std::max(grid * 8u, (grid + 255u) / 256u * 256u)), bd, lds, st, a, c->ks); break;
+        case 36: hipLaunchKernelGGL((k_encode_ad<11, 4, 4, -1, 512>), dim3(std::max(grid * 8u, (grid + 255u) / 256u * 256u)), bd, lds, st, a, c->ks); break;
+        case 37: hipLaunchKernelGGL((k_encode_tiled<11, 4, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        default: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
     }
 #else
     // the shipped kernel: per-wave hybrid (flat chunk list for short frames, with the tag behind the
     // first chunk loads; software-pipelined one-load DPP per-packet copy, 4 packets per batch, for
     // the rest), tag in the copy loop for long-frame sets, per-set store policy
-    hipLaunchKernelGGL((k_encode<11, 4, 4, -1>), gd, bd, 0, st, a, c->ks);
+    (void)gd;
+    hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, 0, st, a, c->ks);
 #endif
     return launch_check("k_encode");
 }
