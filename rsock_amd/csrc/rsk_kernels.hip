@@ -1396,14 +1396,20 @@ __device__ __forceinline__ bool wire_flat_choice(bool vec, uint32_t wlen) {
     return fl < kFlatBelowMeanBytes * (uint32_t)__popcll(__ballot(vec));
 }
 
-template <int E, int MODE, int PU, int U>
+// GI: k_encode's grouped-interleave mapping (8-packet groups across 1024-wave super-blocks, grid by
+// enc_grid); otherwise the tiled mapping (A/B build: wire variant 10).
+template <int E, int MODE, int PU, int U, bool GI>
 __device__ __forceinline__ void encode_wire_set(const EncArgs &a, const WireArgs &wa, const KeySched &ks) {
     using G = WireGeom<E>;
     __shared__ uint4 lds[kWavesPerBlock][WireLds<E, MODE>::kBytes / 16];
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    const uint64_t base = ((uint64_t)blockIdx.x * kWavesPerBlock + w) * 64u;
-    if (base >= a.n) return;  // wave-uniform; no block barriers below
-    const uint64_t i = base + lane;
+    const uint64_t wg = (uint64_t)blockIdx.x * kWavesPerBlock + w;
+    constexpr uint32_t kGrp = GI ? 8u : 64u;
+    const uint64_t sb = wg / 1024u, wl = wg % 1024u;
+    const uint64_t first = GI ? sb * 65536u + wl * 8u : wg * 64u;
+    if (first >= a.n) return;  // wave-uniform; no block barriers below
+    const uint64_t gi = GI ? sb * 65536u + ((uint64_t)(lane / 8u) * 1024u + wl) * 8u + lane % 8u : first + lane;
+    const uint64_t i = gi < a.n ? gi : a.n;
     if constexpr (MODE >= 3) {  // split hybrid: is this set ours?
         bool v0 = false;
         uint32_t wl = 0;
@@ -1457,7 +1463,7 @@ __device__ __forceinline__ void encode_wire_set(const EncArgs &a, const WireArgs
             const uint64_t nfo = (uint64_t)(uint32_t)__shfl_down((int)(uint32_t)L.fo, 1) |
                                  ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(L.fo >> 32), 1) << 32);
             const bool nvec = __shfl_down((int)vec, 1) != 0;
-            const bool gaps = __ballot(vec && nvec && lane != 63u && end != nfo) != 0ull;
+            const bool gaps = __ballot(vec && nvec && lane % kGrp != kGrp - 1u && end != nfo) != 0ull;
             if (MODE == 5 && defer) {
                 if (gaps) copy_wire_pkt_dpp<E, PU - 100, 2, true>(a, ks, L, stage, sum_pre, wst, lane, vm);
                 else copy_wire_pkt_dpp<E, PU - 100, 0, true>(a, ks, L, stage, sum_pre, wst, lane, vm);
@@ -1475,19 +1481,19 @@ __device__ __forceinline__ void encode_wire_set(const EncArgs &a, const WireArgs
     }
 }
 
-template <int E, int MODE, int PU, int U>
+template <int E, int MODE, int PU, int U, bool GI = true>
 __global__ __launch_bounds__(kBlock) void k_encode_wire(EncArgs a, WireArgs wa, KeySched ks) {
     stage_tags(ks);
-    encode_wire_set<E, MODE, PU, U>(a, wa, ks);
+    encode_wire_set<E, MODE, PU, U, GI>(a, wa, ks);
 }
 
 // The same held to 4 waves per SIMD (<= 128 VGPRs): the deferred-tag build (MODE 5) needs 131 and
 // would otherwise drop to 3, which costs the sets that keep the tag in phase 1 (C4 +9 %).
-template <int E, int MODE, int PU, int U>
+template <int E, int MODE, int PU, int U, bool GI = true>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_encode_wire_w4(
     EncArgs a, WireArgs wa, KeySched ks) {
     stage_tags(ks);
-    encode_wire_set<E, MODE, PU, U>(a, wa, ks);
+    encode_wire_set<E, MODE, PU, U, GI>(a, wa, ks);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2392,9 +2398,10 @@ int rsk__set_encode_variant(rsk_ctx *c, int v) {
 // one-load DPP copy, 8 packets per iteration, tag + payload prefix in the copy loop for sets of long
 // frames (default), 1 = per-packet, 2 = flat, 3 = one-launch hybrid, 4 = two-launch hybrid with the
 // two-load copy PU=2, 5 = the same PU=4, 6 / 7 = DPP copy PU=4 / 16, 8 = 0 with the tag in phase 1,
-// 9 = 0 without the 4-waves-per-SIMD bound.
+// 9 = 0 without the 4-waves-per-SIMD bound, 10 = 0 on the tiled mapping (64 consecutive packets per
+// wave; variants 1-9 use the grouped interleave like 0).
 int rsk__set_wire_variant(rsk_ctx *c, int v) {
-    if (!c || v < 0 || v > 9) return RSK_EINVAL;
+    if (!c || v < 0 || v > 10) return RSK_EINVAL;
     c->wire_variant = v;
     return RSK_OK;
 }
@@ -2559,12 +2566,14 @@ int rsk_encode_wire_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const
     uint8_t eth[16] = {0};
     std::memcpy(eth, wire->eth, 14);
     std::memcpy(w.eth, eth, 16);
-    const uint64_t waves = (n + 63ull) / 64ull;
-    const unsigned grid = (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
+    const unsigned grid = enc_grid(n, 8, 1024);
     const hipStream_t st = (hipStream_t)stream;
 #define RSK_WIRE(E, M, PU, U) hipLaunchKernelGGL((k_encode_wire<E, M, PU, U>), dim3(grid), dim3(kBlock), 0, st, a, w, c->ks)
 #define RSK_WIRE4(E, M, PU, U) hipLaunchKernelGGL((k_encode_wire_w4<E, M, PU, U>), dim3(grid), dim3(kBlock), 0, st, a, w, c->ks)
 #ifdef RSK_AB
+    const unsigned tgrid = (unsigned)(((n + 63ull) / 64ull + kWavesPerBlock - 1) / kWavesPerBlock);
+#define RSK_WIRET(E, M, PU, U) hipLaunchKernelGGL((k_encode_wire<E, M, PU, U, false>), dim3(tgrid), dim3(kBlock), 0, st, a, w, c->ks)
+#define RSK_WIRE4T(E, M, PU, U) hipLaunchKernelGGL((k_encode_wire_w4<E, M, PU, U, false>), dim3(tgrid), dim3(kBlock), 0, st, a, w, c->ks)
     const int v = c->wire_variant;
     if (wire->with_eth) {
         if (v == 1) RSK_WIRE(14, 0, 2, 4);
@@ -2576,6 +2585,7 @@ int rsk_encode_wire_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const
         else if (v == 7) { RSK_WIRE(14, 3, 116, 2); RSK_WIRE(14, 4, 2, 2); }
         else if (v == 8) { RSK_WIRE(14, 3, 108, 2); RSK_WIRE(14, 4, 2, 2); }
         else if (v == 9) { RSK_WIRE(14, 5, 108, 2); RSK_WIRE(14, 4, 2, 2); }
+        else if (v == 10) { RSK_WIRE4T(14, 5, 108, 2); RSK_WIRET(14, 4, 2, 2); }
         else { RSK_WIRE4(14, 5, 108, 2); RSK_WIRE(14, 4, 2, 2); }
     } else {
         if (v == 1) RSK_WIRE(0, 0, 2, 4);
@@ -2587,6 +2597,7 @@ int rsk_encode_wire_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const
         else if (v == 7) { RSK_WIRE(0, 3, 116, 2); RSK_WIRE(0, 4, 2, 2); }
         else if (v == 8) { RSK_WIRE(0, 3, 108, 2); RSK_WIRE(0, 4, 2, 2); }
         else if (v == 9) { RSK_WIRE(0, 5, 108, 2); RSK_WIRE(0, 4, 2, 2); }
+        else if (v == 10) { RSK_WIRE4T(0, 5, 108, 2); RSK_WIRET(0, 4, 2, 2); }
         else { RSK_WIRE4(0, 5, 108, 2); RSK_WIRE(0, 4, 2, 2); }
     }
 #else
@@ -2597,6 +2608,10 @@ int rsk_encode_wire_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const
 #endif
 #undef RSK_WIRE
 #undef RSK_WIRE4
+#ifdef RSK_AB
+#undef RSK_WIRET
+#undef RSK_WIRE4T
+#endif
     return launch_check("k_encode_wire");
 }
 
