@@ -205,11 +205,26 @@ __device__ uint32_t dlb_digit(unsigned long long *st, uint32_t t, uint32_t d, ui
         return 0u;
     }
     dlb_publish(st + (uint64_t)t * 256u + d, (unsigned long long)cnt);
+    // walk back kLb tiles per step: their words are requested together (one round trip per step,
+    // not per tile); a tile before tile 0 reads as an inclusive 0
+    constexpr int kLb = 4;
     uint32_t excl = 0;
-    for (int64_t j = (int64_t)t - 1; j >= 0; --j) {
-        const unsigned long long v = dlb_wait(st + (uint64_t)j * 256u + d);
-        excl += (uint32_t)v;
-        if (v & kDlbIncl) break;
+    for (int64_t j = (int64_t)t - 1; j >= 0; j -= kLb) {
+        unsigned long long v[kLb];
+#pragma unroll
+        for (int q = 0; q < kLb; ++q)
+            v[q] = j - q >= 0 ? __hip_atomic_load(st + (uint64_t)(j - q) * 256u + d, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT)
+                              : kDlbIncl;
+        bool done = false;
+#pragma unroll
+        for (int q = 0; q < kLb; ++q) {
+            if (done) break;
+            if (v[q] == kDlbEmpty) v[q] = dlb_wait(st + (uint64_t)(j - q) * 256u + d);
+            excl += (uint32_t)v[q];
+            done = (v[q] & kDlbIncl) != 0ull;
+        }
+        if (done) break;
     }
     dlb_publish(st + (uint64_t)t * 256u + d, kDlbIncl | (unsigned long long)(excl + cnt));
     return excl;

@@ -1229,6 +1229,153 @@ __device__ __forceinline__ void copy_wire_pkt_dpp(const EncArgs &a, const KeySch
     }
 }
 
+// ---- software-pipelined form of copy_wire_pkt_dpp (as copy_pkt_pipe for k_encode): the loads of
+// the next PU packets (TAG: the payload prefix of lane p's packet, two aligned 16-B chunks, then the
+// payload chunks) are issued before the current PU packets are summed and stored.  Every load runs
+// with all lanes (dead lanes re-read a mapped chunk), so a batch's load count is static and the wait
+// for the older batch leaves the newer one in flight.  Payload chunks are stored as soon as they are
+// summed; only the prefix chunks wait for the packet's checksum.
+template <int E, int PU, bool TAG>
+__device__ __forceinline__ void wire_issue(const EncArgs &a, const Lane1 &L, int32_t wst, uint32_t lane,
+                                           uint64_t bm, uint4 (&A)[PU][2], uint4 (&pc)[2]) {
+    using G = WireGeom<E>;
+    uint32_t js[PU], myj;
+    bool on[PU], mine;
+    batch_slots<PU>(bm, lane, js, on, myj, mine);
+    if constexpr (TAG) {  // lane p: the first 16 payload bytes of packet p
+        const uint64_t po = shfl64(L.po, myj);
+        const uint32_t wl = (uint32_t)__shfl((int)wst, (int)myj);  // with every lane active (bpermute)
+        const uint32_t P = mine ? wl - G::HB : 0u;
+        const uint8_t *pay = a.payload + (mine ? po : 0u);
+        const uint8_t *al = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(pay) & ~(uintptr_t)15);
+        const uint32_t r = (uint32_t)(reinterpret_cast<uintptr_t>(pay) & 15u);
+        pc[0] = ld16<0>(al);
+        pc[1] = ld16<0>(16u - r < P ? al + 16 : al);
+    }
+#pragma unroll
+    for (int p = 0; p < PU; ++p) {
+        const uint32_t wlen = on[p] ? (uint32_t)rdl((uint32_t)wst, js[p]) : 0u;
+        const uint32_t P = wlen - G::HB;
+        const uint8_t *pay = a.payload + rdl64(L.po, js[p]);
+        const uint32_t shp = (uint32_t)((reinterpret_cast<uintptr_t>(pay) + G::D0) & 15u);
+        const uint8_t *src_al = pay + G::D0 - shp;
+        const int32_t last_rel = (int32_t)P - 1 - G::D0 + (int32_t)shp;
+        const uint8_t *dummy = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(pay) & ~(uintptr_t)15);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const uint32_t m = lane + 64u * q;  // source chunk of frame chunk NPRE + m
+            const bool live = on[p] && (int32_t)(16u * m) <= last_rel;
+            const uint4 v = ld16<0>(live ? src_al + 16u * m : dummy);
+            A[p][q] = live ? v : make_uint4(0u, 0u, 0u, 0u);
+        }
+    }
+}
+
+template <int E, int PU, int NT, bool TAG>
+__device__ __forceinline__ void wire_store(const EncArgs &a, const KeySched &ks, const Lane1 &L, uint32_t *stage,
+                                           uint32_t sum_pre, int32_t wst, uint32_t lane, uint64_t bm,
+                                           const uint4 (&A)[PU][2], const uint4 (&pc)[2]) {
+    using G = WireGeom<E>;
+    uint32_t js[PU], myj;
+    bool on[PU], mine;
+    batch_slots<PU>(bm, lane, js, on, myj, mine);
+    uint32_t dsum = 0;  // TAG: lane p, checksum share of the bytes it adds to packet p's prefix image
+    if constexpr (TAG) {
+        const uint64_t po = shfl64(L.po, myj);
+        const uint32_t wl = (uint32_t)__shfl((int)wst, (int)myj);  // with every lane active (bpermute)
+        const uint32_t P = mine ? wl - G::HB : 0u;
+        const uint32_t r = (uint32_t)((reinterpret_cast<uintptr_t>(a.payload) + po) & 15u);
+        const uint4 f = rsk::funnel16(pc[0], pc[1], r);
+        uint32_t pw[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int k = (int)P - 4 * q;
+            pw[q] &= k >= 4 ? 0xffffffffu : (k <= 0 ? 0u : ((1u << (8 * k)) - 1u));
+        }
+        uint32_t t0, t1;
+        tag_of(ks, pw[0] & 0xffu, t0, t1);
+        uint32_t D[G::NPW];
+#pragma unroll
+        for (int q = 0; q < G::NPW; ++q) D[q] = 0;
+        put_bytes(D, G::HL, t0, 4);
+        put_bytes(D, G::HL + 4, t1, 4);
+        wire_put_prefix<E>(D, pw);  // payload bytes from wire offset HB (frame byte 31 = payload[0])
+        if (mine && P) {
+#pragma unroll
+            for (int q = G::HL / 4; q < G::NPW; ++q) {
+                stage[myj * G::NPW + q] |= D[q];
+                dsum += hsum(D[q]);
+            }
+        }
+        wave_lds_sync();
+    }
+    uint32_t ck[PU];
+#pragma unroll
+    for (int p = 0; p < PU; ++p) {
+        const uint32_t wlen = on[p] ? (uint32_t)rdl((uint32_t)wst, js[p]) : 0u;
+        uint8_t *dst = a.frame + rdl64(L.fo, js[p]);
+        const uint32_t shp = (uint32_t)((reinterpret_cast<uintptr_t>(a.payload + rdl64(L.po, js[p])) + G::D0) & 15u);
+        uint4 B[2];
+        B[0] = make_uint4(wave_shl1(A[p][0].x), wave_shl1(A[p][0].y), wave_shl1(A[p][0].z), wave_shl1(A[p][0].w));
+        B[1] = make_uint4(wave_shl1(A[p][1].x), wave_shl1(A[p][1].y), wave_shl1(A[p][1].z), wave_shl1(A[p][1].w));
+        const uint4 l0 = make_uint4(rdl(A[p][1].x, 0), rdl(A[p][1].y, 0), rdl(A[p][1].z, 0),
+                                    rdl(A[p][1].w, 0));  // read in uniform flow (see k_encode)
+        if (lane == 63u) B[0] = l0;
+        const uint32_t nch = (wlen + 15u) >> 4;
+        const uint32_t nst = on[p] ? (padded_len(dst, wlen, a.pad) + 15u) >> 4 : 0u;
+        uint32_t part = 0;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const uint32_t k = G::NPRE + lane + 64u * q;
+            uint4 v = rsk::funnel16(A[p][q], B[q], shp);
+            const int lim = (int)wlen - 16 * (int)k;
+            if (k < nch) {
+                if (lim < 16) v = rsk::keep_bytes16(v, lim);
+                part = hsum4(v, part);
+            }
+            if (k < nst) store_last16<NT>(dst + 16u * k, v, lim, a.pad != 0u);
+        }
+        ck[p] = part;
+    }
+#pragma unroll
+    for (int p = 0; p < PU; ++p)
+        ck[p] = ~fold16(wave_sum(ck[p]) + rdl(sum_pre, js[p]) + (TAG ? rdl(dsum, (uint32_t)p) : 0u)) & 0xffffu;
+#pragma unroll
+    for (int p = 0; p < PU; ++p) {
+        if (!on[p]) continue;
+        const uint32_t wlen = (uint32_t)rdl((uint32_t)wst, js[p]);
+        uint8_t *dst = a.frame + rdl64(L.fo, js[p]);
+        const uint32_t nst = (padded_len(dst, wlen, a.pad) + 15u) >> 4;
+        if (lane < (uint32_t)G::NPRE && lane < nst) {
+            const uint4 sv = *reinterpret_cast<const uint4 *>(stage + js[p] * G::NPW + 4u * lane);
+            uint32_t w4[4] = {sv.x, sv.y, sv.z, sv.w};
+            if (lane == (uint32_t)(G::CK / 16)) w4[(G::CK & 15) >> 2] |= ck[p] << (8 * (G::CK & 3));
+            store_last16<NT>(dst + 16u * lane, make_uint4(w4[0], w4[1], w4[2], w4[3]), (int)wlen - 16 * (int)lane,
+                             a.pad != 0u);
+        }
+    }
+}
+
+template <int E, int PU, int NT, bool TAG>
+__device__ __forceinline__ void copy_wire_pkt_pipe(const EncArgs &a, const KeySched &ks, const Lane1 &L,
+                                                   uint32_t *stage, uint32_t sum_pre, int32_t wst, uint32_t lane,
+                                                   uint64_t vm) {
+    uint4 A0[PU][2], A1[PU][2], p0[2], p1[2];
+    uint64_t cur = take_batch<PU>(vm);
+    if (!cur) return;
+    wire_issue<E, PU, TAG>(a, L, wst, lane, cur, A0, p0);
+    while (true) {
+        const uint64_t nxt = take_batch<PU>(vm);
+        if (nxt) wire_issue<E, PU, TAG>(a, L, wst, lane, nxt, A1, p1);
+        wire_store<E, PU, NT, TAG>(a, ks, L, stage, sum_pre, wst, lane, cur, A0, p0);
+        if (!nxt) break;
+        cur = take_batch<PU>(vm);
+        if (cur) wire_issue<E, PU, TAG>(a, L, wst, lane, cur, A0, p0);
+        wire_store<E, PU, NT, TAG>(a, ks, L, stage, sum_pre, wst, lane, nxt, A1, p1);
+        if (!cur) break;
+    }
+}
+
 // ---- flat copy for short packets, two passes over the set: (1) the payload chunks of all packets as
 // one flat chunk list (as copy_flat), each lane adding its chunk's halfword sum into the packet's
 // LDS slot; (2) the NPRE prefix chunks of every packet as a dense (packet, chunk) grid read from the
@@ -1456,7 +1603,21 @@ __device__ __forceinline__ void encode_wire_set(const EncArgs &a, const WireArgs
     }
     if (!flat) {
         wave_lds_sync();
-        if constexpr (PU >= 100) {
+        if constexpr (PU >= 200) {  // software-pipelined DPP copy, PU - 200 packets per batch
+            const uint32_t wend = vec ? padded_len(a.frame + L.fo, (uint32_t)wst, a.pad) : 0u;
+            const uint64_t end = L.fo + wend;
+            const uint64_t nfo = (uint64_t)(uint32_t)__shfl_down((int)(uint32_t)L.fo, 1) |
+                                 ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(L.fo >> 32), 1) << 32);
+            const bool nvec = __shfl_down((int)vec, 1) != 0;
+            const bool gaps = __ballot(vec && nvec && lane % kGrp != kGrp - 1u && end != nfo) != 0ull;
+            if (MODE == 5 && defer) {
+                if (gaps) copy_wire_pkt_pipe<E, PU - 200, 2, true>(a, ks, L, stage, sum_pre, wst, lane, vm);
+                else copy_wire_pkt_pipe<E, PU - 200, 0, true>(a, ks, L, stage, sum_pre, wst, lane, vm);
+            } else {
+                if (gaps) copy_wire_pkt_pipe<E, PU - 200, 2, false>(a, ks, L, stage, sum_pre, wst, lane, vm);
+                else copy_wire_pkt_pipe<E, PU - 200, 0, false>(a, ks, L, stage, sum_pre, wst, lane, vm);
+            }
+        } else if constexpr (PU >= 100) {
             // store policy per set, as k_encode: stream the stores when the wire packets leave gaps
             const uint32_t wend = vec ? padded_len(a.frame + L.fo, (uint32_t)wst, a.pad) : 0u;
             const uint64_t end = L.fo + wend;
@@ -2386,10 +2547,11 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 // 27 / 28 / 29 / 30 = persistent k_encode_gs: SET 16 on 1024 blocks / 8 on 1024 / 16 on 2048 / 32 on 1024;
 // 31 / 32 / 33 / 34 = grouped interleave k_encode_gi <GRP, SBW> = <8, 1024> / <8, 4096> / <16, 1024> / <4, 1024>;
 // 35 / 36 = k_encode_ad (mapping chosen on the device from a pay_len sample), long at >= 1024 / 512 B;
-// 37 = the tiled mapping with the shipped copy (the form shipped before the grouped interleave).
+// 37 = the tiled mapping with the shipped copy (the form shipped before the grouped interleave);
+// 38 / 39 / 40 / 41 / 42 = grouped interleave <GRP, SBW> = <8,256> / <8,512> / <8,2048> / <16,512> / <32,256>.
 // v + 100 * cap (cap 1..4): the same kernel held to `cap` blocks per CU by unused LDS.
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
-    if (!c || v < 0 || v % 100 > 37 || v / 100 > 4) return RSK_EINVAL;
+    if (!c || v < 0 || v % 100 > 42 || v / 100 > 4) return RSK_EINVAL;
     c->enc_variant = v;
     return RSK_OK;
 }
@@ -2399,9 +2561,10 @@ int rsk__set_encode_variant(rsk_ctx *c, int v) {
 // frames (default), 1 = per-packet, 2 = flat, 3 = one-launch hybrid, 4 = two-launch hybrid with the
 // two-load copy PU=2, 5 = the same PU=4, 6 / 7 = DPP copy PU=4 / 16, 8 = 0 with the tag in phase 1,
 // 9 = 0 without the 4-waves-per-SIMD bound, 10 = 0 on the tiled mapping (64 consecutive packets per
-// wave; variants 1-9 use the grouped interleave like 0).
+// wave; variants 1-9 use the grouped interleave like 0), 11 / 12 = 0 with the software-pipelined copy,
+// 4 / 3 packets per batch, 13 = 11 without the 4-waves-per-SIMD bound.
 int rsk__set_wire_variant(rsk_ctx *c, int v) {
-    if (!c || v < 0 || v > 10) return RSK_EINVAL;
+    if (!c || v < 0 || v > 13) return RSK_EINVAL;
     c->wire_variant = v;
     return RSK_OK;
 }
@@ -2529,6 +2692,11 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         case 35: hipLaunchKernelGGL((k_encode_ad<11, 4, 4, -1, 1024>), dim3(std::max(grid * 8u, (grid + 255u) / 256u * 256u)), bd, lds, st, a, c->ks); break;
         case 36: hipLaunchKernelGGL((k_encode_ad<11, 4, 4, -1, 512>), dim3(std::max(grid * 8u, (grid + 255u) / 256u * 256u)), bd, lds, st, a, c->ks); break;
         case 37: hipLaunchKernelGGL((k_encode_tiled<11, 4, 4, -1>), gd, bd, lds, st, a, c->ks); break;
+        case 38: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 256>), dim3(enc_grid(n, 8, 256)), bd, lds, st, a, c->ks); break;
+        case 39: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 512>), dim3(enc_grid(n, 8, 512)), bd, lds, st, a, c->ks); break;
+        case 40: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 2048>), dim3(enc_grid(n, 8, 2048)), bd, lds, st, a, c->ks); break;
+        case 41: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 16, 512>), dim3(enc_grid(n, 16, 512)), bd, lds, st, a, c->ks); break;
+        case 42: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 32, 256>), dim3(enc_grid(n, 32, 256)), bd, lds, st, a, c->ks); break;
         default: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
     }
 #else
@@ -2586,6 +2754,9 @@ int rsk_encode_wire_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const
         else if (v == 8) { RSK_WIRE(14, 3, 108, 2); RSK_WIRE(14, 4, 2, 2); }
         else if (v == 9) { RSK_WIRE(14, 5, 108, 2); RSK_WIRE(14, 4, 2, 2); }
         else if (v == 10) { RSK_WIRE4T(14, 5, 108, 2); RSK_WIRET(14, 4, 2, 2); }
+        else if (v == 11) { RSK_WIRE4(14, 5, 204, 2); RSK_WIRE(14, 4, 2, 2); }
+        else if (v == 12) { RSK_WIRE4(14, 5, 203, 2); RSK_WIRE(14, 4, 2, 2); }
+        else if (v == 13) { RSK_WIRE(14, 5, 204, 2); RSK_WIRE(14, 4, 2, 2); }
         else { RSK_WIRE4(14, 5, 108, 2); RSK_WIRE(14, 4, 2, 2); }
     } else {
         if (v == 1) RSK_WIRE(0, 0, 2, 4);
@@ -2598,6 +2769,9 @@ int rsk_encode_wire_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const
         else if (v == 8) { RSK_WIRE(0, 3, 108, 2); RSK_WIRE(0, 4, 2, 2); }
         else if (v == 9) { RSK_WIRE(0, 5, 108, 2); RSK_WIRE(0, 4, 2, 2); }
         else if (v == 10) { RSK_WIRE4T(0, 5, 108, 2); RSK_WIRET(0, 4, 2, 2); }
+        else if (v == 11) { RSK_WIRE4(0, 5, 204, 2); RSK_WIRE(0, 4, 2, 2); }
+        else if (v == 12) { RSK_WIRE4(0, 5, 203, 2); RSK_WIRE(0, 4, 2, 2); }
+        else if (v == 13) { RSK_WIRE(0, 5, 204, 2); RSK_WIRE(0, 4, 2, 2); }
         else { RSK_WIRE4(0, 5, 108, 2); RSK_WIRE(0, 4, 2, 2); }
     }
 #else
