@@ -1108,6 +1108,54 @@ __device__ __forceinline__ void copy_wire_pkt(const EncArgs &a, const Lane1 &L, 
     }
 }
 
+// A wire packet whose first byte sits r = dst mod 16 (1..15) bytes into a chunk: destination chunk j
+// (aligned base d0 = dst - r) holds wire-image bytes [16j - r, 16j - r + 16), i.e. the 16 bytes at
+// offset 16 - r of image chunks j - 1 and j.  Image chunks c < NPRE are the prefix image in LDS (the
+// TCP checksum ORed into its chunk), c >= NPRE the payload chunks V of the copy (lane c - NPRE, slot
+// q; zero past the packet).  Lane l of slot q stores destination chunk NPRE + l + 64q with its
+// predecessor from lane l - 1 by a DPP wave shift (lane 0: the last prefix chunk, or lane 63 of slot
+// 0), lanes 0 .. NPRE - 1 the prefix chunks; chunk 0 from byte r on, the last up to the packet's
+// (padded) end, so packets packed at any byte offset never touch their neighbours.
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);  // wave_shr:1
+}
+template <int E, int NT>
+__device__ __forceinline__ void wire_store_shifted(const EncArgs &a, const uint32_t *img, uint32_t ck, uint8_t *dst,
+                                                   uint32_t r, uint32_t wlen, const uint4 (&V)[2], uint32_t lane) {
+    using G = WireGeom<E>;
+    uint8_t *d0 = dst - r;
+    const uint32_t nst = (r + padded_len(dst, wlen, a.pad) + 15u) >> 4;
+    const int wend = (int)(r + wlen);  // packet bytes counted from d0
+    const bool pad = a.pad != 0u;
+    const uint32_t sh = 16u - r;
+    // slot 1's lane 0 takes lane 63 of slot 0 (read in uniform flow); slot 0's lane 0 the last prefix chunk
+    const uint4 l63 = make_uint4(rdl(V[0].x, 63), rdl(V[0].y, 63), rdl(V[0].z, 63), rdl(V[0].w, 63));
+    const uint4 lastpre = *reinterpret_cast<const uint4 *>(img + 4 * (G::NPRE - 1));  // never the checksum chunk
+    static_assert(G::CK / 16 < G::NPRE - 1, "checksum chunk below the last prefix chunk");
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        uint4 prev = make_uint4(wave_shr1(V[q].x), wave_shr1(V[q].y), wave_shr1(V[q].z), wave_shr1(V[q].w));
+        if (lane == 0u) prev = q == 0 ? lastpre : l63;
+        const uint32_t j = G::NPRE + lane + 64u * q;
+        if (j < nst) store_last16<NT>(d0 + 16u * j, rsk::funnel16(prev, V[q], sh), wend - 16 * (int)j, pad);
+    }
+    if (lane < (uint32_t)G::NPRE && lane < nst) {
+        uint4 c1 = *reinterpret_cast<const uint4 *>(img + 4u * lane);
+        uint4 c0 = lane ? *reinterpret_cast<const uint4 *>(img + 4u * (lane - 1u)) : make_uint4(0u, 0u, 0u, 0u);
+        constexpr uint32_t kc = G::CK / 16, kw = (G::CK & 15) >> 2, kb = 8 * (G::CK & 3);
+        const uint32_t cw = ck << kb;
+        if (lane == kc) {
+            if (kw == 0) c1.x |= cw; else if (kw == 1) c1.y |= cw; else if (kw == 2) c1.z |= cw; else c1.w |= cw;
+        }
+        if (lane == kc + 1u) {
+            if (kw == 0) c0.x |= cw; else if (kw == 1) c0.y |= cw; else if (kw == 2) c0.z |= cw; else c0.w |= cw;
+        }
+        const uint4 d = rsk::funnel16(c0, c1, sh);
+        if (lane == 0u) rsk::store_range16(d0, d, r, 16u);
+        else store_last16<NT>(d0 + 16u * lane, d, wend - 16 * (int)lane, pad);
+    }
+}
+
 // ---- the same with one aligned load per chunk: the funnel partner comes from lane + 1 by DPP (as
 // copy_pkt_dpp), all PU packets' loads issued before the first shift. ------------------------------
 // TAG (sets of long frames, as copy_pkt_dpp_tag): phase 1 left the tag, payload[0] at frame byte
@@ -1212,18 +1260,23 @@ __device__ __forceinline__ void copy_wire_pkt_dpp(const EncArgs &a, const KeySch
 #pragma unroll
         for (int p = 0; p < PU; ++p) {
             if (!on[p]) continue;
-            const uint32_t nst = (padded_len(dstp[p], wlen[p], a.pad) + 15u) >> 4;
-            if (lane < (uint32_t)G::NPRE && lane < nst) {
-                const uint4 sv = *reinterpret_cast<const uint4 *>(stage + js[p] * G::NPW + 4u * lane);
-                uint32_t w4[4] = {sv.x, sv.y, sv.z, sv.w};
-                if (lane == (uint32_t)(G::CK / 16)) w4[(G::CK & 15) >> 2] |= ck[p] << (8 * (G::CK & 3));
-                store_last16<NT>(dstp[p] + 16u * lane, make_uint4(w4[0], w4[1], w4[2], w4[3]),
-                                (int)wlen[p] - 16 * (int)lane, a.pad != 0u);
-            }
+            const uint32_t r = (uint32_t)(reinterpret_cast<uintptr_t>(dstp[p]) & 15u);  // uniform
+            if (r == 0u) {
+                const uint32_t nst = (padded_len(dstp[p], wlen[p], a.pad) + 15u) >> 4;
+                if (lane < (uint32_t)G::NPRE && lane < nst) {
+                    const uint4 sv = *reinterpret_cast<const uint4 *>(stage + js[p] * G::NPW + 4u * lane);
+                    uint32_t w4[4] = {sv.x, sv.y, sv.z, sv.w};
+                    if (lane == (uint32_t)(G::CK / 16)) w4[(G::CK & 15) >> 2] |= ck[p] << (8 * (G::CK & 3));
+                    store_last16<NT>(dstp[p] + 16u * lane, make_uint4(w4[0], w4[1], w4[2], w4[3]),
+                                    (int)wlen[p] - 16 * (int)lane, a.pad != 0u);
+                }
 #pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const uint32_t k = G::NPRE + lane + 64u * q;
-                if (k < nst) store_last16<NT>(dstp[p] + 16u * k, v[p][q], (int)wlen[p] - 16 * (int)k, a.pad != 0u);
+                for (int q = 0; q < 2; ++q) {
+                    const uint32_t k = G::NPRE + lane + 64u * q;
+                    if (k < nst) store_last16<NT>(dstp[p] + 16u * k, v[p][q], (int)wlen[p] - 16 * (int)k, a.pad != 0u);
+                }
+            } else {
+                wire_store_shifted<E, NT>(a, stage + js[p] * G::NPW, ck[p], dstp[p], r, wlen[p], v[p], lane);
             }
         }
     }
@@ -1562,8 +1615,7 @@ __device__ __forceinline__ void encode_wire_set(const EncArgs &a, const WireArgs
         uint32_t wl = 0;
         if (i < a.n) {
             const uint32_t P = a.pay_len[i];
-            v0 = P != 0u && P <= (uint32_t)RSK_MAX_PAYLOAD &&
-                 ((reinterpret_cast<uintptr_t>(a.frame + a.frame_off[i]) & 15u) == 0);
+            v0 = P != 0u && P <= (uint32_t)RSK_MAX_PAYLOAD;  // any alignment (round 2: the DPP copy takes all)
             wl = G::HL + RSK_HEAD_SIZE + P;
         }
         if (wire_flat_choice<E>(v0, wl) != (MODE == 4)) return;
@@ -1571,18 +1623,21 @@ __device__ __forceinline__ void encode_wire_set(const EncArgs &a, const WireArgs
     Lane1 L = encode_phase1<MODE != 5>(a, ks, i);
     bool defer = false;
     if constexpr (MODE == 5) {  // as k_encode MODE 6: set mean frame length decides
-        const bool v = L.st > 0 && !L.slow;
+        const bool v = L.st > 0;
         uint32_t fl = v ? (uint32_t)L.st : 0u;
 #pragma unroll
         for (int off = 32; off; off >>= 1) fl += __shfl_xor(fl, off);
         defer = fl >= kDeferTagMeanBytes * (uint32_t)__popcll(__ballot(v));
-        if (!defer || L.slow) encode_tag(a, ks, L);
+        if (!defer) encode_tag(a, ks, L);
     }
     uint32_t PW[G::NPW];
     uint32_t sum_pre;
     int32_t wst;
-    wire_phase1<E>(a, wa, L, i, PW, sum_pre, wst, !defer || L.slow);
-    const bool vec = L.st > 0 && !L.slow;
+    // the DPP per-packet copy (PU 100..199) writes wire packets at any alignment; the other paths
+    // leave unaligned ones to the byte path
+    constexpr bool kAnyAlign = PU >= 100 && PU < 200;
+    wire_phase1<E>(a, wa, L, i, PW, sum_pre, wst, !defer || (L.slow && !kAnyAlign));
+    const bool vec = L.st > 0 && (kAnyAlign || !L.slow);
     const uint64_t vm = __ballot(vec);
     bool flat = MODE == 1 || MODE == 4;
     if constexpr (MODE == 2) flat = wire_flat_choice<E>(vec, (uint32_t)wst);
@@ -1635,7 +1690,7 @@ __device__ __forceinline__ void encode_wire_set(const EncArgs &a, const WireArgs
         }
         else copy_wire_pkt<E, PU>(a, L, stage, sum_pre, wst, lane, vm);
     }
-    const uint64_t sm = __ballot(L.st > 0 && L.slow);
+    const uint64_t sm = __ballot(L.st > 0 && L.slow && !kAnyAlign);
     if (sm) {
         wave_lds_sync();
         copy_wire_bytes<E>(a, L, stage, sum_pre, wst, lane, sm);
@@ -2548,10 +2603,12 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 // 31 / 32 / 33 / 34 = grouped interleave k_encode_gi <GRP, SBW> = <8, 1024> / <8, 4096> / <16, 1024> / <4, 1024>;
 // 35 / 36 = k_encode_ad (mapping chosen on the device from a pay_len sample), long at >= 1024 / 512 B;
 // 37 = the tiled mapping with the shipped copy (the form shipped before the grouped interleave);
-// 38 / 39 / 40 / 41 / 42 = grouped interleave <GRP, SBW> = <8,256> / <8,512> / <8,2048> / <16,512> / <32,256>.
+// 38 / 39 / 40 / 41 / 42 = grouped interleave <GRP, SBW> = <8,256> / <8,512> / <8,2048> / <16,512> / <32,256>;
+// 43 = 0 with the tag in the copy loop for every per-packet set (MODE 10); 44 / 45 / 46 = 0 with
+// 3 / 5 / 2 packets per pipelined batch.
 // v + 100 * cap (cap 1..4): the same kernel held to `cap` blocks per CU by unused LDS.
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
-    if (!c || v < 0 || v % 100 > 42 || v / 100 > 4) return RSK_EINVAL;
+    if (!c || v < 0 || v % 100 > 46 || v / 100 > 4) return RSK_EINVAL;
     c->enc_variant = v;
     return RSK_OK;
 }
@@ -2697,6 +2754,10 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         case 40: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 2048>), dim3(enc_grid(n, 8, 2048)), bd, lds, st, a, c->ks); break;
         case 41: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 16, 512>), dim3(enc_grid(n, 16, 512)), bd, lds, st, a, c->ks); break;
         case 42: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 32, 256>), dim3(enc_grid(n, 32, 256)), bd, lds, st, a, c->ks); break;
+        case 43: hipLaunchKernelGGL((k_encode<10, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
+        case 44: hipLaunchKernelGGL((k_encode<11, 3, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
+        case 45: hipLaunchKernelGGL((k_encode<11, 5, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
+        case 46: hipLaunchKernelGGL((k_encode<11, 2, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
         default: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
     }
 #else

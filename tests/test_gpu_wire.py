@@ -1,6 +1,7 @@
 """GPU: rsk_encode_wire_batch (RConn::Output + RawTcp::SendRawTcp / libnet build)
 against the oracle, byte for byte, for both link layouts, odd payload offsets, unaligned packet
-offsets (byte path) and the zero-pad modes; every packet's IPv4 and TCP checksums re-verified."""
+offsets (every offset r in a 16-B chunk, and packets back to back at byte granularity) and the
+zero-pad modes; every packet's IPv4 and TCP checksums re-verified."""
 from __future__ import annotations
 
 import os
@@ -19,7 +20,7 @@ KEY = b"hello135"
 
 
 @pytest.mark.parametrize("eth", [False, True])
-@pytest.mark.parametrize("layout", ["aligned", "odd_payload", "odd_wire"])
+@pytest.mark.parametrize("layout", ["aligned", "odd_payload", "odd_wire", "any_wire", "packed_wire"])
 @pytest.mark.parametrize("pad", [0, 16, 128])
 @pytest.mark.parametrize("mix", ["mixed", "short", "bimodal", "long"])
 # shipped kernel only; RSK_LIB=librsk_ab.so RSK_WIRE_VARIANTS=0,1,...,9 covers the A/B build
@@ -27,6 +28,8 @@ KEY = b"hello135"
 def test_wire_batch(codec, gpu, oracle, eth, layout, pad, mix, variant):
     import torch
 
+    if layout == "packed_wire" and pad:
+        pytest.skip("back-to-back packets leave no room for the zero pad")
     rng = np.random.default_rng(hash((eth, layout, pad, mix)) & 0xFFFF)
     lens = [0, 1, 2, 8, 9, 10, 11, 12, 15, 16, 17, 31, 32, 33, 100, 1000, 1400, 1468, 1469, 1470] + \
         list(rng.integers(1200 if mix == "long" else 1, 1470 if mix in ("mixed", "long") else 160, 400))
@@ -40,6 +43,11 @@ def test_wire_batch(codec, gpu, oracle, eth, layout, pad, mix, variant):
     payload = rng.integers(0, 256, n * pitch_p + 64, dtype=np.uint8)
     pitch_w = 1664 if pad == 128 else 1600  # PAD128 needs every slot's padded end inside the slot
     wire_off = (np.arange(n) * pitch_w + (5 if layout == "odd_wire" else 0)).astype(np.uint64)
+    if layout == "any_wire":  # every offset r = 0..15 within a 16-B chunk
+        wire_off = (np.arange(n) * pitch_w + (np.arange(n) * 7) % 16).astype(np.uint64)
+    elif layout == "packed_wire":  # back to back at byte granularity, 0-3 byte gaps (must survive)
+        wl = np.where((plen > 0) & (plen <= 1469), (14 if eth else 0) + 40 + 31 + plen.astype(np.int64), 0)
+        wire_off = np.concatenate([[3], np.cumsum(wl + rng.integers(0, 4, n))[:-1] + 3]).astype(np.uint64)
     cmd = rng.integers(0, 5, n).astype(np.uint8)
     conv = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
     ckey = rng.integers(0, 2**63, n, dtype=np.uint64)
