@@ -259,10 +259,9 @@ __device__ __forceinline__ uint64_t key_hash(const Key &k) {
 // Global table probe: a slot is one u64, fingerprint (hash bits 32..63) << 32 | the compacted index
 // of the key's first packet so far.  A slot with another fingerprint is skipped without touching that
 // packet's fields, a matching fingerprint is confirmed on the full key, and the index is lowered by
-// compare-and-swap (the fingerprint half never changes once claimed).  The first access is the CAS
-// itself: it claims an empty slot and returns an occupied one's word, so a new key costs one atomic
-// at the memory side (round 2: a load, a CAS and a separate atomicMin word cost four; the table's
-// atomic request rate is what bounds this kernel).
+// compare-and-swap (the fingerprint half never changes once claimed).  A relaxed load comes first:
+// a hot key's slot is read, not written, by every later tile (no RMW unless the index drops); a new
+// key costs the load and one CAS (round 2, first half: a load, a CAS and a separate atomicMin word).
 __device__ __forceinline__ uint32_t global_probe(const DmIn &a, const uint32_t *cidx, const uint32_t *cep,
                                                  unsigned long long *slots, uint32_t mask, const Key &k,
                                                  uint64_t hv, uint32_t j) {
@@ -270,8 +269,11 @@ __device__ __forceinline__ uint32_t global_probe(const DmIn &a, const uint32_t *
     const unsigned long long mine = ((unsigned long long)fp << 32) | j;
     uint32_t h = (uint32_t)hv & mask;
     for (;;) {
-        unsigned long long e = atomicCAS(slots + h, ~0ull, mine);
-        if (e == ~0ull) return h;  // claimed
+        unsigned long long e = __hip_atomic_load(slots + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (e == ~0ull) {
+            e = atomicCAS(slots + h, ~0ull, mine);
+            if (e == ~0ull) return h;  // claimed
+        }
         if ((uint32_t)(e >> 32) == fp) {
             const uint32_t o = (uint32_t)e;
             if (key_eq(load_key(a, cidx[o], cep[o]), k)) {
