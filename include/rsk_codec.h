@@ -151,9 +151,7 @@ typedef struct rsk_encode_in {
 typedef struct rsk_encode_out {
     uint8_t *frame_arena;     /* device bytes                                              */
     const uint64_t *frame_off;/* [n] where frame (wire packet) i starts; any offset is correct
-                                 and takes the vector path (16-B aligned: no partial head chunk;
-                                 wire build: short unaligned packets in short-frame sets take
-                                 a byte path)                                                  */
+                                 and takes the vector path (16-B aligned: no partial head chunk) */
     int32_t *status;          /* [n] 31+P, RSK_SEND_OVERSIZE or RSK_SEND_RESET              */
     uint32_t flags;           /* RSK_ENC_* below; 0 = write exactly 31+P bytes per frame      */
 } rsk_encode_out;

@@ -1530,6 +1530,111 @@ __device__ __forceinline__ void copy_wire_flat(const EncArgs &a, const Lane1 &L,
     }
 }
 
+// ---- the flat copy at any packet alignment (sets with an unaligned packet): the flat list holds
+// DESTINATION chunks j >= NPRE of every packet (r = dst mod 16; chunk j holds wire-image bytes
+// [16j - r, 16j - r + 16), the image chunks j - 1 and j funnelled by 16 - r).  A lane loads the
+// source chunks of image chunks j - 1 and j (three aligned loads; image chunk NPRE - 1 is the last
+// prefix chunk, from LDS), adds image chunk j's halfword sum to the packet's checksum (each image
+// chunk once: the extra destination chunk past the image sums nothing) and stores chunk j whole;
+// pass 2 stores the shifted prefix chunks (chunk 0 from byte r on) with the checksum.  Aligned
+// packets (r = 0) of such a set take the same path with chunk j = image chunk j.
+template <int E, int U>
+__device__ __forceinline__ void copy_wire_flat_any(const EncArgs &a, const Lane1 &L, const uint32_t *stage,
+                                                   uint32_t sum_pre, int32_t wst, uint32_t lane, bool mine,
+                                                   CopyRec *recs, uint32_t *cend, uint32_t *psum) {
+    using G = WireGeom<E>;
+    uint32_t cc = 0;
+    CopyRec r;
+    r.src_al = nullptr; r.dst = nullptr; r.cstart = 0; r.sh = 0; r.last_rel = 0; r.flen = 0;
+    if (mine) {
+        uint8_t *dst = a.frame + L.fo;
+        const uint32_t wlen = (uint32_t)wst;
+        const uint32_t ro = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15u);
+        const uint32_t nst = (ro + padded_len(dst, wlen, a.pad) + 15u) >> 4;  // destination chunks from d0
+        cc = nst > (uint32_t)G::NPRE ? nst - G::NPRE : 0u;
+        const uint8_t *pay = a.payload + L.po;
+        const uint32_t sh = (uint32_t)((reinterpret_cast<uintptr_t>(pay) + G::D0) & 15u);
+        r.src_al = pay + G::D0 - sh;
+        r.dst = dst;
+        r.sh = sh | (ro << 4);
+        r.last_rel = (int32_t)(wlen - G::HB) - 1 - G::D0 + (int32_t)sh;
+        r.flen = wlen;
+    }
+    uint32_t inc = cc;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t v = __shfl_up(inc, off);
+        if (lane >= (uint32_t)off) inc += v;
+    }
+    r.cstart = inc - cc;
+    recs[lane] = r;
+    cend[lane] = inc;
+    psum[lane] = sum_pre;
+    const uint32_t C = (uint32_t)__shfl((int)inc, 63);
+    wave_lds_sync();
+    for (uint32_t g0 = 0; g0 < C; g0 += 64u * U) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t g = g0 + 64u * u + lane;
+            if (g >= C) continue;
+            uint32_t lo = 0;
+#pragma unroll
+            for (uint32_t st = 32; st; st >>= 1)
+                if (cend[lo + st - 1] <= g) lo += st;
+            const CopyRec rr = recs[lo];
+            const uint32_t sh = rr.sh & 15u, ro = rr.sh >> 4;
+            const uint32_t m = g - rr.cstart;  // image / destination chunk NPRE + m
+            // image chunk NPRE + m from source chunks m, m + 1; image chunk NPRE + m - 1 from m - 1, m
+            uint4 S0 = make_uint4(0u, 0u, 0u, 0u), S1 = S0, S2 = S0;
+            if ((int32_t)(16u * m) <= rr.last_rel) S1 = ld16<0>(rr.src_al + 16u * m);
+            if ((int32_t)(16u * m + 16u) <= rr.last_rel) S2 = ld16<0>(rr.src_al + 16u * m + 16u);
+            if (ro != 0u && m != 0u) S0 = ld16<0>(rr.src_al + 16u * m - 16u);
+            const int32_t limi = (int32_t)rr.flen - 16 * (G::NPRE + (int32_t)m);  // packet bytes in image chunk
+            uint4 im = limi > 0 ? funnel16_lane(S1, S2, sh) : make_uint4(0u, 0u, 0u, 0u);
+            if (limi > 0 && limi < 16) im = rsk::keep_bytes16(im, limi);
+            const uint32_t s = hsum4(im, 0u);
+            if (s) atomicAdd(&psum[lo], s);
+            uint4 d = im;
+            if (ro != 0u) {
+                const uint4 ip = m == 0u ? *reinterpret_cast<const uint4 *>(stage + lo * G::NPW + 4 * (G::NPRE - 1))
+                                         : funnel16_lane(S0, S1, sh);  // image chunk NPRE + m - 1 (full)
+                d = funnel16_lane(ip, im, 16u - ro);
+            }
+            const uint32_t jj = G::NPRE + m;
+            store_last16<0>(rr.dst - ro + 16u * jj, d, (int)(ro + rr.flen) - 16 * (int)jj, a.pad != 0u);
+        }
+    }
+    wave_lds_sync();
+    // pass 2: shifted prefix chunk (j, c) for g = NPRE * j + c
+    static_assert(G::CK / 16 < G::NPRE - 1, "checksum chunk below the last prefix chunk");
+#pragma unroll
+    for (int t = 0; t < G::NPRE; ++t) {
+        const uint32_t g = 64u * t + lane;
+        const uint32_t j = g / G::NPRE, c = g - j * G::NPRE;
+        const CopyRec rr = recs[j];
+        if (rr.dst == nullptr) continue;  // not framed
+        const uint32_t ro = rr.sh >> 4;
+        const uint32_t nstj = (ro + padded_len(rr.dst, rr.flen, a.pad) + 15u) >> 4;
+        if (c >= nstj) continue;
+        const uint32_t ck = ~fold16(psum[j]) & 0xffffu;
+        constexpr uint32_t kc = G::CK / 16, kw = (G::CK & 15) >> 2, kb = 8 * (G::CK & 3);
+        uint4 c1 = *reinterpret_cast<const uint4 *>(stage + j * G::NPW + 4u * c);
+        uint4 c0 = c ? *reinterpret_cast<const uint4 *>(stage + j * G::NPW + 4u * (c - 1u)) : make_uint4(0u, 0u, 0u, 0u);
+        const uint32_t cw = ck << kb;
+        if (c == kc) {
+            if (kw == 0) c1.x |= cw; else if (kw == 1) c1.y |= cw; else if (kw == 2) c1.z |= cw; else c1.w |= cw;
+        }
+        if (c == kc + 1u) {
+            if (kw == 0) c0.x |= cw; else if (kw == 1) c0.y |= cw; else if (kw == 2) c0.z |= cw; else c0.w |= cw;
+        }
+        uint8_t *d0 = rr.dst - ro;
+        if (ro == 0u) store_last16<0>(d0 + 16u * c, c1, (int)rr.flen - 16 * (int)c, a.pad != 0u);
+        else if (c == 0u) rsk::store_range16(d0, funnel16_lane(c0, c1, 16u - ro), ro, 16u);
+        else store_last16<0>(d0 + 16u * c, funnel16_lane(c0, c1, 16u - ro), (int)(ro + rr.flen) - 16 * (int)c,
+                             a.pad != 0u);
+    }
+}
+
 // ---- wire packets that are not 16-B aligned: byte path (prefix bytes from the lane image)
 template <int E>
 __device__ __forceinline__ void copy_wire_bytes(const EncArgs &a, const Lane1 &L, const uint32_t *stage,
@@ -1653,7 +1758,10 @@ __device__ __forceinline__ void encode_wire_set(const EncArgs &a, const WireArgs
         if (flat) {
             CopyRec *recs = reinterpret_cast<CopyRec *>(slice + WireLds<E, MODE>::kStage);
             uint32_t *cend = reinterpret_cast<uint32_t *>(slice + WireLds<E, MODE>::kStage + 64 * sizeof(CopyRec));
-            copy_wire_flat<E, U>(a, L, stage, sum_pre, wst, lane, vec, recs, cend, cend + 64);
+            if (MODE == 4 && __ballot(L.st > 0 && L.slow) != 0ull)  // an unaligned packet: any-alignment list
+                copy_wire_flat_any<E, U>(a, L, stage, sum_pre, wst, lane, L.st > 0, recs, cend, cend + 64);
+            else
+                copy_wire_flat<E, U>(a, L, stage, sum_pre, wst, lane, vec, recs, cend, cend + 64);
         }
     }
     if (!flat) {
@@ -1690,7 +1798,8 @@ __device__ __forceinline__ void encode_wire_set(const EncArgs &a, const WireArgs
         }
         else copy_wire_pkt<E, PU>(a, L, stage, sum_pre, wst, lane, vm);
     }
-    const uint64_t sm = __ballot(L.st > 0 && L.slow && !kAnyAlign);
+    // (the flat half sends a set with an unaligned packet through copy_wire_flat_any)
+    const uint64_t sm = __ballot(L.st > 0 && L.slow && !kAnyAlign && !(MODE == 4 && flat));
     if (sm) {
         wave_lds_sync();
         copy_wire_bytes<E>(a, L, stage, sum_pre, wst, lane, sm);
