@@ -119,7 +119,8 @@ __device__ __forceinline__ void head_words(uint32_t cmd, uint32_t id0, uint32_t 
 
 // ---- phase 1: one lane per packet ---------------------------------------------------------------
 // status (RConn.cpp:88-98), tag (rhash.cpp:20-41 via md5_tag), frame words 0..7 (tag + EncHead +
-// payload[0]); `slow` marks a framed packet whose frame is not 16-B aligned (byte path).
+// payload[0]); `slow` marks a framed packet whose frame is not 16-B aligned (k_encode_wire: the
+// shifted copies; the byte path of the A/B modes).
 struct Lane1 {
     int32_t st;
     uint64_t po, fo;
@@ -1635,7 +1636,8 @@ __device__ __forceinline__ void copy_wire_flat_any(const EncArgs &a, const Lane1
     }
 }
 
-// ---- wire packets that are not 16-B aligned: byte path (prefix bytes from the lane image)
+// ---- wire packets that are not 16-B aligned, A/B modes 0-3 only: byte path (prefix bytes from the
+// lane image)
 template <int E>
 __device__ __forceinline__ void copy_wire_bytes(const EncArgs &a, const Lane1 &L, const uint32_t *stage,
                                                 uint32_t sum_pre, int32_t wst, uint32_t lane, uint64_t sm) {
@@ -1738,8 +1740,8 @@ __device__ __forceinline__ void encode_wire_set(const EncArgs &a, const WireArgs
     uint32_t PW[G::NPW];
     uint32_t sum_pre;
     int32_t wst;
-    // the DPP per-packet copy (PU 100..199) writes wire packets at any alignment; the other paths
-    // leave unaligned ones to the byte path
+    // the DPP per-packet copy (PU 100..199) writes wire packets at any alignment, and so does the
+    // flat half (MODE 4, copy_wire_flat_any); the A/B modes leave unaligned ones to the byte path
     constexpr bool kAnyAlign = PU >= 100 && PU < 200;
     wire_phase1<E>(a, wa, L, i, PW, sum_pre, wst, !defer || (L.slow && !kAnyAlign));
     const bool vec = L.st > 0 && (kAnyAlign || !L.slow);
