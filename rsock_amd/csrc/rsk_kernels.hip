@@ -2716,10 +2716,10 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 // 37 = the tiled mapping with the shipped copy (the form shipped before the grouped interleave);
 // 38 / 39 / 40 / 41 / 42 = grouped interleave <GRP, SBW> = <8,256> / <8,512> / <8,2048> / <16,512> / <32,256>;
 // 43 = 0 with the tag in the copy loop for every per-packet set (MODE 10); 44 / 45 / 46 = 0 with
-// 3 / 5 / 2 packets per pipelined batch.
+// 3 / 5 / 2 packets per pipelined batch; 47 / 48 = the unpipelined copy (MODE 6), 8 / 12 packets.
 // v + 100 * cap (cap 1..4): the same kernel held to `cap` blocks per CU by unused LDS.
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
-    if (!c || v < 0 || v % 100 > 46 || v / 100 > 4) return RSK_EINVAL;
+    if (!c || v < 0 || v % 100 > 48 || v / 100 > 4) return RSK_EINVAL;
     c->enc_variant = v;
     return RSK_OK;
 }
@@ -2869,6 +2869,8 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         case 44: hipLaunchKernelGGL((k_encode<11, 3, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
         case 45: hipLaunchKernelGGL((k_encode<11, 5, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
         case 46: hipLaunchKernelGGL((k_encode<11, 2, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
+        case 47: hipLaunchKernelGGL((k_encode<6, 8, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
+        case 48: hipLaunchKernelGGL((k_encode<6, 12, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
         default: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
     }
 #else
