@@ -1,10 +1,15 @@
 #!/usr/bin/env python3
 """Benchmark: device-resident EncHead+MD5 encode then decode+verify+compact (BASELINE.json metric).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4|c5] [--no-cpu-baseline] [--eager]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4|c5] [--tag md5|table]
+                  [--no-cpu-baseline] [--eager]
 
 One step = one pass of the hot path over one batch: k_encode (RConn::Output framing of every
 packet) followed by k_decode + k_compact (RConn::OnRecv of every frame), inputs resident in HBM.
+The headline computes the tag by one MD5 compression per packet and lane in both kernels
+(RSK_TAG_MD5, as util/rhash.cpp:20-41 does per packet); at N = 1 the same step with the tag looked
+up in the key's 256-entry table (RSK_TAG_TABLE) is timed afterwards and reported under its own
+label (`variant_tag_table_lut`), never as `value`.
 The timed region replays a HIP graph of the step (one host launch per step; --eager: the three
 library calls per step instead); the per-kernel times behind `roofline` come from HIP events on
 the step's stream around the same launches issued one by one right after the timed region.
@@ -33,6 +38,10 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Mpkt/s + GiB/s device-resident EncHead+MD5 encode/decode at 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# tag modes (rsk_set_tag_mode): the headline computes MD5 per lane, as the reference does per packet
+TAG_LABEL = {"md5": "md5_per_lane", "table": "tag_table_lut"}
+TAG_TEXT = {"md5": "one MD5 compression per packet and lane",
+            "table": "lookup in the key's 256-entry tag table staged in LDS (MD5 run once per key, 256 tags)"}
 
 
 def enc_bytes_per_pkt(p):
@@ -76,11 +85,12 @@ def _cpu_quota() -> float | None:
         return None
 
 
-def cpu_baseline(cfg: str, n_sample: int, min_seconds: float) -> dict:
-    """The reference's own codec (oracle/_ref, compiled from /root/reference sources) or, if that
-    was not built, the C restatement, timed on this host's cores over a bounded sample
-    (SURVEY.md §8d: std::thread x every core of the affinity mask, contiguous shards, plus a
-    1-thread number on the same arenas)."""
+def cpu_baseline(cfg: str, n_sample: int, min_seconds: float, use_ref: bool = False) -> dict:
+    """The clean-room C restatement (oracle/rsk_oracle.c, "port", SURVEY.md §8d: "the build's own
+    clean-room restatement ... the reference binary itself never goes to the GPU box") timed on this
+    host's cores over a bounded sample: std::thread x every core of the affinity mask, contiguous
+    shards, plus a 1-thread number on the same arenas.  use_ref (--cpu-baseline-ref, a cross-check
+    in the build container): the reference's own codec compiled into oracle/_ref instead."""
     from rsock_amd import workload
     from tests import oracle_lib
 
@@ -89,7 +99,9 @@ def cpu_baseline(cfg: str, n_sample: int, min_seconds: float) -> dict:
     payload = workload.payload_bytes_np(d)
     frames = np.zeros(d.n * d.frame_pitch, np.uint8)
     key = b"hello135"
-    if oracle_lib.ref_available():
+    if use_ref:
+        if not oracle_lib.ref_available():
+            raise SystemExit("bench: --cpu-baseline-ref needs oracle/_ref (make -C oracle ref)")
         ref = oracle_lib.RefOracle()
         kind = "reference"
 
@@ -100,9 +112,7 @@ def cpu_baseline(cfg: str, n_sample: int, min_seconds: float) -> dict:
         kind = "port"
 
         def run(threads, m):
-            dm = _prefix(d, m)
-            fr, st = orc.encode_batch(key, payload, dm, workload.ID_UNIFORM, nthreads=threads)
-            orc.decode_batch(key, fr, dm.frame_off, dm.frame_len, nthreads=threads)
+            orc.bench_codec(key, payload, _prefix(d, m), workload.ID_UNIFORM, frames, threads)
 
     def timed(threads, m, seconds):
         run(threads, m)  # warm (page faults on the frame arena)
@@ -219,6 +229,13 @@ def main() -> None:
     ap.add_argument("--eager", action="store_true",
                     help="launch the step's kernels one by one in the timed region instead of replaying a "
                          "captured HIP graph of the step")
+    ap.add_argument("--tag", default="md5", choices=["md5", "table"],
+                    help="tag mode of the headline (default md5: MD5 per lane; table: the LUT variant)")
+    ap.add_argument("--no-tag-variant", action="store_true",
+                    help="skip timing the other tag mode after the headline (N = 1)")
+    ap.add_argument("--cpu-baseline-ref", action="store_true",
+                    help="time the reference's own codec (oracle/_ref, build container only) as the CPU "
+                         "baseline instead of the clean-room restatement")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal only: every rank uses GPU 0 (N ranks on a 1-GPU box)")
     args = ap.parse_args()
@@ -258,7 +275,7 @@ def main() -> None:
         # weak scaling: rank r owns packets [r*n, (r+1)*n) of the config's global stream
         d = workload.describe(cfg, rank * n, (rank + 1) * n, n=world * n)
     w = workload.DeviceWorkload(d, dev)
-    cx = rc.Codec(b"hello135", gpu)
+    cx = rc.Codec(b"hello135", gpu, tag_mode=args.tag)
     graph_mode = not args.eager
     # graph capture needs a stream other than the null stream; the codec's per-stream workspaces are
     # sized on it by the warmup, before the capture
@@ -277,53 +294,61 @@ def main() -> None:
         if ev is not None:
             ev[2].record(stream)
 
-    with torch.cuda.stream(stream):
-        for _ in range(args.warmup):
-            step()
-    torch.cuda.synchronize()
     # correctness gate on the measured data: every packet must verify
     expect_valid = int(((d.pay_len >= 1) & (d.pay_len <= 1469)).sum())
 
     def gate(when):
         nv = int(w.dec.n_valid.item())
         if nv != expect_valid:
-            raise SystemExit(f"bench: decode verified {nv} of {expect_valid} packets ({when})")
+            raise SystemExit(f"bench: decode verified {nv} of {expect_valid} packets ({when}, tag {cx.tag_mode})")
 
-    gate("warmup")
-    graph = None
-    if graph_mode:
-        # the whole step (k_encode, k_decode, k_compact) as one HIP graph: one launch per step from
-        # the host instead of three library calls, so the timed region measures the GPU, not Python
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, stream=stream):
-            step()
-        w.dec.n_valid.zero_()
-        graph.replay()
-        torch.cuda.synchronize()
-        gate("graph replay")
-
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        if graph is not None:
-            graph.replay()
-        else:
-            step(evs[k])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    gate("timed region")
-    if graph is not None:
-        # per-kernel durations for the roofline: HIP events on the step's stream around the same
-        # launches, issued one by one (the graph replays the identical kernels and arguments)
+    def timed(mode: str, steps: int, warmup: int, sync_ranks: bool):
+        """Warm up, capture the step as a graph (the tag mode is fixed at capture), time `steps`
+        replays between barriers, then per-kernel HIP events on the step's stream."""
+        cx.set_tag_mode(mode)
         with torch.cuda.stream(stream):
-            for k in range(args.steps):
+            for _ in range(warmup):
+                step()
+        torch.cuda.synchronize()
+        gate(f"warmup")
+        graph = None
+        if graph_mode:
+            # the whole step (k_encode, k_decode, k_compact) as one HIP graph: one launch per step from
+            # the host instead of three library calls, so the timed region measures the GPU, not Python
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=stream):
+                step()
+            w.dec.n_valid.zero_()
+            graph.replay()
+            torch.cuda.synchronize()
+            gate("graph replay")
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+        if sync_ranks:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            if graph is not None:
+                graph.replay()
+            else:
                 step(evs[k])
         torch.cuda.synchronize()
+        if sync_ranks:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        gate("timed region")
+        cx.check_device_errors()  # raises if a compaction look-back gave up (rsk_check_device_errors)
+        if graph is not None:
+            # per-kernel durations for the roofline: HIP events on the step's stream around the same
+            # launches, issued one by one (the graph replays the identical kernels and arguments)
+            with torch.cuda.stream(stream):
+                for k in range(steps):
+                    step(evs[k])
+            torch.cuda.synchronize()
+            del graph
+        return el, evs
+
+    elapsed, evs = timed(args.tag, args.steps, args.warmup, world > 1)
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -338,6 +363,15 @@ def main() -> None:
     enc_bytes = int(enc_bytes_per_pkt(d.pay_len.astype(np.int64)).sum())
     bytes_step = enc_bytes + d.n * dec_bytes_per_pkt()
     achieved = enc_bytes / (enc_ms * 1e-3) / 1e9
+
+    other = None
+    if world == 1 and not args.no_tag_variant:
+        # the other tag mode, reported beside the headline under its own label
+        omode = "table" if args.tag == "md5" else "md5"
+        el_o, evs_o = timed(omode, args.steps, max(2, args.warmup // 2), False)
+        enc_o = float(np.mean([e[0].elapsed_time(e[1]) for e in evs_o]))
+        dec_o = float(np.mean([e[1].elapsed_time(e[2]) for e in evs_o]))
+        other = (omode, el_o, enc_o, dec_o)
 
     if rank == 0:
         tr = load_traffic(cfg, d.n, d.frame_pitch)
@@ -355,14 +389,16 @@ def main() -> None:
             "dtype": "u8",
             "data": "synthetic (splitmix64 payloads/fields, SURVEY.md §8d)",
             "config": {
-                "workload": f"{cfg.upper()}: {d.n} packets/GPU, {p}-B payloads, encode(tag+EncHead+copy) then "
-                            f"decode+verify+compact, device-resident",
+                "workload": f"{cfg.upper()}: {d.n} packets/GPU, {p}-B payloads, encode (tag = "
+                            f"{TAG_TEXT[args.tag]} + EncHead + payload copy) then decode + tag verify + compact, "
+                            f"device-resident",
                 "packets_per_gpu": d.n,
                 "packets_total": n_total if strong else world * d.n,
                 "payload_bytes": p,
                 "frame_slot_bytes": d.frame_pitch,
                 "zero_pad": d.pad,
                 "key": "hello135",
+                "tag": TAG_LABEL[args.tag],
                 "parallelism": f"shard{world} (no collective)",
             },
             "gib_per_s": round(world * bytes_step * args.steps / elapsed_max / 2**30, 2),
@@ -383,8 +419,19 @@ def main() -> None:
         }
         if tr is not None:
             line["roofline"]["traffic_source"] = tr.get("source", "profiles/traffic.json")
+        if other is not None:
+            omode, el_o, enc_o, dec_o = other
+            line[f"variant_{TAG_LABEL[omode]}"] = {
+                "label": f"NOT the headline: same step with the tag = {TAG_TEXT[omode]}",
+                "value": round(d.n * args.steps / el_o / 1e6, 2),
+                "unit": "Mpkt/s",
+                "ms_per_step": round(el_o / args.steps * 1e3, 4),
+                "kernels_ms": {"k_encode": round(enc_o, 4), "decode+compact": round(dec_o, 4)},
+                "roofline_frac": round(enc_bytes / (enc_o * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(cfg, min(args.cpu_sample, d.n), args.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline(cfg, min(args.cpu_sample, d.n), args.cpu_seconds,
+                                                use_ref=args.cpu_baseline_ref)
         print(json.dumps(line), flush=True)
     cx.close()
     if world > 1:

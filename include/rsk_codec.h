@@ -110,25 +110,56 @@ typedef struct rsk_ctx rsk_ctx;
 
 /* Create a codec context bound to HIP device `device` for hash key `key` (host pointer, key_len
  * bytes, any length; rsock's default is "hello135", bean/RConfig.h:44).  The tag is
- * MD5(key || payload[0])[8..15] (util/rhash.cpp:20-41), so a key has 256 tags: the key's MD5
- * message schedule is precomputed here (chaining state of the whole-key blocks, the constant words
- * of the block that carries the payload byte, the padding block when one is needed) and one GPU
- * launch (k_tag_table) compresses the 256 tags into a 2-KB device table that the framing and
- * verifying kernels stage in LDS.  Synchronous; returns NULL on failure (rsk_last_error). */
+ * MD5(key || payload[0])[8..15] (util/rhash.cpp:20-41).  The key's MD5 message schedule is
+ * precomputed here (chaining state of the whole-key blocks, the constant words of the block that
+ * carries the payload byte, the padding block when one is needed), and one GPU launch (k_tag_table)
+ * compresses the key's 256 possible tags into a 2-KB device table for RSK_TAG_TABLE.  The context
+ * starts in RSK_TAG_MD5.  Synchronous; returns NULL on failure (rsk_last_error). */
 rsk_ctx *rsk_create(const uint8_t *key, uint32_t key_len, int device);
 void rsk_destroy(rsk_ctx *ctx);
+
+/* Tag mode of every later framing / verifying launch of this context (outputs are identical):
+ *   RSK_TAG_MD5    (default) one MD5 compression per packet and lane, as the reference computes it
+ *                  per packet (compute_hash / hash_equal, util/rhash.cpp:20-41, 71-92);
+ *   RSK_TAG_TABLE  the tag is a function of payload[0] alone, so it is looked up in the key's
+ *                  256-entry table (staged in LDS per block) instead of recomputed.
+ * The mode is read when a call is issued (a hipGraph keeps the mode of its capture); do not change it
+ * while another thread issues calls on the same context.  rsk_set_tag_mode returns RSK_EINVAL for an
+ * unknown mode, rsk_get_tag_mode the current mode (or RSK_EINVAL for a NULL ctx). */
+#define RSK_TAG_MD5 0
+#define RSK_TAG_TABLE 1
+int rsk_set_tag_mode(rsk_ctx *ctx, int mode);
+int rsk_get_tag_mode(const rsk_ctx *ctx);
 
 /* Streams: a context may be used from several streams at once.  Its device scratch (compaction
  * ballots and look-back state, demux and send-seq tables) is kept per stream, so calls on different streams
  * never share it; calls on ONE stream must be issued in the order the caller wants them to run
  * (from one host thread at a time, as with any hipStream_t).  The only per-context state the
- * kernels read is the immutable key schedule and tag table.
+ * kernels read is the immutable key schedule and tag table (and the tag mode, passed by value).
  *
  * Pre-size the compaction scratch of `stream` (rsk_reserve: the legacy default stream, NULL) for
  * batches of up to n packets.  Batch calls grow it on demand, which waits for that stream to
  * drain and allocates; reserve first if batch calls will be captured into a hipGraph. */
 int rsk_reserve(rsk_ctx *ctx, uint32_t n_max);
 int rsk_reserve_stream(rsk_ctx *ctx, uint32_t n_max, void *stream);
+/* Scratch stays allocated per stream until the context is destroyed or the stream is released:
+ * rsk_release_stream waits for `stream` to drain and frees its scratch (call it before destroying a
+ * stream whose handle value a later stream may reuse).  A batch call issued while `stream` is being
+ * captured into a hipGraph cannot allocate, grow or initialise that scratch (RSK_EINVAL): reserve
+ * the stream and run one eager call on it before the capture.  A graph's scratch is its capture
+ * stream's: replay it on that stream, or on streams ordered with it. */
+int rsk_release_stream(rsk_ctx *ctx, void *stream);
+
+/* Device-side error flags, sticky per context.  RSK_DEVERR_LOOKBACK: a decoupled look-back (the
+ * VALID-list compaction of the decode entry points, the demux) gave up waiting for a predecessor
+ * tile after ~4M polls, so that call's valid_idx / n_valid / demux outputs are wrong (the stalled
+ * compaction tile also writes n_valid = 0xFFFFFFFF); the spin limit exists so that such a stall can
+ * never hang the GPU.  rsk_check_device_errors waits for the device, stores the flags in *flags
+ * (may be NULL) and clears them; when any flag was set it returns RSK_EDEVICE and re-initialises
+ * the context's look-back state on every stream at its next call there (graphs captured earlier
+ * must be captured again). */
+#define RSK_DEVERR_LOOKBACK 0x1u
+int rsk_check_device_errors(rsk_ctx *ctx, uint32_t *flags);
 
 /* Text of the last HIP error seen by this thread (static storage). */
 const char *rsk_last_error(void);

@@ -51,6 +51,11 @@ int rsk_rconn_output(rsk_rconn *r, int64_t nread, const char *base, uint8_t cmd,
 int rsk_rconn_onrecv(rsk_rconn *r, int64_t nread, const char *base, int tcp_close, void *user);
 /* Run everything queued and deliver every outstanding result. */
 int rsk_rconn_flush(rsk_rconn *r);
+/* Send and reset callbacks run at delivery, not inside rsk_rconn_output, so their return values
+ * (RawTcp::Send / RConnReset::SendReset results, which RConn::Output returns synchronously,
+ * RConn.cpp:108-123) cannot be the output call's result: every callback that returned < 0 is
+ * counted here instead (since creation). */
+uint64_t rsk_rconn_callback_failures(const rsk_rconn *r);
 
 #ifdef __cplusplus
 }

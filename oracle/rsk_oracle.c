@@ -470,6 +470,65 @@ typedef struct {
     const uint8_t *key;
     size_t key_len;
     uint32_t lo, hi;
+    const uint8_t *payload_arena;
+    const uint64_t *pay_off;
+    const uint16_t *pay_len;
+    const uint8_t *cmd;
+    const uint32_t *conv;
+    const uint64_t *conn_key;
+    const uint8_t *id;
+    uint8_t *frame_arena;
+    const uint64_t *frame_off;
+    uint64_t good;
+} bench_job;
+
+static void *bench_run(void *arg) {
+    bench_job *j = (bench_job *)arg;
+    uint64_t good = 0;
+    for (uint32_t i = j->lo; i < j->hi; i++) {
+        uint8_t base[RSK_MAX_PKT_SIZE];
+        memset(base, 0, sizeof base); /* RConn.cpp:100: char base[OM_MAX_PKT_SIZE] = {0} */
+        int st = orc_rconn_output(j->key, j->key_len, j->payload_arena + j->pay_off[i], j->pay_len[i], j->cmd[i],
+                                  j->id, j->conv[i], j->conn_key[i], base);
+        if (st <= 0) continue;
+        uint8_t *fr = j->frame_arena + j->frame_off[i];
+        memcpy(fr, base, (size_t)st);
+        orc_dec d;
+        if (orc_rconn_onrecv(j->key, j->key_len, fr, st, 0, &d) == RSK_RECV_VALID) good++;
+    }
+    j->good = good;
+    return NULL;
+}
+
+uint64_t orc_bench_codec(const uint8_t *key, size_t key_len, uint32_t n, const uint8_t *payload_arena,
+                         const uint64_t *pay_off, const uint16_t *pay_len, const uint8_t *cmd,
+                         const uint32_t *conv, const uint64_t *conn_key, const uint8_t id[8],
+                         uint8_t *frame_arena, const uint64_t *frame_off, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if ((uint32_t)nthreads > n) nthreads = n ? (int)n : 1;
+    bench_job *jobs = (bench_job *)calloc((size_t)nthreads, sizeof *jobs);
+    pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof *th);
+    for (int t = 0; t < nthreads; t++) {
+        bench_job j = {key, key_len, (uint32_t)((uint64_t)n * t / nthreads), (uint32_t)((uint64_t)n * (t + 1) / nthreads),
+                       payload_arena, pay_off, pay_len, cmd, conv, conn_key, id, frame_arena, frame_off, 0};
+        jobs[t] = j;
+    }
+    for (int t = 1; t < nthreads; t++) pthread_create(&th[t], NULL, bench_run, &jobs[t]);
+    bench_run(&jobs[0]);
+    uint64_t good = jobs[0].good;
+    for (int t = 1; t < nthreads; t++) {
+        pthread_join(th[t], NULL);
+        good += jobs[t].good;
+    }
+    free(jobs);
+    free(th);
+    return good;
+}
+
+typedef struct {
+    const uint8_t *key;
+    size_t key_len;
+    uint32_t lo, hi;
     const uint8_t *frame_arena;
     const uint64_t *frame_off;
     const uint16_t *frame_len;

@@ -133,6 +133,15 @@ void orc_encode_batch(const uint8_t *key, size_t key_len, uint32_t n, const uint
                       const uint8_t id_uniform[8], uint8_t *frame_arena, const uint64_t *frame_off,
                       int32_t *status, int nthreads);
 
+/* CPU baseline (bench.py cpu_baseline, kind "port"): per packet i in [0, n), RConn::Output framing
+ * into a zeroed 1500-B stack buffer (RConn.cpp:100-104), the frame stored to frame_arena +
+ * frame_off[i], then RConn::OnRecv (DecodeBuf + hash_equal) on the stored frame.  Contiguous shards
+ * over nthreads pthreads; returns the number of verified packets. */
+uint64_t orc_bench_codec(const uint8_t *key, size_t key_len, uint32_t n, const uint8_t *payload_arena,
+                         const uint64_t *pay_off, const uint16_t *pay_len, const uint8_t *cmd,
+                         const uint32_t *conv, const uint64_t *conn_key, const uint8_t id[8],
+                         uint8_t *frame_arena, const uint64_t *frame_off, int nthreads);
+
 void orc_decode_batch(const uint8_t *key, size_t key_len, uint32_t n, const uint8_t *frame_arena,
                       const uint64_t *frame_off, const uint16_t *frame_len,
                       const uint8_t *is_tcp_close, uint8_t *hlen, uint8_t *cmd, uint8_t *id,

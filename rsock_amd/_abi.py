@@ -33,6 +33,8 @@ PARSE_DROP, PARSE_DELIVER, PARSE_SYN, PARSE_MALFORMED, PARSE_SLOT_SHORT = 0, 1, 
 CAP_SLOT_MIN = 64
 PARSE_HAS_ACK_POOL, PARSE_IS_SERVER = 0x1, 0x2
 FILTER_MAX_PORTS = 64
+TAG_MD5, TAG_TABLE = 0, 1
+DEVERR_LOOKBACK = 0x1
 DEMUX_ID, DEMUX_CONN_KEY, DEMUX_CONV, DEMUX_DST, DEMUX_CMD_BARRIER = 0x01, 0x02, 0x04, 0x08, 0x10
 
 _vp = ctypes.c_void_p
@@ -125,8 +127,12 @@ class CaptureFilter(ctypes.Structure):
 SIGNATURES = [
     ("rsk_create", _vp, [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_int]),
     ("rsk_destroy", None, [_vp]),
+    ("rsk_set_tag_mode", ctypes.c_int, [_vp, ctypes.c_int]),
+    ("rsk_get_tag_mode", ctypes.c_int, [_vp]),
     ("rsk_reserve", ctypes.c_int, [_vp, ctypes.c_uint32]),
     ("rsk_reserve_stream", ctypes.c_int, [_vp, ctypes.c_uint32, _vp]),
+    ("rsk_release_stream", ctypes.c_int, [_vp, _vp]),
+    ("rsk_check_device_errors", ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_uint32)]),
     ("rsk_last_error", ctypes.c_char_p, []),
     ("rsk_version", ctypes.c_char_p, []),
     ("rsk_encode_batch", ctypes.c_int,
@@ -182,6 +188,7 @@ SIGNATURES = [
      [_vp, ctypes.c_int64, ctypes.c_char_p, ctypes.c_uint8, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint64, _vp]),
     ("rsk_rconn_onrecv", ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_char_p, ctypes.c_int, _vp]),
     ("rsk_rconn_flush", ctypes.c_int, [_vp]),
+    ("rsk_rconn_callback_failures", ctypes.c_uint64, [_vp]),
 ]
 
 SEND_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p)

@@ -232,15 +232,32 @@ class TcpInfoBuffers:
         return {f.name: getattr(self, f.name).cpu().numpy() for f in fields(self)}
 
 
-class Codec:
-    """One rsk_ctx: a hash key bound to a HIP device."""
+TAG_MODES = {"md5": _abi.TAG_MD5, "table": _abi.TAG_TABLE}
 
-    def __init__(self, key: bytes = b"hello135", device: int = 0):
+
+class Codec:
+    """One rsk_ctx: a hash key bound to a HIP device.  ``tag_mode`` "md5" (default: the MD5
+    compression per packet, as util/rhash.cpp:20-41 computes it) or "table" (the key's 256 tags
+    looked up; identical outputs), see rsk_set_tag_mode."""
+
+    def __init__(self, key: bytes = b"hello135", device: int = 0, tag_mode: str = "md5"):
         self.key = bytes(key)
         self.device = int(device)
         self._ctx = lib().rsk_create(self.key, len(self.key), self.device)
         if not self._ctx:
             raise RskError(f"rsk_create failed: {lib().rsk_last_error().decode()}")
+        self.set_tag_mode(tag_mode)
+
+    def set_tag_mode(self, mode) -> None:
+        """rsk_set_tag_mode: "md5" / "table" (or the RSK_TAG_* value; the A/B build also takes 2, the
+        MD5 with its round constants staged in LDS)."""
+        m = TAG_MODES[mode] if isinstance(mode, str) else int(mode)
+        _check(lib().rsk_set_tag_mode(self._ctx, m), "rsk_set_tag_mode")
+
+    @property
+    def tag_mode(self) -> str:
+        m = lib().rsk_get_tag_mode(self._ctx)
+        return {v: k for k, v in TAG_MODES.items()}.get(m, str(m))
 
     def close(self) -> None:
         if self._ctx:
@@ -272,6 +289,20 @@ class Codec:
         fn = lib().rsk__set_send_seq_groupby
         fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
         _check(fn(self._ctx, v), "rsk__set_send_seq_groupby")
+
+    def check_device_errors(self) -> int:
+        """rsk_check_device_errors: waits for the device, returns the sticky RSK_DEVERR_* flags (and
+        clears them); raises RskError when any is set (that call's compaction / demux outputs were
+        wrong; the look-back state is re-initialised at the next call)."""
+        f = ctypes.c_uint32(0)
+        rc = lib().rsk_check_device_errors(self._ctx, ctypes.byref(f))
+        if rc != 0:
+            raise RskError(f"device error flags 0x{f.value:x}: {lib().rsk_last_error().decode()}")
+        return f.value
+
+    def release_stream(self, stream=None) -> None:
+        """rsk_release_stream: wait for `stream` and free its scratch."""
+        _check(lib().rsk_release_stream(self._ctx, _stream(stream)), "rsk_release_stream")
 
     def reserve(self, n_max: int, stream=None) -> None:
         """Pre-size the compaction scratch of `stream` (default: torch's current stream)."""

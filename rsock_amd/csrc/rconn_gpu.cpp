@@ -36,7 +36,8 @@ RConnGpu::RConnGpu(const std::string &hash_key, int device, uint32_t batch) : de
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(device_);
-    ok_ = alloc_slots() == 0 && rsk_reserve(ctx_, batch_) == RSK_OK;
+    // no compaction scratch to reserve: decodes run on the slot streams without valid_idx / n_valid
+    ok_ = alloc_slots() == 0;
     (void)hipSetDevice(prev);
 }
 
@@ -187,8 +188,8 @@ int RConnGpu::deliver_enc(EncSlot &s) {
         const int st = s.h_status[i];
         char *f = reinterpret_cast<char *>(s.frame) + (size_t)i * kFramePitch;
         if (st > 0) std::memcpy(f, s.h_hdr + 32 * (size_t)i, RSK_HEAD_SIZE);  // tag | EncHead (RConn.cpp:101-103)
-        if (st > 0 && send_cb_) send_cb_(f, st, s.user[i]);
-        if (st == RSK_SEND_RESET && reset_cb_) reset_cb_(s.user[i]);
+        if (st > 0 && send_cb_ && send_cb_(f, st, s.user[i]) < 0) ++n_cb_fail_;
+        if (st == RSK_SEND_RESET && reset_cb_ && reset_cb_(s.user[i]) < 0) ++n_cb_fail_;
         ++n_sent_;
     }
     s.count = 0;
@@ -347,5 +348,7 @@ int rsk_rconn_onrecv(rsk_rconn *r, int64_t nread, const char *base, int tcp_clos
 }
 
 int rsk_rconn_flush(rsk_rconn *r) { return r ? r->impl.Flush() : RSK_EINVAL; }
+
+uint64_t rsk_rconn_callback_failures(const rsk_rconn *r) { return r ? r->impl.callback_failures() : 0; }
 
 }  // extern "C"

@@ -72,6 +72,10 @@ public:
     int Flush();
 
     uint64_t frames_sent() const { return n_sent_; }
+    // send / reset callbacks that returned < 0 since creation (RConn::Output returns the callee's
+    // result synchronously, RConn.cpp:108-123; here the callbacks run at delivery, so their failures
+    // are counted instead)
+    uint64_t callback_failures() const { return n_cb_fail_; }
     uint64_t frames_received() const { return n_recv_; }
 
 private:
@@ -134,7 +138,7 @@ private:
     SendFn send_cb_;
     ResetFn reset_cb_;
     RecvFn recv_cb_;
-    uint64_t n_sent_ = 0, n_recv_ = 0;
+    uint64_t n_sent_ = 0, n_recv_ = 0, n_cb_fail_ = 0;
 };
 
 }  // namespace rsk

@@ -41,6 +41,8 @@ struct rsk_ctx {
     // single-packet shim buffers
     ShimIO *shim_dev = nullptr;
     uint2 *tag_dev = nullptr;  // 256-entry tag table (rsk::KeySched::tab)
+    uint32_t *err_dev = nullptr;  // sticky device error flags (RSK_DEVERR_*, rsk_check_device_errors)
+    uint32_t compact_stall_tile = ~0u;  // see rsk__inject_compact_stall (tests)
     ShimIO *shim_host = nullptr;
     hipStream_t shim_stream = nullptr;
     std::mutex shim_mu;
@@ -82,12 +84,24 @@ struct DeviceGuard {
     }
 };
 
+// True when s is being captured into a graph (stream operations are recorded, not run).
+inline bool capturing(hipStream_t s) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
+
 // At least `need` bytes of `kind` scratch for stream s.  Growing waits for s to drain (the old
-// buffer may still be read by work queued on s) and then reallocates.
+// buffer may still be read by work queued on s) and then reallocates; neither can happen while s is
+// being captured (RSK_EINVAL: reserve before the capture, rsk_codec.h).
 inline int stream_ws(rsk_ctx *c, hipStream_t s, int kind, size_t need, void **out) {
     std::lock_guard<std::mutex> lk(c->ws_mu);
     WsBuf &b = c->ws[s][kind];
     if (!b.p || b.bytes < need) {
+        if (capturing(s)) {
+            snprintf(g_last_error, sizeof g_last_error,
+                     "scratch of a capturing stream must be reserved before the capture (rsk_reserve_stream)");
+            return RSK_EINVAL;
+        }
         if (b.p) {
             hipError_t e = hipStreamSynchronize(s);
             if (e != hipSuccess) { set_error("hipStreamSynchronize", e); return RSK_EDEVICE; }
@@ -114,12 +128,37 @@ inline int stream_compact(rsk_ctx *c, hipStream_t s, size_t words, unsigned long
     std::lock_guard<std::mutex> lk(c->ws_mu);
     WsBuf &b = c->ws[s][WS_COMPACT];
     if (!b.zeroed) {
+        if (capturing(s)) {  // a captured memset has not run yet: an eager call would read stale state
+            snprintf(g_last_error, sizeof g_last_error,
+                     "compaction state of a capturing stream must be initialised by an eager call first");
+            return RSK_EINVAL;
+        }
         hipError_t e = hipMemsetAsync(b.p, 0, b.bytes, s);
         if (e != hipSuccess) { set_error("hipMemsetAsync(compaction state)", e); return RSK_EDEVICE; }
         b.zeroed = true;
     }
     *out = reinterpret_cast<unsigned long long *>(p);
     *cap = b.bytes / sizeof(unsigned long long);
+    return RSK_OK;
+}
+
+// After a look-back timeout (RSK_DEVERR_LOOKBACK) a stalled tile may publish words under a later
+// call's epoch: every stream's compaction state is zeroed again at its next use.
+inline void invalidate_compact(rsk_ctx *c) {
+    std::lock_guard<std::mutex> lk(c->ws_mu);
+    for (auto &kv : c->ws) kv.second[WS_COMPACT].zeroed = false;
+}
+
+// Sync s, then free its scratch (rsk_release_stream).
+inline int release_ws(rsk_ctx *c, hipStream_t s) {
+    std::lock_guard<std::mutex> lk(c->ws_mu);
+    auto it = c->ws.find(s);
+    if (it == c->ws.end()) return RSK_OK;
+    hipError_t e = hipStreamSynchronize(s);
+    if (e != hipSuccess) { set_error("hipStreamSynchronize", e); return RSK_EDEVICE; }
+    for (WsBuf &b : it->second)
+        if (b.p) (void)hipFree(b.p);
+    c->ws.erase(it);
     return RSK_OK;
 }
 

@@ -150,7 +150,8 @@ struct DmIn {
 // the XCDs' L2s): the published words are the only data one block reads from another, so no
 // ordering is needed, and acquire / release at device scope would add an L2 invalidate / write-back
 // per access (first build: 0.56 ms for C4's flags pass instead of ~0.02).  A spin that outlives
-// kDlbSpinMax reads gives up (the batch result is then wrong, the GPU is not hung).
+// kDlbSpinMax reads gives up (the GPU is not hung): the batch result is then wrong, and the spin sets
+// RSK_DEVERR_LOOKBACK in the context's sticky error word (rsk_check_device_errors).
 constexpr unsigned long long kDlbEmpty = ~0ull;
 constexpr unsigned long long kDlbIncl = 1ull << 63;
 constexpr uint32_t kDlbSpinMax = 1u << 22;
@@ -158,13 +159,15 @@ constexpr uint32_t kDlbSpinMax = 1u << 22;
 __device__ __forceinline__ void dlb_publish(unsigned long long *s, unsigned long long v) {
     __hip_atomic_store(s, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ unsigned long long dlb_wait(unsigned long long *s) {
+__device__ __forceinline__ unsigned long long dlb_wait(unsigned long long *s, uint32_t *err) {
     unsigned long long v;
     uint32_t spins = 0;
     do {
         v = __hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } while (v == kDlbEmpty && ++spins < kDlbSpinMax);
-    return v == kDlbEmpty ? kDlbIncl : v;
+    if (v != kDlbEmpty) return v;
+    __hip_atomic_fetch_or(err, RSK_DEVERR_LOOKBACK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return kDlbIncl;
 }
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll
@@ -173,7 +176,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 }
 
 // Called by all 64 lanes of one wave of block b; agg uniform; returns b's exclusive prefix (uniform).
-__device__ uint32_t dlb_wave(unsigned long long *st, uint32_t b, uint32_t agg, uint32_t lane) {
+__device__ uint32_t dlb_wave(unsigned long long *st, uint32_t b, uint32_t agg, uint32_t lane, uint32_t *err) {
     if (b == 0u) {
         if (lane == 0u) dlb_publish(st, kDlbIncl | agg);
         return 0u;
@@ -182,7 +185,7 @@ __device__ uint32_t dlb_wave(unsigned long long *st, uint32_t b, uint32_t agg, u
     uint32_t excl = 0;
     for (int64_t top = (int64_t)b - 1;; top -= 64) {
         const int64_t j = top - (int64_t)lane;
-        const unsigned long long v = j >= 0 ? dlb_wait(st + j) : kDlbIncl;  // before block 0: inclusive 0
+        const unsigned long long v = j >= 0 ? dlb_wait(st + j, err) : kDlbIncl;  // before block 0: inclusive 0
         const uint64_t im = __ballot((v & kDlbIncl) != 0ull);
         uint32_t val = (uint32_t)v;
         if (im) {  // the nearest inclusive predecessor ends the walk
@@ -199,7 +202,7 @@ __device__ uint32_t dlb_wave(unsigned long long *st, uint32_t b, uint32_t agg, u
 // Per-digit look-back for the onesweep radix scatter: thread d of tile t publishes its digit count,
 // walks back over tiles until an inclusive word, publishes the inclusive count; returns the count
 // of digit d in tiles before t.
-__device__ uint32_t dlb_digit(unsigned long long *st, uint32_t t, uint32_t d, uint32_t cnt) {
+__device__ uint32_t dlb_digit(unsigned long long *st, uint32_t t, uint32_t d, uint32_t cnt, uint32_t *err) {
     if (t == 0u) {
         dlb_publish(st + d, kDlbIncl | cnt);
         return 0u;
@@ -220,7 +223,7 @@ __device__ uint32_t dlb_digit(unsigned long long *st, uint32_t t, uint32_t d, ui
 #pragma unroll
         for (int q = 0; q < kLb; ++q) {
             if (done) break;
-            if (v[q] == kDlbEmpty) v[q] = dlb_wait(st + (uint64_t)(j - q) * 256u + d);
+            if (v[q] == kDlbEmpty) v[q] = dlb_wait(st + (uint64_t)(j - q) * 256u + d, err);
             excl += (uint32_t)v[q];
             done = (v[q] & kDlbIncl) != 0ull;
         }
@@ -445,7 +448,7 @@ __device__ __forceinline__ void tile_offsets(const uint64_t (*m)[kWaves], uint32
 // writes n_valid.
 __global__ __launch_bounds__(kBlock) void k_dm_flags_prep(DmIn a, unsigned long long *st_v,
                                                           unsigned long long *st_c, uint32_t *cidx, uint32_t *cep,
-                                                          uint32_t *nvp) {
+                                                          uint32_t *nvp, uint32_t *err) {
     __shared__ uint64_t mv[kRows][kWaves], mc[kRows][kWaves];
     __shared__ uint32_t pre[2];
     const uint32_t b = blockIdx.x, t = threadIdx.x, w = t >> 6, lane = t & 63u;
@@ -475,13 +478,13 @@ __global__ __launch_bounds__(kBlock) void k_dm_flags_prep(DmIn a, unsigned long 
     tile_offsets(mv, w, ov, av);
     tile_offsets(mc, w, oc, ac);
     if (w == 0u) {
-        const uint32_t e = dlb_wave(st_v, b, av, lane);
+        const uint32_t e = dlb_wave(st_v, b, av, lane, err);
         if (lane == 0u) {
             pre[0] = e;
             if (b == gridDim.x - 1u) *nvp = e + av;
         }
     } else if (w == 1u) {
-        const uint32_t e = dlb_wave(st_c, b, ac, lane);
+        const uint32_t e = dlb_wave(st_c, b, ac, lane, err);
         if (lane == 0u) pre[1] = e;
     }
     __syncthreads();
@@ -506,7 +509,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_leader_rank(const uint32_t *nvp, 
                                                            const unsigned long long *slots, const uint32_t *cidx,
                                                            unsigned long long *st_l, uint32_t *fkey, uint32_t *fval,
                                                            uint32_t *rank_at, uint32_t *seg_first, uint32_t *nsegp,
-                                                           uint32_t *ghist) {
+                                                           uint32_t *ghist, uint32_t *err) {
     __shared__ uint64_t ml[kRows][kWaves];
     __shared__ uint32_t pre;
     const uint32_t nv = *nvp;
@@ -537,7 +540,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_leader_rank(const uint32_t *nvp, 
     uint32_t ol[kRows], al;
     tile_offsets(ml, w, ol, al);
     if (w == 0u) {
-        const uint32_t e = dlb_wave(st_l, b, al, lane);
+        const uint32_t e = dlb_wave(st_l, b, al, lane, err);
         if (lane == 0u) {
             pre = e;
             if (b == gridDim.x - 1u) *nsegp = e + al;
@@ -651,7 +654,8 @@ __global__ __launch_bounds__(kBlock) void k_dm_segof_hist(const uint32_t *nvp, c
 // out digit run by digit run (consecutive threads, consecutive addresses).
 __global__ __launch_bounds__(kBlock) void k_dm_onesweep(uint32_t pass, const uint32_t *nvp, const uint32_t *nsegp,
                                                         const uint32_t *kin, const uint32_t *vin, const uint32_t *ghist,
-                                                        unsigned long long *st, uint32_t *kout, uint32_t *vout) {
+                                                        unsigned long long *st, uint32_t *kout, uint32_t *vout,
+                                                        uint32_t *err) {
     __shared__ uint32_t run[256], lbase[256], dbase[256];
     __shared__ uint32_t wcnt[kWaves][256];
     __shared__ uint32_t sk[kTile], sv[kTile];
@@ -681,7 +685,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_onesweep(uint32_t pass, const uin
     }
     __syncthreads();
     // global position of this tile's first digit-t item: digits before t overall + digit t before this tile
-    const uint32_t before = dlb_digit(st + (uint64_t)pass * 256u * gridDim.x, tile, t, run[t]);
+    const uint32_t before = dlb_digit(st + (uint64_t)pass * 256u * gridDim.x, tile, t, run[t], err);
     if (w == 0) {  // exclusive scans of the global histogram and of the tile's bins (4 per lane)
         uint32_t g[4], c[4], gs = 0, cs = 0;
 #pragma unroll
@@ -871,11 +875,12 @@ extern "C" int rsk_demux_batch(rsk_ctx *c, uint32_t n, const rsk_demux_in *in, u
     hipError_t e = hipMemsetAsync(w.slots, 0xff, w.fill_bytes, s);
     if (e != hipSuccess) { rsk::set_error("hipMemsetAsync(table)", e); return RSK_EDEVICE; }
     const uint32_t nb = w.nb;
-    hipLaunchKernelGGL(k_dm_flags_prep, dim3(w.nt), dim3(kBlock), 0, s, a, w.st_v, w.st_c, w.cidx, w.cep, w.nv);
+    hipLaunchKernelGGL(k_dm_flags_prep, dim3(w.nt), dim3(kBlock), 0, s, a, w.st_v, w.st_c, w.cidx, w.cep, w.nv,
+                       c->err_dev);
     hipLaunchKernelGGL(k_dm_insert, dim3((n + kInsTile - 1) / kInsTile), dim3(kBlock), 0, s, a, w.nv, w.cidx,
                        w.cep, w.slots, w.tsize - 1u, w.hslot);
     hipLaunchKernelGGL(k_dm_leader_rank, dim3(w.nt), dim3(kBlock), 0, s, w.nv, w.hslot, w.slots, w.cidx, w.st_l,
-                       w.kA, w.vA, w.rank_at, out->seg_first, w.nseg, w.ghist);
+                       w.kA, w.vA, w.rank_at, out->seg_first, w.nseg, w.ghist, c->err_dev);
     hipLaunchKernelGGL(k_dm_segof_hist, dim3(w.nt), dim3(kBlock), 0, s, w.nv, w.nseg, w.rank_at, w.kA, w.vA,
                        w.ghist);
     if ((r = rsk::launch_check("k_dm_segof_hist"))) return r;
@@ -887,7 +892,7 @@ extern "C" int rsk_demux_batch(rsk_ctx *c, uint32_t n, const rsk_demux_in *in, u
         const uint32_t *kin = (p & 1u) ? w.kB : w.kA, *vin = (p & 1u) ? w.vB : w.vA;
         uint32_t *kout = (p & 1u) ? w.kA : w.kB, *vout = (p & 1u) ? w.vA : w.vB;
         hipLaunchKernelGGL(k_dm_onesweep, dim3(w.nt), dim3(kBlock), 0, s, p, w.nv, w.nseg, kin, vin, w.ghist, w.st_r,
-                           kout, vout);
+                           kout, vout, c->err_dev);
         if ((r = rsk::launch_check("k_dm_onesweep"))) return r;
     }
     hipLaunchKernelGGL(k_dm_final, dim3(nb), dim3(kBlock), 0, s, w.nv, w.nseg, w.kA, w.vA, w.kB, w.vB,

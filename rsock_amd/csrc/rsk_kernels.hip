@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cassert>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -75,34 +76,56 @@ __device__ __forceinline__ uint64_t rdl64(uint64_t v, uint32_t j) {
     return (uint64_t)rdl((uint32_t)v, j) | ((uint64_t)rdl((uint32_t)(v >> 32), j) << 32);
 }
 
-// ---- the tag (util/rhash.cpp:20-41): MD5(key || payload[0]) depends on one payload byte, so a key
-// has 256 possible tags.  k_tag_table computes them once per context with the MD5 compression of
-// rsk_md5.h; every kernel that frames or verifies stages the 2-KB table into LDS (one entry per
-// thread of the 256-thread block, before any early exit) and looks the tag up with one ds_read_b64.
-// RSK_TAG_INLINE (A/B build only) computes the MD5 per lane instead.
-#ifndef RSK_TAG_INLINE
+// ---- the tag (util/rhash.cpp:20-41): MD5(key || payload[0])[8..15].  Two modes, chosen per context
+// at run time (rsk_set_tag_mode, uniform per launch through KeySched::tag_mode):
+//   RSK_TAG_MD5 (default)  every lane runs the MD5 compression of rsk_md5.h for its packet, as the
+//                          reference does per packet (rhash.cpp:20-41): the key's message words are
+//                          kernel arguments (SGPRs), only the word holding payload[0] is per lane, the
+//                          round constants are instruction immediates;
+//   RSK_TAG_TABLE          the tag depends on one payload byte, so a key has 256 tags: k_tag_table
+//                          computes them once per context and every kernel that frames or verifies
+//                          stages the 2-KB table in LDS (one entry per thread of the 256-thread block,
+//                          before any early exit) and looks the tag up with one ds_read_b64.
+// A/B build only: RSK_TAG_MD5_LDS (2) = RSK_TAG_MD5 with the 64 round constants read from an LDS copy
+// staged per block (the north star's layout) instead of immediates.
 __shared__ uint2 s_tags[256];
+#ifdef RSK_AB
+__shared__ uint32_t s_md5k[64];
+struct KLds {
+    template <int I>
+    __device__ __forceinline__ uint32_t get() const { return s_md5k[I]; }
+};
+constexpr int kTagMd5Lds = 2;
 #endif
 
 __device__ __forceinline__ void stage_tags(const KeySched &ks) {
     static_assert(kBlock == 256, "one tag-table entry per thread");
-#ifndef RSK_TAG_INLINE
-    s_tags[threadIdx.x] = ks.tab[threadIdx.x];
-    __syncthreads();
-#else
-    (void)ks;
+    if (ks.tag_mode == RSK_TAG_TABLE) {  // uniform: the whole block takes the barrier or none does
+        s_tags[threadIdx.x] = ks.tab[threadIdx.x];
+        __syncthreads();
+    }
+#ifdef RSK_AB
+    if (ks.tag_mode == kTagMd5Lds) {
+        if (threadIdx.x < 64u) s_md5k[threadIdx.x] = rsk::Md5Consts::K[threadIdx.x];
+        __syncthreads();
+    }
 #endif
 }
 
 __device__ __forceinline__ void tag_of(const KeySched &ks, uint32_t b, uint32_t &t0, uint32_t &t1) {
-#ifndef RSK_TAG_INLINE
-    (void)ks;
-    const uint2 t = s_tags[b & 255u];
-    t0 = t.x;
-    t1 = t.y;
-#else
-    rsk::md5_tag(ks, b, t0, t1);
+    if (ks.tag_mode == RSK_TAG_TABLE) {
+        const uint2 t = s_tags[b & 255u];
+        t0 = t.x;
+        t1 = t.y;
+        return;
+    }
+#ifdef RSK_AB
+    if (ks.tag_mode == kTagMd5Lds) {
+        rsk::md5_tag(ks, b & 255u, t0, t1, KLds());
+        return;
+    }
 #endif
+    rsk::md5_tag(ks, b & 255u, t0, t1);
 }
 
 // Frame bytes 8..31 as words H[2..7] (bean/EncHead.cpp:9-24 field order; byte 30 reserved = 0,
@@ -845,59 +868,6 @@ __global__ __launch_bounds__(kBlock) void k_encode(EncArgs a, KeySched ks) {
     encode_set<MODE, PU, U, NT, GRP>(a, ks, i < a.n ? i : a.n, lane, recs[w], cend[w]);
 }
 
-#ifdef RSK_AB
-// A/B build only: the mapping chosen on the device per launch.  Every block reads the same sample
-// (pay_len of the first 256 packets) beside its tag-table stage and takes the same decision: mean
-// payload >= LONGP bytes -> 8 packets per wave (tiled, the grid's every block); otherwise the
-// grouped interleave <8, 1024> over the first grid / 8 blocks, the rest exit.  The grid is sized for
-// the 8-packet mapping.
-template <int MODE, int PU, int U, int NT, uint32_t LONGP>
-__global__ __launch_bounds__(kBlock) void k_encode_ad(EncArgs a, KeySched ks) {
-    __shared__ CopyRec recs[kWavesPerBlock][64];
-    __shared__ uint32_t cend[kWavesPerBlock][64];
-    __shared__ uint32_t wsum[kWavesPerBlock];
-    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    uint32_t p = threadIdx.x < a.n ? a.pay_len[threadIdx.x] : 0u;
-#pragma unroll
-    for (int off = 32; off; off >>= 1) p += __shfl_xor(p, off);
-    if (lane == 0u) wsum[w] = p;
-    stage_tags(ks);  // its barrier publishes wsum too
-    const uint32_t cnt = a.n < (uint32_t)kBlock ? a.n : (uint32_t)kBlock;
-    const bool lng = wsum[0] + wsum[1] + wsum[2] + wsum[3] >= LONGP * cnt;
-    const uint64_t wg = (uint64_t)blockIdx.x * kWavesPerBlock + w;
-    if (lng) {
-        const uint64_t base = wg * 8u;
-        if (base >= a.n) return;
-        EncArgs b = a;
-        b.n = (uint32_t)(base + 8u < a.n ? base + 8u : a.n);
-        encode_set<MODE, PU, U, NT>(b, ks, lane < 8u ? base + lane : b.n, lane, recs[w], cend[w]);
-        return;
-    }
-    const uint64_t sb = wg / 1024u, wl = wg % 1024u;
-    const uint64_t first = sb * 1024u * 64u + wl * 8u;
-    if (first >= a.n) return;
-    const uint64_t i = sb * 1024u * 64u + ((uint64_t)(lane / 8u) * 1024u + wl) * 8u + lane % 8u;
-    encode_set<MODE, PU, U, NT, 8>(a, ks, i < a.n ? i : a.n, lane, recs[w], cend[w]);
-}
-
-// A/B build only: persistent form of the SET mapping — the grid holds only resident blocks and each
-// wave strides over SET-packet sets (set w, w + W, ...), so the tag table is staged once per block
-// and the resident waves still sweep the arenas as one compact window.
-template <int MODE, int PU, int U, int NT, int SET>
-__global__ __launch_bounds__(kBlock) void k_encode_gs(EncArgs a, KeySched ks) {
-    __shared__ CopyRec recs[kWavesPerBlock][64];
-    __shared__ uint32_t cend[kWavesPerBlock][64];
-    stage_tags(ks);
-    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    const uint64_t nsets = ((uint64_t)a.n + SET - 1) / SET, stride = (uint64_t)gridDim.x * kWavesPerBlock;
-    for (uint64_t sidx = (uint64_t)blockIdx.x * kWavesPerBlock + w; sidx < nsets; sidx += stride) {
-        const uint64_t base = sidx * SET;
-        EncArgs b = a;
-        b.n = (uint32_t)(base + SET < a.n ? base + SET : a.n);
-        encode_set<MODE, PU, U, NT>(b, ks, lane < (uint32_t)SET ? base + lane : b.n, lane, recs[w], cend[w]);
-    }
-}
-#endif
 
 // ---------------------------------------------------------------------------------------------
 // Encode straight to wire packets (RConn::Output + RawTcp::SendRawTcp / libnet)
@@ -1912,23 +1882,28 @@ __device__ __forceinline__ void store_dec(const DecOut &d, uint64_t i, const Dec
 // read the same value; the next call on the stream, or the next replay of a captured graph, sees
 // the next epoch.  Epochs run 1 .. 2^31 - 1 (0 is the zeroed state).  Device-scope relaxed
 // atomics (acquire / release would add an L2 write-back / invalidate per access, rsk_demux.hip);
-// a spin that outlives kCmpSpinMax reads gives up (wrong list, no hang).  Round 1 used k_scan (one
+// a spin that outlives kCmpSpinMax reads gives up (no hang): it sets RSK_DEVERR_LOOKBACK in the
+// context's sticky error word and the tile poisons n_valid (rsk_check_device_errors).  Round 1 used k_scan (one
 // workgroup) + k_scatter; a look-back inside the decode launch itself (one word per 256-packet
 // block) was measured slower than both (C2: 40 us vs 31): the block-granular chain is the cost.
 constexpr unsigned long long kCmpIncl = 1ull << 32;
 constexpr uint32_t kCmpSpinMax = 1u << 22;
 
-__device__ __forceinline__ unsigned long long cmp_wait(unsigned long long *s, uint32_t epoch) {
+__device__ __forceinline__ unsigned long long cmp_wait(unsigned long long *s, uint32_t epoch, bool &timed_out) {
     unsigned long long v;
     uint32_t spins = 0;
     do {
         v = __hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } while ((uint32_t)(v >> 33) != epoch && ++spins < kCmpSpinMax);
-    return (uint32_t)(v >> 33) == epoch ? v : kCmpIncl;
+    if ((uint32_t)(v >> 33) == epoch) return v;
+    timed_out = true;
+    return kCmpIncl;
 }
 
-// all 64 lanes of one wave of tile b; agg uniform; returns b's exclusive prefix (uniform)
-__device__ uint32_t cmp_lookback(unsigned long long *st, uint32_t b, uint32_t agg, uint32_t lane, uint32_t epoch) {
+// all 64 lanes of one wave of tile b; agg uniform; returns b's exclusive prefix (uniform); `to`
+// (uniform) is set when a predecessor's word never arrived
+__device__ uint32_t cmp_lookback(unsigned long long *st, uint32_t b, uint32_t agg, uint32_t lane, uint32_t epoch,
+                                 bool &to) {
     const unsigned long long tag = (unsigned long long)epoch << 33;
     if (b == 0u) {
         if (lane == 0u) __hip_atomic_store(st, tag | kCmpIncl | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1938,7 +1913,9 @@ __device__ uint32_t cmp_lookback(unsigned long long *st, uint32_t b, uint32_t ag
     uint32_t excl = 0;
     for (int64_t top = (int64_t)b - 1;; top -= 64) {
         const int64_t j = top - (int64_t)lane;
-        const unsigned long long v = j >= 0 ? cmp_wait(st + j, epoch) : kCmpIncl;  // before tile 0: 0
+        bool lto = false;
+        const unsigned long long v = j >= 0 ? cmp_wait(st + j, epoch, lto) : kCmpIncl;  // before tile 0: 0
+        if (__ballot(lto)) to = true;
         const uint64_t im = __ballot((v & kCmpIncl) != 0ull);
         uint32_t val = (uint32_t)v;
         if (im && lane > (uint32_t)__builtin_ctzll(im)) val = 0u;  // beyond the nearest inclusive word
@@ -2391,7 +2368,8 @@ __global__ __launch_bounds__(kBlock) void k_filter_parse_decode(ParseArgs a, Dec
 
 // st[0]: the epoch counter; st[1 + t]: tile t's look-back word
 __global__ __launch_bounds__(kBlock) void k_compact(const uint64_t *masks, uint32_t nw, unsigned long long *st,
-                                                    uint32_t *valid_idx, uint32_t *n_valid) {
+                                                    uint32_t *valid_idx, uint32_t *n_valid, uint32_t *err,
+                                                    uint32_t stall_tile) {
     __shared__ uint64_t ms[64];
     __shared__ uint32_t mex[64];
     __shared__ uint32_t pre;
@@ -2411,12 +2389,19 @@ __global__ __launch_bounds__(kBlock) void k_compact(const uint64_t *masks, uint3
         ms[lane] = m;
         mex[lane] = inc - c;
         const uint32_t agg = (uint32_t)__shfl((int)inc, 63);
-        const uint32_t p = cmp_lookback(st + 1, blockIdx.x, agg, lane, epoch);
+        bool to = false;
+        // stall_tile (tests only, rsk__inject_compact_stall): that tile publishes nothing, as a tile
+        // that never gets scheduled would; the others must time out, flag it and not hang
+        const uint32_t p = blockIdx.x == stall_tile ? 0u : cmp_lookback(st + 1, blockIdx.x, agg, lane, epoch, to);
         if (lane == 0u) {
             pre = p;
             if (blockIdx.x == gridDim.x - 1u) {  // every tile has read the epoch (see above)
                 if (n_valid) *n_valid = p + agg;
                 __hip_atomic_store(st, (unsigned long long)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (to) {  // wrong prefix: flag it (sticky) and poison the count
+                __hip_atomic_fetch_or(err, RSK_DEVERR_LOOKBACK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (n_valid) __hip_atomic_store(n_valid, 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
     }
@@ -2601,6 +2586,7 @@ void build_sched(const uint8_t *key, uint32_t klen, KeySched &ks) {
     if (two) {
         words(tail + 64, m);
         std::memcpy(ks.pad, m, sizeof m);
+        for (int w = 1; w < 14; ++w) assert(ks.pad[w] == 0u);  // rsk::md5_tag reads words 0, 14, 15 only
     }
     ks.bword = (int32_t)(rem / 4u);
     ks.bshift = (int32_t)(8u * (rem % 4u));
@@ -2638,8 +2624,11 @@ int ensure_compact(rsk_ctx *c, uint32_t n, hipStream_t s, Compact &k) {
     return RSK_OK;
 }
 
-int run_compaction(const Compact &k, uint32_t *valid_idx, uint32_t *n_valid, hipStream_t s) {
-    hipLaunchKernelGGL(k_compact, dim3(k.ntiles), dim3(kBlock), 0, s, k.masks, k.nw, k.st, valid_idx, n_valid);
+int run_compaction(rsk_ctx *c, const Compact &k, uint32_t *valid_idx, uint32_t *n_valid, hipStream_t s) {
+    const uint32_t stall = c->compact_stall_tile;
+    c->compact_stall_tile = ~0u;
+    hipLaunchKernelGGL(k_compact, dim3(k.ntiles), dim3(kBlock), 0, s, k.masks, k.nw, k.st, valid_idx, n_valid,
+                       c->err_dev, stall);
     return launch_check("k_compact");
 }
 
@@ -2699,40 +2688,24 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 #ifdef RSK_AB
 // A/B build only: selects the encode kernel variant for in-process A/B runs (tools/ab_encode.py).
 // 0 = the shipped k_encode<11, 4, 4, -1, 8, 1024> (grouped interleave; software-pipelined per-packet
-// copy, 4 packets per batch; flat sets' tag behind the first chunk loads).  The others are the tiled
-// mapping k_encode_tiled<MODE, PU, U, NT> (see encode_set) unless named: 37 = the tiled form of 0, 22 = the same
-// with the flat sets' tag in phase 1 (<9, 4, 4, -1>); 17 = round 2's first form <6, 12, 4, -1> (12 packets per
-// iteration, no pipelining); 1 = as 17 with the tag always in phase 1; 2 / 3 = 17 with 8 / 16
-// packets per iteration; 4 = 2 chunks per lane per flat iteration; 5 / 6 = normal / nontemporal
-// stores on every per-packet set; 7 = flat path only; 8 = per-packet path only (unpipelined);
-// 9 / 10 / 14 / 15 / 16 = pipelined with 6 / 8 / 3 / 5 / 2 packets per batch (11 = 4);
-// 12 / 13 = k_copy_probe (memory-side ceiling probe, wrong bytes) with 12 / 4 packets per batch;
-// 18 = shipped with the tag in the copy loop for every per-packet set; 19 / 20 / 21 = shipped with
-// the flat sets' tag behind the first chunk loads, 4 / 2 / 8 chunk rows per flat iteration;
-// 23 / 24 / 25 / 26 = shipped with 32 / 16 / 8 / 4 packets per wave (smaller region per wave);
-// 27 / 28 / 29 / 30 = persistent k_encode_gs: SET 16 on 1024 blocks / 8 on 1024 / 16 on 2048 / 32 on 1024;
-// 31 / 32 / 33 / 34 = grouped interleave k_encode_gi <GRP, SBW> = <8, 1024> / <8, 4096> / <16, 1024> / <4, 1024>;
-// 35 / 36 = k_encode_ad (mapping chosen on the device from a pay_len sample), long at >= 1024 / 512 B;
-// 37 = the tiled mapping with the shipped copy (the form shipped before the grouped interleave);
-// 38 / 39 / 40 / 41 / 42 = grouped interleave <GRP, SBW> = <8,256> / <8,512> / <8,2048> / <16,512> / <32,256>;
-// 43 = 0 with the tag in the copy loop for every per-packet set (MODE 10); 44 / 45 / 46 = 0 with
-// 3 / 5 / 2 packets per pipelined batch; 47 / 48 = the unpipelined copy (MODE 6), 8 / 12 packets.
+// copy, 4 packets per batch; flat sets' tag behind the first chunk loads); 12 / 13 = k_copy_probe
+// (memory-side ceiling probe, wrong bytes) with 12 / 4 packets per batch; 37 = the tiled mapping
+// with the shipped copy; 47 = the unpipelined copy (MODE 6), 8 packets per iteration.  Rounds 1-2
+// measured ~45 more variants (profiles/r01_ab_*, r02_ab_*); their code is in the git history.
 // v + 100 * cap (cap 1..4): the same kernel held to `cap` blocks per CU by unused LDS.
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
-    if (!c || v < 0 || v % 100 > 48 || v / 100 > 4) return RSK_EINVAL;
+    const int k = v % 100;
+    if (!c || v < 0 || v / 100 > 4 || !(k == 0 || k == 12 || k == 13 || k == 37 || k == 47)) return RSK_EINVAL;
     c->enc_variant = v;
     return RSK_OK;
 }
 
 // Internal (A/B and tests): wire-build copy path.  0 = two-launch hybrid whose per-packet half uses the
 // one-load DPP copy, 8 packets per iteration, tag + payload prefix in the copy loop for sets of long
-// frames (default), 1 = per-packet, 2 = flat, 3 = one-launch hybrid, 4 = two-launch hybrid with the
-// two-load copy PU=2, 5 = the same PU=4, 6 / 7 = DPP copy PU=4 / 16, 8 = 0 with the tag in phase 1,
-// 9 = 0 without the 4-waves-per-SIMD bound, 10 = 0 on the tiled mapping (64 consecutive packets per
-// wave; variants 1-9 use the grouped interleave like 0), 11 / 12 = 0 with the software-pipelined copy,
-// 4 / 3 packets per batch, 13 = 11 without the 4-waves-per-SIMD bound.
+// frames (default), 8 = 0 with the tag in phase 1, 10 = 0 on the tiled mapping (64 consecutive
+// packets per wave).  Rounds 1-2's other variants: profiles/r0*_ab_wire_*, code in the git history.
 int rsk__set_wire_variant(rsk_ctx *c, int v) {
-    if (!c || v < 0 || v > 13) return RSK_EINVAL;
+    if (!c || !(v == 0 || v == 8 || v == 10)) return RSK_EINVAL;
     c->wire_variant = v;
     return RSK_OK;
 }
@@ -2757,6 +2730,8 @@ rsk_ctx *rsk_create(const uint8_t *key, uint32_t key_len, int device) {
     DeviceGuard g(device);
     hipStream_t s = nullptr;
     e = g.ok ? hipMalloc(&c->tag_dev, 256 * sizeof(uint2)) : hipErrorInvalidDevice;
+    if (e == hipSuccess) e = hipMalloc(&c->err_dev, sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemset(c->err_dev, 0, sizeof(uint32_t));
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
     if (e == hipSuccess) {
         hipLaunchKernelGGL(k_tag_table, dim3(1), dim3(256), 0, s, c->ks, c->tag_dev);
@@ -2767,6 +2742,7 @@ rsk_ctx *rsk_create(const uint8_t *key, uint32_t key_len, int device) {
     if (e != hipSuccess) {
         set_error("rsk_create: tag table", e);
         if (c->tag_dev) (void)hipFree(c->tag_dev);
+        if (c->err_dev) (void)hipFree(c->err_dev);
         delete c;
         return nullptr;
     }
@@ -2774,18 +2750,64 @@ rsk_ctx *rsk_create(const uint8_t *key, uint32_t key_len, int device) {
     return c;
 }
 
+int rsk_set_tag_mode(rsk_ctx *c, int mode) {
+    if (!c) return RSK_EINVAL;
+#ifdef RSK_AB
+    const int max_mode = kTagMd5Lds;
+#else
+    const int max_mode = RSK_TAG_TABLE;
+#endif
+    if (mode < RSK_TAG_MD5 || mode > max_mode) return RSK_EINVAL;
+    c->ks.tag_mode = mode;
+    return RSK_OK;
+}
+
+int rsk_get_tag_mode(const rsk_ctx *c) { return c ? c->ks.tag_mode : RSK_EINVAL; }
+
 void rsk_destroy(rsk_ctx *c) {
     if (!c) return;
     DeviceGuard g(c->device);
     rsk::free_ws(c);
     if (c->shim_dev) (void)hipFree(c->shim_dev);
     if (c->tag_dev) (void)hipFree(c->tag_dev);
+    if (c->err_dev) (void)hipFree(c->err_dev);
     if (c->shim_host) (void)hipHostFree(c->shim_host);
     if (c->shim_stream) (void)hipStreamDestroy(c->shim_stream);
     delete c;
 }
 
 int rsk_reserve(rsk_ctx *c, uint32_t n_max) { return rsk_reserve_stream(c, n_max, nullptr); }
+
+int rsk_release_stream(rsk_ctx *c, void *stream) {
+    if (!c) return RSK_EINVAL;
+    DeviceGuard g(c->device);
+    if (!g.ok) return RSK_EDEVICE;
+    return rsk::release_ws(c, (hipStream_t)stream);
+}
+
+// Internal (tests): the next compaction launch of this context runs with tile `tile` publishing
+// nothing (a stalled tile), to exercise the look-back timeout, the sticky flag and the recovery.
+int rsk__inject_compact_stall(rsk_ctx *c, uint32_t tile) {
+    if (!c) return RSK_EINVAL;
+    c->compact_stall_tile = tile;
+    return RSK_OK;
+}
+
+int rsk_check_device_errors(rsk_ctx *c, uint32_t *flags) {
+    if (!c) return RSK_EINVAL;
+    DeviceGuard g(c->device);
+    if (!g.ok) return RSK_EDEVICE;
+    uint32_t f = 0;
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(&f, c->err_dev, sizeof f, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && f) e = hipMemset(c->err_dev, 0, sizeof f);
+    if (e != hipSuccess) { set_error("rsk_check_device_errors", e); return RSK_EDEVICE; }
+    if (flags) *flags = f;
+    if (!f) return RSK_OK;
+    rsk::invalidate_compact(c);
+    snprintf(g_last_error, sizeof g_last_error, "device error flags 0x%x (RSK_DEVERR_LOOKBACK: a look-back gave up)", f);
+    return RSK_EDEVICE;
+}
 
 int rsk_reserve_stream(rsk_ctx *c, uint32_t n_max, void *stream) {
     if (!c) return RSK_EINVAL;
@@ -2823,54 +2845,10 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
     const int cap = c->enc_variant / 100;
     const size_t lds = cap ? (size_t)(163840 / cap) - 16384 : 0;
     switch (c->enc_variant % 100) {
-        case 1: hipLaunchKernelGGL((k_encode_tiled<3, 12, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 2: hipLaunchKernelGGL((k_encode_tiled<6, 8, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 3: hipLaunchKernelGGL((k_encode_tiled<6, 16, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 4: hipLaunchKernelGGL((k_encode_tiled<6, 12, 2, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 5: hipLaunchKernelGGL((k_encode_tiled<6, 12, 4, 0>), gd, bd, lds, st, a, c->ks); break;
-        case 6: hipLaunchKernelGGL((k_encode_tiled<6, 12, 4, 2>), gd, bd, lds, st, a, c->ks); break;
-        case 7: hipLaunchKernelGGL((k_encode_tiled<7, 12, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 8: hipLaunchKernelGGL((k_encode_tiled<8, 12, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 9: hipLaunchKernelGGL((k_encode_tiled<9, 6, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 10: hipLaunchKernelGGL((k_encode_tiled<9, 8, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 11: hipLaunchKernelGGL((k_encode_tiled<9, 4, 4, -1>), gd, bd, lds, st, a, c->ks); break;
         case 12: hipLaunchKernelGGL((k_copy_probe<12>), gd, bd, lds, st, a); break;
         case 13: hipLaunchKernelGGL((k_copy_probe<4>), gd, bd, lds, st, a); break;
-        case 14: hipLaunchKernelGGL((k_encode_tiled<9, 3, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 15: hipLaunchKernelGGL((k_encode_tiled<9, 5, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 16: hipLaunchKernelGGL((k_encode_tiled<9, 2, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 17: hipLaunchKernelGGL((k_encode_tiled<6, 12, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 18: hipLaunchKernelGGL((k_encode_tiled<10, 4, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 19: hipLaunchKernelGGL((k_encode_tiled<11, 4, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 20: hipLaunchKernelGGL((k_encode_tiled<11, 4, 2, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 21: hipLaunchKernelGGL((k_encode_tiled<11, 4, 8, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 22: hipLaunchKernelGGL((k_encode_tiled<9, 4, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 23: hipLaunchKernelGGL((k_encode_tiled<11, 4, 4, -1, 32>), dim3(grid * 2), bd, lds, st, a, c->ks); break;
-        case 24: hipLaunchKernelGGL((k_encode_tiled<11, 4, 4, -1, 16>), dim3(grid * 4), bd, lds, st, a, c->ks); break;
-        case 25: hipLaunchKernelGGL((k_encode_tiled<11, 4, 4, -1, 8>), dim3(grid * 8), bd, lds, st, a, c->ks); break;
-        case 26: hipLaunchKernelGGL((k_encode_tiled<11, 4, 4, -1, 4>), dim3(grid * 16), bd, lds, st, a, c->ks); break;
-        case 27: hipLaunchKernelGGL((k_encode_gs<11, 4, 4, -1, 16>), dim3(std::min(grid * 4u, 1024u)), bd, lds, st, a, c->ks); break;
-        case 28: hipLaunchKernelGGL((k_encode_gs<11, 4, 4, -1, 8>), dim3(std::min(grid * 8u, 1024u)), bd, lds, st, a, c->ks); break;
-        case 29: hipLaunchKernelGGL((k_encode_gs<11, 4, 4, -1, 16>), dim3(std::min(grid * 4u, 2048u)), bd, lds, st, a, c->ks); break;
-        case 30: hipLaunchKernelGGL((k_encode_gs<11, 4, 4, -1, 32>), dim3(std::min(grid * 2u, 1024u)), bd, lds, st, a, c->ks); break;
-        case 31: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-        case 32: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 4096>), dim3(enc_grid(n, 8, 4096)), bd, lds, st, a, c->ks); break;
-        case 33: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 16, 1024>), dim3(enc_grid(n, 16, 1024)), bd, lds, st, a, c->ks); break;
-        case 34: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 4, 1024>), dim3(enc_grid(n, 4, 1024)), bd, lds, st, a, c->ks); break;
-        case 35: hipLaunchKernelGGL((k_encode_ad<11, 4, 4, -1, 1024>), dim3(std::max(grid * 8u, (grid + 255u) / 256u * 256u)), bd, lds, st, a, c->ks); break;
-        case 36: hipLaunchKernelGGL((k_encode_ad<11, 4, 4, -1, 512>), dim3(std::max(grid * 8u, (grid + 255u) / 256u * 256u)), bd, lds, st, a, c->ks); break;
         case 37: hipLaunchKernelGGL((k_encode_tiled<11, 4, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 38: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 256>), dim3(enc_grid(n, 8, 256)), bd, lds, st, a, c->ks); break;
-        case 39: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 512>), dim3(enc_grid(n, 8, 512)), bd, lds, st, a, c->ks); break;
-        case 40: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 2048>), dim3(enc_grid(n, 8, 2048)), bd, lds, st, a, c->ks); break;
-        case 41: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 16, 512>), dim3(enc_grid(n, 16, 512)), bd, lds, st, a, c->ks); break;
-        case 42: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 32, 256>), dim3(enc_grid(n, 32, 256)), bd, lds, st, a, c->ks); break;
-        case 43: hipLaunchKernelGGL((k_encode<10, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-        case 44: hipLaunchKernelGGL((k_encode<11, 3, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-        case 45: hipLaunchKernelGGL((k_encode<11, 5, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-        case 46: hipLaunchKernelGGL((k_encode<11, 2, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
         case 47: hipLaunchKernelGGL((k_encode<6, 8, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-        case 48: hipLaunchKernelGGL((k_encode<6, 12, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
         default: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
     }
 #else
@@ -2918,34 +2896,12 @@ int rsk_encode_wire_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const
 #define RSK_WIRE4T(E, M, PU, U) hipLaunchKernelGGL((k_encode_wire_w4<E, M, PU, U, false>), dim3(tgrid), dim3(kBlock), 0, st, a, w, c->ks)
     const int v = c->wire_variant;
     if (wire->with_eth) {
-        if (v == 1) RSK_WIRE(14, 0, 2, 4);
-        else if (v == 2) RSK_WIRE(14, 1, 2, 2);
-        else if (v == 3) RSK_WIRE(14, 2, 2, 2);
-        else if (v == 4) { RSK_WIRE(14, 3, 2, 2); RSK_WIRE(14, 4, 2, 2); }
-        else if (v == 5) { RSK_WIRE(14, 3, 4, 2); RSK_WIRE(14, 4, 2, 2); }
-        else if (v == 6) { RSK_WIRE(14, 3, 104, 2); RSK_WIRE(14, 4, 2, 2); }
-        else if (v == 7) { RSK_WIRE(14, 3, 116, 2); RSK_WIRE(14, 4, 2, 2); }
-        else if (v == 8) { RSK_WIRE(14, 3, 108, 2); RSK_WIRE(14, 4, 2, 2); }
-        else if (v == 9) { RSK_WIRE(14, 5, 108, 2); RSK_WIRE(14, 4, 2, 2); }
+        if (v == 8) { RSK_WIRE(14, 3, 108, 2); RSK_WIRE(14, 4, 2, 2); }
         else if (v == 10) { RSK_WIRE4T(14, 5, 108, 2); RSK_WIRET(14, 4, 2, 2); }
-        else if (v == 11) { RSK_WIRE4(14, 5, 204, 2); RSK_WIRE(14, 4, 2, 2); }
-        else if (v == 12) { RSK_WIRE4(14, 5, 203, 2); RSK_WIRE(14, 4, 2, 2); }
-        else if (v == 13) { RSK_WIRE(14, 5, 204, 2); RSK_WIRE(14, 4, 2, 2); }
         else { RSK_WIRE4(14, 5, 108, 2); RSK_WIRE(14, 4, 2, 2); }
     } else {
-        if (v == 1) RSK_WIRE(0, 0, 2, 4);
-        else if (v == 2) RSK_WIRE(0, 1, 2, 2);
-        else if (v == 3) RSK_WIRE(0, 2, 2, 2);
-        else if (v == 4) { RSK_WIRE(0, 3, 2, 2); RSK_WIRE(0, 4, 2, 2); }
-        else if (v == 5) { RSK_WIRE(0, 3, 4, 2); RSK_WIRE(0, 4, 2, 2); }
-        else if (v == 6) { RSK_WIRE(0, 3, 104, 2); RSK_WIRE(0, 4, 2, 2); }
-        else if (v == 7) { RSK_WIRE(0, 3, 116, 2); RSK_WIRE(0, 4, 2, 2); }
-        else if (v == 8) { RSK_WIRE(0, 3, 108, 2); RSK_WIRE(0, 4, 2, 2); }
-        else if (v == 9) { RSK_WIRE(0, 5, 108, 2); RSK_WIRE(0, 4, 2, 2); }
+        if (v == 8) { RSK_WIRE(0, 3, 108, 2); RSK_WIRE(0, 4, 2, 2); }
         else if (v == 10) { RSK_WIRE4T(0, 5, 108, 2); RSK_WIRET(0, 4, 2, 2); }
-        else if (v == 11) { RSK_WIRE4(0, 5, 204, 2); RSK_WIRE(0, 4, 2, 2); }
-        else if (v == 12) { RSK_WIRE4(0, 5, 203, 2); RSK_WIRE(0, 4, 2, 2); }
-        else if (v == 13) { RSK_WIRE(0, 5, 204, 2); RSK_WIRE(0, 4, 2, 2); }
         else { RSK_WIRE4(0, 5, 108, 2); RSK_WIRE(0, 4, 2, 2); }
     }
 #else
@@ -2982,7 +2938,7 @@ int rsk_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *frame_arena, const u
     hipLaunchKernelGGL(k_decode, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, a, d, c->ks);
     int r = launch_check("k_decode");
     if (r || !compact) return r;
-    return run_compaction(ck, out->valid_idx, out->n_valid, (hipStream_t)stream);
+    return run_compaction(c, ck, out->valid_idx, out->n_valid, (hipStream_t)stream);
 }
 
 int rsk_encode_headers_batch(rsk_ctx *c, uint32_t n, const rsk_encode_hdr_in *in, uint8_t *hdr, int32_t *status,
@@ -3023,7 +2979,7 @@ int rsk_decode_headers_batch(rsk_ctx *c, uint32_t n, const uint8_t *hdr, const u
     hipLaunchKernelGGL(k_decode_hdr, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, a, d, c->ks);
     int r = launch_check("k_decode_hdr");
     if (r || !compact) return r;
-    return run_compaction(ck, out->valid_idx, out->n_valid, (hipStream_t)stream);
+    return run_compaction(c, ck, out->valid_idx, out->n_valid, (hipStream_t)stream);
 }
 
 // Host: the 32-B decode slot of one received frame (EncHead::DecodeBuf reads frame[8] = len; the
@@ -3076,7 +3032,7 @@ int parse_decode(rsk_ctx *c, uint32_t n, const uint8_t *cap_arena, const uint64_
     }
     int r = launch_check("k_parse_decode");
     if (r || !compact) return r;
-    return run_compaction(ck, dec->valid_idx, dec->n_valid, (hipStream_t)stream);
+    return run_compaction(c, ck, dec->valid_idx, dec->n_valid, (hipStream_t)stream);
 }
 }  // namespace
 
@@ -3119,7 +3075,7 @@ int rsk_syncinput_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *rec_arena,
     hipLaunchKernelGGL(k_syncinput_decode, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, a, d, c->ks);
     int r = launch_check("k_syncinput_decode");
     if (r || !compact) return r;
-    return run_compaction(ck, dec->valid_idx, dec->n_valid, (hipStream_t)stream);
+    return run_compaction(c, ck, dec->valid_idx, dec->n_valid, (hipStream_t)stream);
 }
 
 int rsk_filter_parse_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *cap_arena, const uint64_t *cap_off,
@@ -3155,7 +3111,7 @@ int rsk_filter_parse_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *cap_are
         hipLaunchKernelGGL(k_filter_parse_decode<4>, dim3(grid_for(n)), dim3(kBlock), 0, st, a, d, c->ks, match, *f);
     int r = launch_check("k_filter_parse_decode");
     if (r || !compact) return r;
-    return run_compaction(ck, dec->valid_idx, dec->n_valid, (hipStream_t)stream);
+    return run_compaction(c, ck, dec->valid_idx, dec->n_valid, (hipStream_t)stream);
 }
 
 int rsk_capture_filter_batch(rsk_ctx *c, uint32_t n, const uint8_t *cap_arena, const uint64_t *cap_off,
@@ -3184,7 +3140,7 @@ int rsk_capture_filter_batch(rsk_ctx *c, uint32_t n, const uint8_t *cap_arena, c
         hipLaunchKernelGGL(k_capture_filter<4>, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, a, d, *f);
     int r = launch_check("k_capture_filter");
     if (r || !compact) return r;
-    return run_compaction(ck, match_idx, n_match, (hipStream_t)stream);
+    return run_compaction(c, ck, match_idx, n_match, (hipStream_t)stream);
 }
 
 // BuildFilterStr (cap/cap_util.cpp:67-144) with proto "tcp" (cap/RCap.cpp:64)

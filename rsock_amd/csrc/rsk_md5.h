@@ -4,8 +4,8 @@
 // the message schedule is uniform per launch (kernel arguments -> SGPRs) and only the word holding
 // payload[0] differs per lane, so one tag costs one compression for key_len <= 54 (two otherwise).
 // Round constants and rotations are compile-time literals: after full unrolling every K[i] is an
-// instruction immediate, which needs no LDS traffic and no VGPRs ("MD5
-// constants: immediates vs LDS").
+// instruction immediate, which needs no LDS traffic and no VGPRs ("MD5 constants:
+// immediates vs LDS", measured against an LDS-staged table in the A/B build).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -32,10 +32,18 @@ __host__ __device__ __forceinline__ uint32_t rotl(uint32_t x, int s) {
 #endif
 }
 
+// Where the round constants come from.  KImm (shipped): K[I] is a compile-time literal, so after full
+// unrolling it is an instruction immediate.  A kernel may pass another source with a get<I>() (the
+// A/B build's LDS-staged table, rsk_kernels.hip) to measure the north star's "constants in LDS".
+struct KImm {
+    template <int I>
+    __host__ __device__ __forceinline__ uint32_t get() const { return Md5Consts::K[I]; }
+};
+
 // One MD5 step; the round function and message index are resolved at compile time.
-template <int I>
+template <int I, class KS = KImm>
 __host__ __device__ __forceinline__ void md5_step(uint32_t &a, uint32_t b, uint32_t c, uint32_t d,
-                                                  const uint32_t (&m)[16]) {
+                                                  const uint32_t (&m)[16], const KS &ksrc = KS()) {
     constexpr int R = I / 16;
     constexpr int G = R == 0 ? I : R == 1 ? (5 * I + 1) & 15 : R == 2 ? (3 * I + 5) & 15 : (7 * I) & 15;
     constexpr int S0[4] = {7, 12, 17, 22}, S1[4] = {5, 9, 14, 20}, S2[4] = {4, 11, 16, 23},
@@ -46,26 +54,28 @@ __host__ __device__ __forceinline__ void md5_step(uint32_t &a, uint32_t b, uint3
     else if constexpr (R == 1) f = c ^ (d & (b ^ c));   // G = (b&d) | (c&~d)
     else if constexpr (R == 2) f = b ^ c ^ d;           // H
     else f = c ^ (b | ~d);                              // I
-    a = b + rotl(a + f + Md5Consts::K[I] + m[G], S);
+    a = b + rotl(a + f + ksrc.template get<I>() + m[G], S);
 }
 
-template <int I>
+template <int I, class KS>
 __host__ __device__ __forceinline__ void md5_steps(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d,
-                                                   const uint32_t (&m)[16]) {
+                                                   const uint32_t (&m)[16], const KS &ksrc) {
     if constexpr (I < 64) {
         // state rotation a<-d, d<-c, c<-b, b<-new: expressed by rotating the argument roles
-        md5_step<I + 0>(a, b, c, d, m);
-        md5_step<I + 1>(d, a, b, c, m);
-        md5_step<I + 2>(c, d, a, b, m);
-        md5_step<I + 3>(b, c, d, a, m);
-        md5_steps<I + 4>(a, b, c, d, m);
+        md5_step<I + 0>(a, b, c, d, m, ksrc);
+        md5_step<I + 1>(d, a, b, c, m, ksrc);
+        md5_step<I + 2>(c, d, a, b, m, ksrc);
+        md5_step<I + 3>(b, c, d, a, m, ksrc);
+        md5_steps<I + 4>(a, b, c, d, m, ksrc);
     }
 }
 
 // st <- compress(st, m)
-__host__ __device__ __forceinline__ void md5_compress(uint32_t (&st)[4], const uint32_t (&m)[16]) {
+template <class KS = KImm>
+__host__ __device__ __forceinline__ void md5_compress(uint32_t (&st)[4], const uint32_t (&m)[16],
+                                                      const KS &ksrc = KS()) {
     uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
-    md5_steps<0>(a, b, c, d, m);
+    md5_steps<0>(a, b, c, d, m, ksrc);
     st[0] += a;
     st[1] += b;
     st[2] += c;
@@ -80,26 +90,33 @@ struct KeySched {
     int32_t bword;     // word index of payload[0] inside blk
     int32_t bshift;    // bit position of payload[0] inside that word
     int32_t two_blocks;
-    int32_t _pad0;
+    // How the framing / verifying kernels obtain a tag (rsk_set_tag_mode): RSK_TAG_MD5 (0, default)
+    // runs the MD5 compression per lane; RSK_TAG_TABLE (1) stages `tab` in LDS and looks the tag up.
+    // Uniform per launch (a kernel argument), so the choice is a scalar branch.
+    int32_t tag_mode;
     // Device table of the 256 tags this key can produce (tag = f(key, payload[0]) only): entry b =
     // (t0, t1) for payload[0] = b, built on the GPU by k_tag_table at rsk_create.
     const uint2 *tab;
 };
 
 // Tag words (digest bytes 8..11 and 12..15, little-endian) for payload byte b.
+template <class KS = KImm>
 __host__ __device__ __forceinline__ void md5_tag(const KeySched &ks, uint32_t b, uint32_t &t0,
-                                                 uint32_t &t1) {
+                                                 uint32_t &t1, const KS &ksrc = KS()) {
     uint32_t m[16];
     const uint32_t bb = b << ks.bshift;
 #pragma unroll
     for (int w = 0; w < 16; ++w) m[w] = ks.blk[w] | (w == ks.bword ? bb : 0u);
     uint32_t st[4] = {ks.mid[0], ks.mid[1], ks.mid[2], ks.mid[3]};
-    md5_compress(st, m);
+    md5_compress(st, m, ksrc);
     if (ks.two_blocks) {
+        // the padding block of a key with 55..63 bytes past its last whole block: at most 0x80 in
+        // word 0 and the bit length in words 14..15, zeros elsewhere (build_sched) -- literal zeros
+        // keep 13 words out of the SGPRs of the kernels that inline this
         uint32_t p[16];
 #pragma unroll
-        for (int w = 0; w < 16; ++w) p[w] = ks.pad[w];
-        md5_compress(st, p);
+        for (int w = 0; w < 16; ++w) p[w] = (w == 0 || w >= 14) ? ks.pad[w] : 0u;
+        md5_compress(st, p, ksrc);
     }
     t0 = st[2];
     t1 = st[3];

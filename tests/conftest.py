@@ -38,10 +38,19 @@ def gpu():
     return torch.device("cuda:0")
 
 
+@pytest.fixture(scope="session", params=["md5", "table"])
+def tag_mode(request):
+    """Both tag modes of the library (rsk_set_tag_mode): "md5" = one MD5 compression per packet and
+    lane (the default, as util/rhash.cpp:20-41), "table" = the key's 256-entry tag table.  Every GPU
+    test that takes `codec` (or this fixture) runs in both and must give identical bytes."""
+    return request.param
+
+
 @pytest.fixture(scope="session")
-def codec(gpu):
+def codec(gpu, tag_mode):
     from rsock_amd.codec import Codec
 
-    c = Codec(b"hello135", 0)
+    c = Codec(b"hello135", 0, tag_mode=tag_mode)
+    assert c.tag_mode == tag_mode
     yield c
     c.close()

@@ -74,6 +74,8 @@ class Oracle:
         L.orc_splitmix64_at.restype = ctypes.c_uint64
         L.orc_splitmix64_at.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
         L.orc_fill_splitmix.argtypes = [_vp, ctypes.c_uint64, ctypes.c_uint64]
+        L.orc_bench_codec.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32] + [_vp] * 9 + [ctypes.c_int]
+        L.orc_bench_codec.restype = ctypes.c_uint64
         L.orc_encode_batch.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32] + [_vp] * 11 + [ctypes.c_int]
         L.orc_decode_batch.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32] + [_vp] * 14 + [ctypes.c_int]
         L.orc_parse_decode_batch.argtypes = ([ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, _vp, _vp, _vp,
@@ -217,6 +219,17 @@ class Oracle:
         self.L.orc_encode_batch(key, len(key), n, *[_p(a) for a in arrs], _p(idarr), _p(idu), _p(frames),
                                 _p(fo), _p(status), nthreads)
         return frames, status
+
+    def bench_codec(self, key: bytes, payload: np.ndarray, d, idb: bytes, frames: np.ndarray, nthreads: int) -> int:
+        """orc_bench_codec: framing into a zeroed 1500-B buffer + store + OnRecv per packet (the
+        clean-room CPU baseline, bench.py); returns the verified count."""
+        arrs = [np.ascontiguousarray(x) for x in (payload, d.pay_off.astype(np.uint64), d.pay_len.astype(np.uint16),
+                                                   d.cmd.astype(np.uint8), d.conv.astype(np.uint32),
+                                                   d.conn_key.astype(np.uint64))]
+        idu = np.frombuffer(bytes(idb)[:8].ljust(8, b"\0"), np.uint8).copy()
+        fo = np.ascontiguousarray(d.frame_off.astype(np.uint64))
+        return int(self.L.orc_bench_codec(key, len(key), d.n, *[_p(a) for a in arrs], _p(idu), _p(frames), _p(fo),
+                                          nthreads))
 
     def decode_batch(self, key: bytes, frames: np.ndarray, frame_off: np.ndarray, frame_len: np.ndarray,
                      is_tcp_close: np.ndarray | None = None, nthreads: int = 8) -> dict:

@@ -19,14 +19,19 @@ def gold(name):
     return np.load(os.path.join(GOLD, name), allow_pickle=False)
 
 
+def _golden_encode(cx, gpu, g, pad16=False):
+    n = len(g["status"])
+    frame_off = (np.arange(n) * 1504).astype(np.uint64)
+    return run_encode(cx, gpu, g["payload"], g["pay_off"], np.minimum(g["pay_len"], 65535).astype(np.uint16),
+                      g["cmd"], g["conv"], g["conn_key"], frame_off, n * 1504, idarr=g["id"], pad16=pad16)
+
+
 @pytest.mark.parametrize("pad16", [False, True])
 def test_encode_matches_reference_frames(codec, gpu, pad16):
     g = gold("frames.npz")
     n = len(g["status"])
     pitch = 1504
-    frame_off = (np.arange(n) * pitch).astype(np.uint64)
-    fr, st = run_encode(codec, gpu, g["payload"], g["pay_off"], np.minimum(g["pay_len"], 65535).astype(np.uint16),
-                        g["cmd"], g["conv"], g["conn_key"], frame_off, n * pitch, idarr=g["id"], pad16=pad16)
+    fr, st = _golden_encode(codec, gpu, g, pad16)
     assert np.array_equal(st, g["status"])
     for i in range(n):
         if st[i] > 0:
@@ -44,14 +49,14 @@ def test_decode_matches_reference_onrecv(codec, gpu):
     assert np.array_equal(got["valid_idx"][:nv].view(np.uint32), np.nonzero(g["status"] == 1)[0].astype(np.uint32))
 
 
-def test_tags_all_keys_match_reference(gpu):
+def test_tags_all_keys_match_reference(gpu, tag_mode):
     from rsock_amd.codec import Codec
 
     g = gold("tags.npz")
     kb, ko, kl = g["key_bytes"], g["key_off"], g["key_len"]
     for k in range(len(kl)):
         key = kb[int(ko[k]): int(ko[k]) + int(kl[k])].tobytes()
-        cx = Codec(key, 0)
+        cx = Codec(key, 0, tag_mode=tag_mode)
         try:
             payload = np.repeat(np.arange(256, dtype=np.uint8), 16)
             z = np.zeros(256, np.uint8)
@@ -129,3 +134,30 @@ def test_parse_matches_reference_rawinput(codec, gpu, oracle, flags, align):
         assert np.array_equal(th["cap_pay_off"].view(np.uint16)[dl_], g["pay_off"][sel, j][dl_])
         assert np.array_equal(th["cap_pay_len"].view(np.uint16)[dl_], g["pay_len"][sel, j][dl_])
         assert_dec_equal(out.to_host(), oracle.parse_decode_batch(KEY, arena, offs, wl, cl, dl, flags))
+
+
+def test_tag_mode_api(gpu):
+    """rsk_set_tag_mode / rsk_get_tag_mode: a context starts in RSK_TAG_MD5, takes RSK_TAG_TABLE and
+    back, refuses unknown modes, and both modes frame the golden frames identically."""
+    from rsock_amd import _abi
+    from rsock_amd.codec import Codec, RskError, lib
+
+    cx = Codec(b"hello135", 0)
+    try:
+        assert lib().rsk_get_tag_mode(cx._ctx) == _abi.TAG_MD5 and cx.tag_mode == "md5"
+        assert lib().rsk_set_tag_mode(cx._ctx, 7) == _abi.EINVAL
+        assert lib().rsk_set_tag_mode(cx._ctx, -1) == _abi.EINVAL
+        assert cx.tag_mode == "md5"  # unchanged by a refused mode
+        assert lib().rsk_set_tag_mode(None, 0) == _abi.EINVAL and lib().rsk_get_tag_mode(None) == _abi.EINVAL
+        g = gold("frames.npz")
+        outs = []
+        for mode in ("table", "md5"):
+            cx.set_tag_mode(mode)
+            assert cx.tag_mode == mode
+            fr, st = _golden_encode(cx, gpu, g)
+            outs.append((fr, st))
+        assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+        with pytest.raises(RskError):
+            cx.set_tag_mode(5)
+    finally:
+        cx.close()

@@ -268,12 +268,14 @@ def test_all_first_bytes(codec, gpu, oracle):
         assert fr[b * 48: b * 48 + 8].tobytes() == oracle.tag(KEY, b)
 
 
-def test_tag_tables_per_context(gpu, oracle):
-    """Each context frames with its own key's tag table, with several contexts alive at once."""
+def test_tag_tables_per_context(gpu, oracle, tag_mode):
+    """Each context frames with its own key (schedule and tag table), with several contexts alive at
+    once, and a context whose mode differs from the others' in the middle."""
     from rsock_amd.codec import Codec
 
     keys = [b"", b"k", b"hello135", bytes(range(60)), bytes(range(100, 230))]
-    cxs = [Codec(k, 0) for k in keys]
+    other = "table" if tag_mode == "md5" else "md5"
+    cxs = [Codec(k, 0, tag_mode=other if j == 2 else tag_mode) for j, k in enumerate(keys)]
     try:
         n = 256
         payload = np.arange(256, dtype=np.uint8).repeat(16)
@@ -292,12 +294,12 @@ def test_tag_tables_per_context(gpu, oracle):
 
 
 @pytest.mark.parametrize("klen", [0, 1, 7, 8, 9, 53, 54, 55, 56, 62, 63, 64, 65, 100, 118, 119, 120, 127, 128, 200])
-def test_key_lengths(gpu, oracle, klen):
+def test_key_lengths(gpu, oracle, klen, tag_mode):
     """1-block, 2-block and midstate key schedules (util/rhash.cpp hashes key || payload[0])."""
     from rsock_amd.codec import Codec
 
     key = bytes((np.arange(klen) * 37 + 11) % 256) if klen else b""
-    cx = Codec(key, 0)
+    cx = Codec(key, 0, tag_mode=tag_mode)
     try:
         n = 300
         rng = np.random.default_rng(klen)

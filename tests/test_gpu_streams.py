@@ -134,3 +134,96 @@ def test_compaction_in_captured_graph(codec, gpu):
         g.replay()
         torch.cuda.synchronize()
         _check(out, exp[k], r)
+
+
+def test_compaction_stall_is_flagged_and_recovered(gpu):
+    """a look-back that gives up must not go unnoticed.  Tile 1 of one k_compact launch is
+    made to publish nothing (rsk__inject_compact_stall, a tile that never runs); tile 2 times out (after
+    ~4M polls, no hang), the context's sticky RSK_DEVERR_LOOKBACK flag is raised and
+    rsk_check_device_errors reports it once; the next call on the same stream (state re-initialised)
+    gives the right VALID list again."""
+    import ctypes
+
+    import torch
+
+    from rsock_amd import _abi
+    from rsock_amd.codec import Codec, DecodeBuffers, RskError, lib
+
+    n = 64 * 4096  # 64 compaction tiles
+    d = workload.describe("c2", 0, n, n=n)
+    w = workload.DeviceWorkload(d, gpu)
+    cx = Codec(b"hello135", 0)
+    try:
+        cx.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
+                        w.status, id_uniform=workload.ID_UNIFORM)
+        w.corrupt_frames()
+        keep = np.nonzero(~d.corrupt)[0].astype(np.int32)
+        s = torch.cuda.Stream(gpu)
+        o = DecodeBuffers.alloc(n, gpu)
+
+        def decode_and_check():
+            cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, o, stream=s)
+            torch.cuda.synchronize()
+            nv = int(o.n_valid.item())
+            return nv == keep.size and np.array_equal(o.valid_idx[:nv].cpu().numpy(), keep)
+
+        assert decode_and_check() and cx.check_device_errors() == 0
+        fn = lib().rsk__inject_compact_stall
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+        assert fn(cx._ctx, 1) == 0
+        assert not decode_and_check()  # tiles 2.. took a wrong prefix
+        with pytest.raises(RskError, match="0x1"):
+            cx.check_device_errors()
+        assert cx.check_device_errors() == 0  # read and cleared
+        for _ in range(3):  # state re-zeroed at the next call: right again, epochs run on
+            assert decode_and_check()
+        assert cx.check_device_errors() == 0
+        flags = ctypes.c_uint32(7)
+        assert lib().rsk_check_device_errors(cx._ctx, ctypes.byref(flags)) == 0 and flags.value == 0
+        assert _abi.DEVERR_LOOKBACK == 1
+    finally:
+        cx.close()
+
+
+def test_capture_needs_reserved_stream_and_release(gpu):
+    """A compacting decode captured on a stream whose scratch was never set up is refused (RSK_EINVAL,
+    rsk_codec.h "Streams"), not recorded with a memset that has not run; after reserve + one eager call
+    the capture works; rsk_release_stream frees the stream's scratch and a later call re-creates it."""
+    import torch
+
+    from rsock_amd.codec import Codec, DecodeBuffers, RskError
+
+    n = 8192
+    d = workload.describe("c2", 0, n, n=n)
+    w = workload.DeviceWorkload(d, gpu)
+    cx = Codec(b"hello135", 0)
+    try:
+        cx.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
+                        w.status, id_uniform=workload.ID_UNIFORM)
+        torch.cuda.synchronize()
+        o = DecodeBuffers.alloc(n, gpu)
+        s = torch.cuda.Stream(gpu)
+        g = torch.cuda.CUDAGraph()
+        with pytest.raises(RskError):
+            with torch.cuda.graph(g, stream=s):
+                cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, o, stream=s)
+        torch.cuda.synchronize()
+        s2 = torch.cuda.Stream(gpu)
+        cx.reserve(n, stream=s2)
+        cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, o, stream=s2)  # eager: initialises the state
+        g2 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g2, stream=s2):
+            cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, o, stream=s2)
+        o.n_valid.zero_()
+        g2.replay()
+        torch.cuda.synchronize()
+        assert int(o.n_valid.item()) == n
+        del g2
+        cx.release_stream(s2)
+        o.n_valid.zero_()
+        cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, o, stream=s2)  # scratch re-created
+        torch.cuda.synchronize()
+        assert int(o.n_valid.item()) == n
+        assert cx.check_device_errors() == 0
+    finally:
+        cx.close()
