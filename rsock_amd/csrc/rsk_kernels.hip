@@ -86,16 +86,21 @@ __device__ __forceinline__ uint64_t rdl64(uint64_t v, uint32_t j) {
 //                          computes them once per context and every kernel that frames or verifies
 //                          stages the 2-KB table in LDS (one entry per thread of the 256-thread block,
 //                          before any early exit) and looks the tag up with one ds_read_b64.
-// A/B build only: RSK_TAG_MD5_LDS (2) = RSK_TAG_MD5 with the 64 round constants read from an LDS copy
-// staged per block (the north star's layout) instead of immediates.
+// A/B build only (RSK_AB): RSK_TAG_MD5 reads the 64 round constants from an LDS copy staged per
+// block (the north star's "MD5 round constants ... staged in LDS") instead of instruction
+// immediates; compared against the shipped build by tools/ab_tag.py (profiles/r03_ab_md5_lds.json).
 __shared__ uint2 s_tags[256];
 #ifdef RSK_AB
 __shared__ uint32_t s_md5k[64];
 struct KLds {
     template <int I>
-    __device__ __forceinline__ uint32_t get() const { return s_md5k[I]; }
+    __device__ __forceinline__ uint32_t get() const {
+        // one group of 4 constants per 4 steps, read where they are used: without the scheduling
+        // barrier the compiler issues all 64 reads up front and holds them in 64 VGPRs
+        if constexpr ((I & 3) == 0) __builtin_amdgcn_sched_barrier(0);
+        return s_md5k[I];
+    }
 };
-constexpr int kTagMd5Lds = 2;
 #endif
 
 __device__ __forceinline__ void stage_tags(const KeySched &ks) {
@@ -105,7 +110,7 @@ __device__ __forceinline__ void stage_tags(const KeySched &ks) {
         __syncthreads();
     }
 #ifdef RSK_AB
-    if (ks.tag_mode == kTagMd5Lds) {
+    else {
         if (threadIdx.x < 64u) s_md5k[threadIdx.x] = rsk::Md5Consts::K[threadIdx.x];
         __syncthreads();
     }
@@ -120,12 +125,10 @@ __device__ __forceinline__ void tag_of(const KeySched &ks, uint32_t b, uint32_t 
         return;
     }
 #ifdef RSK_AB
-    if (ks.tag_mode == kTagMd5Lds) {
-        rsk::md5_tag(ks, b & 255u, t0, t1, KLds());
-        return;
-    }
-#endif
+    rsk::md5_tag(ks, b & 255u, t0, t1, KLds());
+#else
     rsk::md5_tag(ks, b & 255u, t0, t1);
+#endif
 }
 
 // Frame bytes 8..31 as words H[2..7] (bean/EncHead.cpp:9-24 field order; byte 30 reserved = 0,
@@ -854,13 +857,20 @@ __global__ __launch_bounds__(kBlock) void k_encode_tiled(EncArgs a, KeySched ks)
 // stretch of the arenas at a time (SBW * GRP packets per super-block) instead of each its own region
 // 64 packets from the next wave's: C3 -3.7 %, C4 -4.1 %, C2 within 1 % against the tiled mapping
 // (profiles/r02_ab_encode_mapping.json).  The grid holds only waves that own a packet (enc_grid).
-template <int MODE, int PU, int U, int NT, int GRP, int SBW>
+// XCD (A/B): blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md); XCD = true renumbers
+// them so that each XCD's blocks own consecutive waves (descriptor lines stay in one XCD's L2).
+template <int MODE, int PU, int U, int NT, int GRP, int SBW, bool XCD = false>
 __global__ __launch_bounds__(kBlock) void k_encode(EncArgs a, KeySched ks) {
     __shared__ CopyRec recs[kWavesPerBlock][64];
     __shared__ uint32_t cend[kWavesPerBlock][64];
     stage_tags(ks);
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    const uint64_t wg = (uint64_t)blockIdx.x * kWavesPerBlock + w;
+    uint32_t blk = blockIdx.x;
+    if constexpr (XCD) {
+        const uint32_t per = gridDim.x / 8u;
+        if (blk < per * 8u) blk = (blk % 8u) * per + blk / 8u;
+    }
+    const uint64_t wg = (uint64_t)blk * kWavesPerBlock + w;
     const uint64_t sb = wg / SBW, wl = wg % SBW;
     const uint64_t first = sb * SBW * 64u + wl * GRP;  // the wave's smallest packet
     if (first >= a.n) return;  // wave-uniform
@@ -2690,12 +2700,16 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 // 0 = the shipped k_encode<11, 4, 4, -1, 8, 1024> (grouped interleave; software-pipelined per-packet
 // copy, 4 packets per batch; flat sets' tag behind the first chunk loads); 12 / 13 = k_copy_probe
 // (memory-side ceiling probe, wrong bytes) with 12 / 4 packets per batch; 37 = the tiled mapping
-// with the shipped copy; 47 = the unpipelined copy (MODE 6), 8 packets per iteration.  Rounds 1-2
+// with the shipped copy; 47 = the unpipelined copy (MODE 6), 8 packets per iteration; 50 / 51 / 52 /
+// 55 = groups of <GRP, SBW> = <1, 1024> / <2, 1024> / <1, 256> / <1, 4096> (concurrent waves on
+// adjacent packets); 53 / 54 = <1, 1024> / <8, 1024> with XCD-contiguous block numbering; 56 = 0 with
+// the tag (payload[0] + MD5) in the copy loop for every per-packet set (MODE 10).  Rounds 1-2
 // measured ~45 more variants (profiles/r01_ab_*, r02_ab_*); their code is in the git history.
 // v + 100 * cap (cap 1..4): the same kernel held to `cap` blocks per CU by unused LDS.
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
     const int k = v % 100;
-    if (!c || v < 0 || v / 100 > 4 || !(k == 0 || k == 12 || k == 13 || k == 37 || k == 47)) return RSK_EINVAL;
+    if (!c || v < 0 || v / 100 > 4 || !(k == 0 || k == 12 || k == 13 || k == 37 || k == 47 || (k >= 50 && k <= 56)))
+        return RSK_EINVAL;
     c->enc_variant = v;
     return RSK_OK;
 }
@@ -2752,12 +2766,7 @@ rsk_ctx *rsk_create(const uint8_t *key, uint32_t key_len, int device) {
 
 int rsk_set_tag_mode(rsk_ctx *c, int mode) {
     if (!c) return RSK_EINVAL;
-#ifdef RSK_AB
-    const int max_mode = kTagMd5Lds;
-#else
-    const int max_mode = RSK_TAG_TABLE;
-#endif
-    if (mode < RSK_TAG_MD5 || mode > max_mode) return RSK_EINVAL;
+    if (mode != RSK_TAG_MD5 && mode != RSK_TAG_TABLE) return RSK_EINVAL;
     c->ks.tag_mode = mode;
     return RSK_OK;
 }
@@ -2849,6 +2858,13 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         case 13: hipLaunchKernelGGL((k_copy_probe<4>), gd, bd, lds, st, a); break;
         case 37: hipLaunchKernelGGL((k_encode_tiled<11, 4, 4, -1>), gd, bd, lds, st, a, c->ks); break;
         case 47: hipLaunchKernelGGL((k_encode<6, 8, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
+        case 50: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 1, 1024>), dim3(enc_grid(n, 1, 1024)), bd, lds, st, a, c->ks); break;
+        case 51: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 2, 1024>), dim3(enc_grid(n, 2, 1024)), bd, lds, st, a, c->ks); break;
+        case 52: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 1, 256>), dim3(enc_grid(n, 1, 256)), bd, lds, st, a, c->ks); break;
+        case 53: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 1, 1024, true>), dim3(enc_grid(n, 1, 1024)), bd, lds, st, a, c->ks); break;
+        case 54: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024, true>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
+        case 55: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 1, 4096>), dim3(enc_grid(n, 1, 4096)), bd, lds, st, a, c->ks); break;
+        case 56: hipLaunchKernelGGL((k_encode<10, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
         default: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
     }
 #else

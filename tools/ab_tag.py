@@ -1,13 +1,13 @@
 #!/usr/bin/env python3
-"""In-process A/B of the tag modes (interleaved rounds in ONE process) on k_encode and k_decode:
-   make -C rsock_amd ab && python tools/ab_tag.py [--config c3] [--rounds 10] [--reps 10] [--modes 0,1,2]
-0 = RSK_TAG_MD5 (MD5 per lane, round constants as instruction immediates: the shipped headline),
-1 = RSK_TAG_TABLE (the key's 256 tags staged in LDS, one ds_read_b64 per packet),
-2 = the A/B build's MD5 per lane with the 64 round constants read from an LDS copy staged per block
-    (the north star's "MD5 round constants ... staged in LDS").
-Runs on the A/B build (rsock_amd/librsk_ab.so through RSK_LIB; mode 2 exists only there).  Checks
-that every mode's frame arena and decode outputs are byte-identical, then prints per-mode median /
-min kernel ms and the encode's algorithmic GB/s."""
+"""A/B of the tag computation on k_encode and k_decode (interleaved rounds in one process):
+   python tools/ab_tag.py [--config c3] [--rounds 10] [--reps 10] [--modes md5,table]
+With the shipped library (default RSK_LIB=librsk.so): md5 = RSK_TAG_MD5 (MD5 per lane, round
+constants as instruction immediates: the headline), table = RSK_TAG_TABLE (the key's 256 tags staged
+in LDS, one ds_read_b64 per packet).  With RSK_LIB=librsk_ab.so (make -C rsock_amd ab), md5 = the MD5
+per lane with its 64 round constants read from an LDS copy staged per block (the north star's "MD5
+round constants ... staged in LDS"); run the two libraries back to back in separate processes.
+Checks that every mode's frame arena and decode outputs are byte-identical, then prints per-mode
+median / min kernel ms and the encode's fraction of 8 TB/s (algorithmic bytes)."""
 import argparse
 import json
 import os
@@ -16,7 +16,6 @@ import sys
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ.setdefault("RSK_LIB", "librsk_ab.so")
 
 
 def main():
@@ -25,7 +24,7 @@ def main():
     ap.add_argument("--packets", type=int, default=0)
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--modes", default="0,1,2")
+    ap.add_argument("--modes", default="md5,table")
     args = ap.parse_args()
     import torch
 
@@ -38,7 +37,7 @@ def main():
     d = workload.describe(args.config, 0, n, n=n)
     w = workload.DeviceWorkload(d, dev)
     cx = rc.Codec(b"hello135", 0)
-    modes = [int(m) for m in args.modes.split(",")]
+    modes = args.modes.split(",")
     s = torch.cuda.current_stream()
 
     def enc():
@@ -76,7 +75,8 @@ def main():
                 torch.cuda.synchronize()
                 times[(m, k)].append(ev[0].elapsed_time(ev[1]) / args.reps)
     byts = int(enc_bytes_per_pkt(d.pay_len.astype(np.int64)).sum())
-    names = {0: "md5_immediates", 1: "tag_table_lds", 2: "md5_consts_in_lds"}
+    lib = os.path.basename(rc._abi.LIB_PATH)
+    names = {"md5": "md5_consts_in_lds" if "ab" in lib else "md5_immediates", "table": "tag_table_lds"}
     out = {}
     for m in modes:
         te, td = np.array(times[(m, "enc")]), np.array(times[(m, "dec")])
@@ -84,7 +84,7 @@ def main():
             "k_encode_median_ms": round(float(np.median(te)), 4), "k_encode_min_ms": round(float(te.min()), 4),
             "k_encode_frac": round(byts / (np.median(te) * 1e-3) / 1e9 / 8000.0, 4),
             "decode_median_ms": round(float(np.median(td)), 4), "decode_min_ms": round(float(td.min()), 4)}
-    print(json.dumps({"config": args.config, "packets": d.n, "frame_pitch": d.frame_pitch, "modes": out}))
+    print(json.dumps({"config": args.config, "lib": lib, "packets": d.n, "frame_pitch": d.frame_pitch, "modes": out}))
 
 
 if __name__ == "__main__":
