@@ -86,11 +86,11 @@ __device__ __forceinline__ uint64_t rdl64(uint64_t v, uint32_t j) {
 //                          computes them once per context and every kernel that frames or verifies
 //                          stages the 2-KB table in LDS (one entry per thread of the 256-thread block,
 //                          before any early exit) and looks the tag up with one ds_read_b64.
-// A/B build only (RSK_AB): RSK_TAG_MD5 reads the 64 round constants from an LDS copy staged per
+// A/B build only (RSK_MD5_K_LDS, librsk_md5lds.so): RSK_TAG_MD5 reads the 64 round constants from an LDS copy staged per
 // block (the north star's "MD5 round constants ... staged in LDS") instead of instruction
 // immediates; compared against the shipped build by tools/ab_tag.py (profiles/r03_ab_md5_lds.json).
 __shared__ uint2 s_tags[256];
-#ifdef RSK_AB
+#ifdef RSK_MD5_K_LDS
 __shared__ uint32_t s_md5k[64];
 struct KLds {
     template <int I>
@@ -109,7 +109,7 @@ __device__ __forceinline__ void stage_tags(const KeySched &ks) {
         s_tags[threadIdx.x] = ks.tab[threadIdx.x];
         __syncthreads();
     }
-#ifdef RSK_AB
+#ifdef RSK_MD5_K_LDS
     else {
         if (threadIdx.x < 64u) s_md5k[threadIdx.x] = rsk::Md5Consts::K[threadIdx.x];
         __syncthreads();
@@ -124,7 +124,7 @@ __device__ __forceinline__ void tag_of(const KeySched &ks, uint32_t b, uint32_t 
         t1 = t.y;
         return;
     }
-#ifdef RSK_AB
+#ifdef RSK_MD5_K_LDS
     rsk::md5_tag(ks, b & 255u, t0, t1, KLds());
 #else
     rsk::md5_tag(ks, b & 255u, t0, t1);
@@ -500,13 +500,13 @@ __device__ __forceinline__ void batch_slots(uint64_t bm, uint32_t lane, uint32_t
     }
 }
 
-template <int PU, int NT, bool TAG>
+template <int PU, int NT, bool TAG, int TG = 0>
 __device__ __forceinline__ void pkt_issue(const EncArgs &a, const Lane1 &L, uint32_t lane, uint64_t bm,
                                           uint4 (&A)[PU][2], uint32_t &b0) {
     uint32_t js[PU], myj;
     bool on[PU], mine;
     batch_slots<PU>(bm, lane, js, on, myj, mine);
-    if constexpr (TAG) {  // payload[0] of the lane's slot packet, ahead of the chunk loads
+    if constexpr (TAG && TG == 0) {  // payload[0] of the lane's slot packet, ahead of the chunk loads
         const uint64_t po = shfl64(L.po, myj);
         b0 = rsk::gptr(a.payload)[mine ? po : 0u];
     }
@@ -527,15 +527,40 @@ __device__ __forceinline__ void pkt_issue(const EncArgs &a, const Lane1 &L, uint
     }
 }
 
-template <int PU, int NT, bool TAG>
+// A frame's last chunk, held back (wave-uniform, SGPRs) to be stored together with the next frame's
+// first chunk: frames packed back to back at byte granularity share that 16-B chunk, and two partial
+// stores from two lanes (up to 2 x 5 byte / short / dword stores) become one 16-B store.
+struct TailCarry {
+    uint4 t;       // the chunk: its first bytes are the previous frame's tail
+    uintptr_t at;  // its 16-B aligned address
+    bool on;
+};
+
+__device__ __forceinline__ uint4 rdl4(const uint4 &v, uint32_t j) {
+    return make_uint4(rdl(v.x, j), rdl(v.y, j), rdl(v.z, j), rdl(v.w, j));
+}
+
+// bytes [0, r) of t, bytes [r, 16) of v
+__device__ __forceinline__ uint4 merge16(const uint4 &t, const uint4 &v, uint32_t r) {
+    const uint4 m = rsk::keep_bytes16(make_uint4(~0u, ~0u, ~0u, ~0u), (int)r);
+    return make_uint4((t.x & m.x) | (v.x & ~m.x), (t.y & m.y) | (v.y & ~m.y), (t.z & m.z) | (v.z & ~m.z),
+                      (t.w & m.w) | (v.w & ~m.w));
+}
+
+// nxt_bm: the packets of the batch stored after this one (its lowest set bit is the next frame in
+// store order), for the TailCarry hand-over; tc carries a held-back tail chunk between calls.
+template <int PU, int NT, bool TAG, int TG = 0>
 __device__ __forceinline__ void pkt_store(const EncArgs &a, const KeySched &ks, const Lane1 &L, uint32_t lane,
-                                          uint64_t bm, const uint4 (&A)[PU][2], uint32_t my_b0) {
+                                          uint64_t bm, const uint4 (&A)[PU][2], uint32_t my_b0, uint64_t nxt_bm,
+                                          TailCarry &tc) {
     uint32_t js[PU], myj;
     bool on[PU], mine;
     batch_slots<PU>(bm, lane, js, on, myj, mine);
     uint32_t t0 = 0, t1 = 0;
-    if constexpr (TAG) {
+    if constexpr (TAG && TG == 0) {
         tag_of(ks, my_b0, t0, t1);
+    } else if constexpr (TAG) {
+        // the tag prepass (copy_pkt_pipe) left each packet's tag and payload[0] in its own lane's H
     } else {  // lane p: the header chunks of its slot packet (store_head)
         uint32_t H[8];
 #pragma unroll
@@ -560,23 +585,54 @@ __device__ __forceinline__ void pkt_store(const EncArgs &a, const KeySched &ks, 
                                   wave_shl1(A[p][1].w));
         }
         uint32_t Hj[8];
+        bool hmerge = false, tmerge = false;
+        uint32_t kt = 0;
         if constexpr (TAG) {
 #pragma unroll
             for (int t = 2; t < 8; ++t) Hj[t] = rdl(L.H[t], js[p]);
-            Hj[0] = rdl(t0, (uint32_t)p);
-            Hj[1] = rdl(t1, (uint32_t)p);
-            Hj[7] |= rdl(my_b0, (uint32_t)p) << 24;
+            if constexpr (TG == 0) {
+                Hj[0] = rdl(t0, (uint32_t)p);
+                Hj[1] = rdl(t1, (uint32_t)p);
+                Hj[7] |= rdl(my_b0, (uint32_t)p) << 24;
+            } else {
+                Hj[0] = rdl(L.H[0], js[p]);
+                Hj[1] = rdl(L.H[1], js[p]);
+            }
+            // byte-packed neighbours (no padding): this frame's first chunk completes the held-back
+            // tail of the previous frame; its own last chunk is held back when the next frame in store
+            // order starts inside it.  All uniform.
+            hmerge = tc.on && tc.at == reinterpret_cast<uintptr_t>(g.d0);
+            tc.on = false;
+            const uint64_t nb = p + 1 < PU && on[p + 1] ? 0ull : nxt_bm;
+            const bool has_next = (p + 1 < PU && on[p + 1]) || nb != 0ull;
+            const uint32_t jn = p + 1 < PU && on[p + 1] ? js[p + 1] : (uint32_t)__builtin_ctzll(nb | (1ull << 63));
+            const uintptr_t end = reinterpret_cast<uintptr_t>(a.frame + rdl64(L.fo, js[p])) + fl;
+            tmerge = a.pad == 0u && has_next && (end & 15u) != 0u &&
+                     reinterpret_cast<uintptr_t>(a.frame + rdl64(L.fo, jn)) == end;
+            kt = nst - 1u;
         }
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
             const uint32_t k = lane + 64u * q;
             if (q == 1 && nst <= 64u) continue;  // uniform
-            if (k >= nst || (!TAG && k < 2u)) continue;
-            const uint4 V = rsk::funnel16(A[p][q], B[q], g.sh);
             if constexpr (TAG) {
-                const uint4 v = k < (g.r >= 2u ? 3u : 2u) ? head_chunk(Hj, k, g.r, V) : V;
-                store_piece<NT>(g.d0 + 16u * k, v, k == 0u ? g.r : 0u, (int)flen - 16 * (int)k, a.pad != 0u);
+                const uint4 V = rsk::funnel16(A[p][q], B[q], g.sh);
+                uint4 v = k < (g.r >= 2u ? 3u : 2u) ? head_chunk(Hj, k, g.r, V) : V;
+                uint32_t lo = k == 0u ? g.r : 0u;
+                if (hmerge && k == 0u) {
+                    v = merge16(tc.t, v, g.r);
+                    lo = 0u;
+                }
+                if (tmerge && (kt >> 6) == (uint32_t)q) {  // uniform: hold the last chunk back
+                    tc.t = rdl4(v, kt & 63u);
+                    tc.at = reinterpret_cast<uintptr_t>(g.d0) + 16u * kt;
+                    tc.on = true;
+                }
+                if (k >= nst || (tmerge && k == kt)) continue;
+                store_piece<NT>(g.d0 + 16u * k, v, lo, (int)flen - 16 * (int)k, a.pad != 0u);
             } else {
+                if (k >= nst || k < 2u) continue;
+                const uint4 V = rsk::funnel16(A[p][q], B[q], g.sh);
                 store_piece<NT>(g.d0 + 16u * k, V, k == 2u ? chunk2_lo(g.r) : 0u, (int)flen - 16 * (int)k,
                                 a.pad != 0u);
             }
@@ -584,22 +640,50 @@ __device__ __forceinline__ void pkt_store(const EncArgs &a, const KeySched &ks, 
     }
 }
 
-template <int PU, int NT, bool TAG>
-__device__ __forceinline__ void copy_pkt_pipe(const EncArgs &a, const KeySched &ks, const Lane1 &L, uint32_t lane,
+// Tag prepass (TAG form, TG > 0): before the batch that needs them, the lanes of the next TG packets
+// (in copy order) load their payload[0] and run their MD5 together, one compression pass per TG
+// packets instead of one per batch of PU packets (a pass costs the same VALU issue however few lanes
+// are active); the byte loads fetch each payload's first line at most TG / PU batches before its
+// chunk loads.  TG == 0: payload[0] loaded beside the batch's chunk loads, MD5 per batch (round 2).
+template <int TG>
+__device__ __forceinline__ void tag_prepass(const EncArgs &a, const KeySched &ks, Lane1 &L, uint32_t lane,
+                                            uint64_t bm, uint64_t &untagged) {
+    if constexpr (TG > 0) {
+        if (!(bm & untagged)) return;  // uniform
+        uint64_t m = 0;
+#pragma unroll
+        for (int k = 0; k < TG; ++k) {
+            const uint64_t b = untagged & (~untagged + 1ull);
+            m |= b;
+            untagged ^= b;
+        }
+        if ((m >> lane) & 1ull) encode_tag(a, ks, L);
+    }
+}
+
+template <int PU, int NT, bool TAG, int TG = 0>
+__device__ __forceinline__ void copy_pkt_pipe(const EncArgs &a, const KeySched &ks, Lane1 &L, uint32_t lane,
                                               uint64_t vm) {
     uint4 A0[PU][2], A1[PU][2];
     uint32_t b0a = 0, b0b = 0;
+    TailCarry tc;
+    tc.t = make_uint4(0u, 0u, 0u, 0u);
+    tc.at = 0;
+    tc.on = false;
+    uint64_t untagged = TAG ? vm : 0ull;
     uint64_t cur = take_batch<PU>(vm);
     if (!cur) return;
-    pkt_issue<PU, NT, TAG>(a, L, lane, cur, A0, b0a);
+    pkt_issue<PU, NT, TAG, TG>(a, L, lane, cur, A0, b0a);
     while (true) {
         const uint64_t nxt = take_batch<PU>(vm);
-        if (nxt) pkt_issue<PU, NT, TAG>(a, L, lane, nxt, A1, b0b);
-        pkt_store<PU, NT, TAG>(a, ks, L, lane, cur, A0, b0a);
+        if (nxt) pkt_issue<PU, NT, TAG, TG>(a, L, lane, nxt, A1, b0b);
+        if constexpr (TAG) tag_prepass<TG>(a, ks, L, lane, cur, untagged);
+        pkt_store<PU, NT, TAG, TG>(a, ks, L, lane, cur, A0, b0a, nxt, tc);
         if (!nxt) break;
         cur = take_batch<PU>(vm);
-        if (cur) pkt_issue<PU, NT, TAG>(a, L, lane, cur, A0, b0a);
-        pkt_store<PU, NT, TAG>(a, ks, L, lane, nxt, A1, b0b);
+        if (cur) pkt_issue<PU, NT, TAG, TG>(a, L, lane, cur, A0, b0a);
+        if constexpr (TAG) tag_prepass<TG>(a, ks, L, lane, nxt, untagged);
+        pkt_store<PU, NT, TAG, TG>(a, ks, L, lane, nxt, A1, b0b, cur, tc);
         if (!cur) break;
     }
 }
@@ -709,7 +793,7 @@ constexpr uint32_t kDeferTagMeanBytes = 1024;
 // with the flat sets' tag in phase 1, 10 = 9 with the tag in the copy loop for every per-packet
 // set, 3 = tag always in phase 1, 7 = flat path only, 8 = per-packet path only.  NT < 0: store
 // policy per set.
-template <int MODE, int PU, int U, int NT, int GRP = 64>
+template <int MODE, int PU, int U, int NT, int GRP = 64, int TG = 0>
 __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks, uint64_t i, uint32_t lane,
                                            CopyRec *recs, uint32_t *cend) {
     Lane1 L = encode_phase1<MODE == 3 || MODE == 7>(a, ks, i);
@@ -753,8 +837,8 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
     // 0.420 ms with the second.
     if constexpr (MODE == 9 || MODE == 10 || MODE == 11) {  // software-pipelined per-packet copy (shipped: 9)
         if (defer) {
-            if (nt) copy_pkt_pipe<PU, 2, true>(a, ks, L, lane, vm);
-            else copy_pkt_pipe<PU, 0, true>(a, ks, L, lane, vm);
+            if (nt) copy_pkt_pipe<PU, 2, true, TG>(a, ks, L, lane, vm);
+            else copy_pkt_pipe<PU, 0, true, TG>(a, ks, L, lane, vm);
         } else {
             if (nt) copy_pkt_pipe<PU, 2, false>(a, ks, L, lane, vm);
             else copy_pkt_pipe<PU, 0, false>(a, ks, L, lane, vm);
@@ -859,8 +943,8 @@ __global__ __launch_bounds__(kBlock) void k_encode_tiled(EncArgs a, KeySched ks)
 // (profiles/r02_ab_encode_mapping.json).  The grid holds only waves that own a packet (enc_grid).
 // XCD (A/B): blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md); XCD = true renumbers
 // them so that each XCD's blocks own consecutive waves (descriptor lines stay in one XCD's L2).
-template <int MODE, int PU, int U, int NT, int GRP, int SBW, bool XCD = false>
-__global__ __launch_bounds__(kBlock) void k_encode(EncArgs a, KeySched ks) {
+template <int MODE, int PU, int U, int NT, int GRP, int SBW, bool XCD, int TG>
+__device__ __forceinline__ void encode_grid(const EncArgs &a, const KeySched &ks) {
     __shared__ CopyRec recs[kWavesPerBlock][64];
     __shared__ uint32_t cend[kWavesPerBlock][64];
     stage_tags(ks);
@@ -875,9 +959,19 @@ __global__ __launch_bounds__(kBlock) void k_encode(EncArgs a, KeySched ks) {
     const uint64_t first = sb * SBW * 64u + wl * GRP;  // the wave's smallest packet
     if (first >= a.n) return;  // wave-uniform
     const uint64_t i = sb * SBW * 64u + ((uint64_t)(lane / GRP) * SBW + wl) * GRP + lane % GRP;
-    encode_set<MODE, PU, U, NT, GRP>(a, ks, i < a.n ? i : a.n, lane, recs[w], cend[w]);
+    encode_set<MODE, PU, U, NT, GRP, TG>(a, ks, i < a.n ? i : a.n, lane, recs[w], cend[w]);
 }
 
+template <int MODE, int PU, int U, int NT, int GRP, int SBW, bool XCD = false, int TG = 0>
+__global__ __launch_bounds__(kBlock) void k_encode(EncArgs a, KeySched ks) {
+    encode_grid<MODE, PU, U, NT, GRP, SBW, XCD, TG>(a, ks);
+}
+
+// the same kernel held to 128 VGPRs (4 waves per SIMD): W = 8 lets the compiler aim higher, W = 4 not
+template <int MODE, int PU, int U, int NT, int GRP, int SBW, int TG, int W>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, W))) void k_encode_w4(EncArgs a, KeySched ks) {
+    encode_grid<MODE, PU, U, NT, GRP, SBW, false, TG>(a, ks);
+}
 
 // ---------------------------------------------------------------------------------------------
 // Encode straight to wire packets (RConn::Output + RawTcp::SendRawTcp / libnet)
@@ -2703,12 +2797,15 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 // with the shipped copy; 47 = the unpipelined copy (MODE 6), 8 packets per iteration; 50 / 51 / 52 /
 // 55 = groups of <GRP, SBW> = <1, 1024> / <2, 1024> / <1, 256> / <1, 4096> (concurrent waves on
 // adjacent packets); 53 / 54 = <1, 1024> / <8, 1024> with XCD-contiguous block numbering; 56 = 0 with
-// the tag (payload[0] + MD5) in the copy loop for every per-packet set (MODE 10).  Rounds 1-2
+// the tag (payload[0] + MD5) in the copy loop for every per-packet set (MODE 10); 57 / 58 / 59 / 60 = 0
+// with the long-frame sets' tag prepass over 8 / 16 / 32 / 64 packets (tag_prepass); 61 / 62 = 56 (every
+// per-packet set in the copy-loop tag form) with the prepass over 16 / 32 packets; 63 / 64 = 0, 65 / 66 =
+// 58, 67 / 68 = 59 held to 4 waves per SIMD, amdgpu_waves_per_eu(4, 8) / (4, 4).  Rounds 1-2
 // measured ~45 more variants (profiles/r01_ab_*, r02_ab_*); their code is in the git history.
 // v + 100 * cap (cap 1..4): the same kernel held to `cap` blocks per CU by unused LDS.
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
     const int k = v % 100;
-    if (!c || v < 0 || v / 100 > 4 || !(k == 0 || k == 12 || k == 13 || k == 37 || k == 47 || (k >= 50 && k <= 56)))
+    if (!c || v < 0 || v / 100 > 4 || !(k == 0 || k == 12 || k == 13 || k == 37 || k == 47 || (k >= 50 && k <= 68)))
         return RSK_EINVAL;
     c->enc_variant = v;
     return RSK_OK;
@@ -2865,6 +2962,18 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         case 54: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024, true>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
         case 55: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 1, 4096>), dim3(enc_grid(n, 1, 4096)), bd, lds, st, a, c->ks); break;
         case 56: hipLaunchKernelGGL((k_encode<10, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
+        case 57: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024, false, 8>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
+        case 58: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024, false, 16>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
+        case 59: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024, false, 32>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
+        case 60: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024, false, 64>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
+        case 61: hipLaunchKernelGGL((k_encode<10, 4, 4, -1, 8, 1024, false, 16>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
+        case 62: hipLaunchKernelGGL((k_encode<10, 4, 4, -1, 8, 1024, false, 32>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
+        case 63: hipLaunchKernelGGL((k_encode_w4<11, 4, 4, -1, 8, 1024, 0, 8>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
+        case 64: hipLaunchKernelGGL((k_encode_w4<11, 4, 4, -1, 8, 1024, 0, 4>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
+        case 65: hipLaunchKernelGGL((k_encode_w4<11, 4, 4, -1, 8, 1024, 16, 8>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
+        case 66: hipLaunchKernelGGL((k_encode_w4<11, 4, 4, -1, 8, 1024, 16, 4>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
+        case 67: hipLaunchKernelGGL((k_encode_w4<11, 4, 4, -1, 8, 1024, 32, 8>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
+        case 68: hipLaunchKernelGGL((k_encode_w4<11, 4, 4, -1, 8, 1024, 32, 4>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
         default: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
     }
 #else

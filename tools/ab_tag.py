@@ -3,7 +3,7 @@
    python tools/ab_tag.py [--config c3] [--rounds 10] [--reps 10] [--modes md5,table]
 With the shipped library (default RSK_LIB=librsk.so): md5 = RSK_TAG_MD5 (MD5 per lane, round
 constants as instruction immediates: the headline), table = RSK_TAG_TABLE (the key's 256 tags staged
-in LDS, one ds_read_b64 per packet).  With RSK_LIB=librsk_ab.so (make -C rsock_amd ab), md5 = the MD5
+in LDS, one ds_read_b64 per packet).  With RSK_LIB=librsk_md5lds.so (make -C rsock_amd md5lds), md5 = the MD5
 per lane with its 64 round constants read from an LDS copy staged per block (the north star's "MD5
 round constants ... staged in LDS"); run the two libraries back to back in separate processes.
 Checks that every mode's frame arena and decode outputs are byte-identical, then prints per-mode
@@ -76,7 +76,7 @@ def main():
                 times[(m, k)].append(ev[0].elapsed_time(ev[1]) / args.reps)
     byts = int(enc_bytes_per_pkt(d.pay_len.astype(np.int64)).sum())
     lib = os.path.basename(rc._abi.LIB_PATH)
-    names = {"md5": "md5_consts_in_lds" if "ab" in lib else "md5_immediates", "table": "tag_table_lds"}
+    names = {"md5": "md5_consts_in_lds" if "md5lds" in lib else "md5_immediates", "table": "tag_table_lds"}
     out = {}
     for m in modes:
         te, td = np.array(times[(m, "enc")]), np.array(times[(m, "dec")])

@@ -23,6 +23,7 @@ def main():
                     help="wire packet pitch alignment (bytes); 0 = the frame slot rule (128 with PAD128 for "
                          "mixed lengths, else 16)")
     ap.add_argument("--wire-variants", default="", help="also time these rsk__set_wire_variant values (A/B)")
+    ap.add_argument("--only", default="", help="time only these paths (comma list), e.g. demux,demux_64conn")
     args = ap.parse_args()
     import torch
 
@@ -147,6 +148,9 @@ def main():
     tcp3, sdec = rc.TcpInfoBuffers.alloc(n, dev), rc.DecodeBuffers.alloc(n, dev)
     ops["syncinput_decode"] = lambda: cx.syncinput_batch(hand, hoff, hlen, tcp3, sdec, stream=s)
     nseg = [int(dmx.n_seg.item()), int(dmx64.n_seg.item())]
+    if args.only:
+        keep = args.only.split(",")
+        ops = {k: f for k, f in ops.items() if k in keep}
     times = {k: [] for k in ops}
     for _ in range(args.rounds):
         for k, f in ops.items():
@@ -183,7 +187,8 @@ def main():
     }
     cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, w.dec, stream=s)
     torch.cuda.synchronize()
-    assert torch.equal(sdec.status, w.dec.status) and torch.equal(sdec.n_valid, w.dec.n_valid)
+    if "syncinput_decode" in ops:
+        assert torch.equal(sdec.status, w.dec.status) and torch.equal(sdec.n_valid, w.dec.n_valid)
     out = {}
     for k, t in times.items():
         m = float(np.median(t))
