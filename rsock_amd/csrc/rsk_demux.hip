@@ -40,7 +40,10 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
-constexpr uint32_t kItems = 16;                 // radix: items per thread per tile
+#ifndef RSK_DM_ITEMS
+#define RSK_DM_ITEMS 16
+#endif
+constexpr uint32_t kItems = RSK_DM_ITEMS;       // radix: items per thread per tile (A/B builds: -DRSK_DM_ITEMS)
 constexpr uint32_t kTile = kBlock * kItems;     // 4096 packets per radix tile
 constexpr uint32_t kNone = 0xffffffffu;
 constexpr uint32_t kCtrl = 0xffffffffu;         // cep[] marker: control packet (singleton segment)

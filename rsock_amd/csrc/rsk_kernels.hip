@@ -67,7 +67,6 @@ struct EncArgs {
     uint32_t id_lo, id_hi;
     uint32_t n;
     uint32_t pad;  // log2 of the zero-pad granularity (4: RSK_ENC_ZERO_PAD16, 7: RSK_ENC_ZERO_PAD128), 0 = none
-    uint32_t tail0;  // k_encode with a tail (TS > 0): packets [tail0, n) go to small sets (enc_tail0)
 };
 
 __device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t j) {
@@ -155,7 +154,7 @@ struct Lane1 {
     bool slow;
 };
 
-template <bool TAG = true, bool ST = true>  // ST: store the status here (else the caller does)
+template <bool TAG = true>
 __device__ __forceinline__ Lane1 encode_phase1(const EncArgs &a, const KeySched &ks, uint64_t i) {
     Lane1 L;
     L.st = 0;
@@ -182,7 +181,7 @@ __device__ __forceinline__ Lane1 encode_phase1(const EncArgs &a, const KeySched 
             head_words(a.cmd[i], id0, id1, a.conv[i], a.conn_key[i], b0, L.H);
             L.slow = (reinterpret_cast<uintptr_t>(a.frame + L.fo) & 15u) != 0;
         }
-        if (ST) a.status[i] = L.st;
+        a.status[i] = L.st;
     }
     return L;
 }
@@ -801,28 +800,18 @@ constexpr uint32_t kDeferTagMeanBytes = 1024;
 // with the flat sets' tag in phase 1, 10 = 9 with the tag in the copy loop for every per-packet
 // set, 3 = tag always in phase 1, 7 = flat path only, 8 = per-packet path only.  NT < 0: store
 // policy per set.
-// TILE (the tail tiles of encode_grid): the wave runs phase 1 over the whole 64-packet set, then
-// frames only lanes [own_lo, own_lo + own_n) of a per-packet set, or the whole set if it is flat and
-// own_lo == 0 (a flat set with own_lo > 0 returns: the tile's first wave frames it).
-template <int MODE, int PU, int U, int NT, int GRP = 64, int TG = 0, bool TILE = false>
+template <int MODE, int PU, int U, int NT, int GRP = 64, int TG = 0>
 __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks, uint64_t i, uint32_t lane,
-                                           CopyRec *recs, uint32_t *cend, uint32_t own_lo = 0,
-                                           uint32_t own_n = 64) {
-    Lane1 L = encode_phase1<MODE == 3 || MODE == 7, !TILE>(a, ks, i);
+                                           CopyRec *recs, uint32_t *cend) {
+    Lane1 L = encode_phase1<MODE == 3 || MODE == 7>(a, ks, i);
     const bool vec = L.st > 0;  // every framed packet takes a vector path, at any alignment
-    uint64_t vm = __ballot(vec);
+    const uint64_t vm = __ballot(vec);
     // set mean frame length over framed packets (wave reduction)
     uint32_t fl = vec ? (uint32_t)L.st : 0u;
 #pragma unroll
     for (int off = 32; off; off >>= 1) fl += __shfl_xor(fl, off);
     const uint32_t cnt = (uint32_t)__popcll(vm);
     const bool flat = MODE == 7 ? true : MODE == 8 ? false : fl < kFlatBelowMeanBytes * cnt;
-    if constexpr (TILE) {
-        if (flat && own_lo != 0u) return;  // wave-uniform
-        const bool own = flat || (lane - own_lo < own_n);
-        if (own && i < a.n) a.status[i] = L.st;
-        if (!flat) vm &= __ballot(own);
-    }
     // MODE 10 (A/B): as 9 with the tag in the copy loop for every per-packet set
     const bool defer = MODE != 3 && MODE != 7 && !flat && (MODE == 10 || fl >= kDeferTagMeanBytes * cnt);
     // MODE 11 (A/B): as 9 with the flat sets' tag and header stores behind the first chunk loads
@@ -965,16 +954,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_tiled(EncArgs a, KeySched ks)
 // (profiles/r02_ab_encode_mapping.json).  The grid holds only waves that own a packet (enc_grid).
 // XCD (A/B): blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md); XCD = true renumbers
 // them so that each XCD's blocks own consecutive waves (descriptor lines stay in one XCD's L2).
-// Tail (TS > 0): the waves past the grouped-interleave region take packets [tail0, n) as 64-packet
-// tiles, 64 / TS waves per tile.  Workgroups start in index order, so these waves run last and fill
-// the SIMDs that the last generation of 64-packet waves leaves idle one by one (each of those copies
-// ~92 KB for C3: their end times spread over a whole wave's duration).  Every wave of a tile reads the
-// tile's 64 descriptors and takes the same decision: a tile of long frames (per-packet copy) is split,
-// wave j framing packets [TS j, TS j + TS) of it (lanes TS.. idle in phase 1); a tile of short frames
-// (flat copy: the wave's work is short anyway, and TS-packet flat sets waste lanes) is framed whole by
-// its first wave, the others return after phase 1 (encode_set TILE: the decision comes from the
-// phase-1 loads themselves, so no extra dependent load delays the kernel's last waves).
-template <int MODE, int PU, int U, int NT, int GRP, int SBW, bool XCD, int TG, int TS = 0>
+template <int MODE, int PU, int U, int NT, int GRP, int SBW, bool XCD, int TG>
 __device__ __forceinline__ void encode_grid(const EncArgs &a, const KeySched &ks) {
     __shared__ CopyRec recs[kWavesPerBlock][64];
     __shared__ uint32_t cend[kWavesPerBlock][64];
@@ -986,33 +966,16 @@ __device__ __forceinline__ void encode_grid(const EncArgs &a, const KeySched &ks
         if (blk < per * 8u) blk = (blk % 8u) * per + blk / 8u;
     }
     const uint64_t wg = (uint64_t)blk * kWavesPerBlock + w;
-    if constexpr (TS > 0) {
-        // waves of the interleaved region over [0, tail0) (as enc_grid: a partial last super-block
-        // holds the waves that own a packet)
-        const uint64_t per_sb = (uint64_t)SBW * 64u, rest = a.tail0 % per_sb;
-        const uint64_t big = a.tail0 / per_sb * SBW + std::min<uint64_t>(SBW, (rest + GRP - 1) / GRP);
-        if (wg >= big) {
-            constexpr uint32_t kSub = 64u / TS;
-            const uint64_t t = wg - big, tb = a.tail0 + t / kSub * 64u;
-            if (tb >= a.n) return;  // wave-uniform
-            const uint64_t ip = tb + lane;
-            encode_set<MODE, PU, U, NT, 64, TG, true>(a, ks, ip < a.n ? ip : a.n, lane, recs[w], cend[w],
-                                                      (uint32_t)(t % kSub) * TS, TS);
-            return;
-        }
-    }
-    EncArgs b = a;
-    if constexpr (TS > 0) b.n = a.tail0;
     const uint64_t sb = wg / SBW, wl = wg % SBW;
     const uint64_t first = sb * SBW * 64u + wl * GRP;  // the wave's smallest packet
-    if (first >= b.n) return;  // wave-uniform
+    if (first >= a.n) return;  // wave-uniform
     const uint64_t i = sb * SBW * 64u + ((uint64_t)(lane / GRP) * SBW + wl) * GRP + lane % GRP;
-    encode_set<MODE, PU, U, NT, GRP, TG>(b, ks, i < b.n ? i : b.n, lane, recs[w], cend[w]);
+    encode_set<MODE, PU, U, NT, GRP, TG>(a, ks, i < a.n ? i : a.n, lane, recs[w], cend[w]);
 }
 
-template <int MODE, int PU, int U, int NT, int GRP, int SBW, bool XCD = false, int TG = 0, int TS = 0>
+template <int MODE, int PU, int U, int NT, int GRP, int SBW, bool XCD = false, int TG = 0>
 __global__ __launch_bounds__(kBlock) void k_encode(EncArgs a, KeySched ks) {
-    encode_grid<MODE, PU, U, NT, GRP, SBW, XCD, TG, TS>(a, ks);
+    encode_grid<MODE, PU, U, NT, GRP, SBW, XCD, TG>(a, ks);
 }
 
 // the same kernel held to 128 VGPRs (4 waves per SIMD): W = 8 lets the compiler aim higher, W = 4 not
@@ -2829,18 +2792,6 @@ unsigned enc_grid(uint64_t n, uint32_t grp, uint32_t sbw) {
     const uint64_t waves = n / per_sb * sbw + std::min<uint64_t>(sbw, (rest + grp - 1) / grp);
     return (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
 }
-// First packet of the tail of a k_encode<.., TS> launch: the last `tail` packets, from a multiple of
-// 64; no tail for batches under two super-blocks (1024 waves x 64 packets) plus the tail.
-uint32_t enc_tail0(uint32_t n, uint32_t tail) {
-    if (n < 2u * 1024u * 64u + tail) return n;
-    return (n - tail) & ~63u;
-}
-unsigned enc_grid_tail(uint32_t n, uint32_t tail0, uint32_t ts) {
-    const uint64_t per_sb = 1024u * 64u, rest = tail0 % per_sb;
-    const uint64_t big = tail0 / per_sb * 1024u + std::min<uint64_t>(1024u, (rest + 7u) / 8u);
-    const uint64_t waves = big + ((uint64_t)(n - tail0) + 63u) / 64u * (64u / ts);
-    return (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
-}
 }  // namespace
 
 extern "C" {
@@ -2860,15 +2811,13 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 // the tag (payload[0] + MD5) in the copy loop for every per-packet set (MODE 10); 57 / 58 / 59 / 60 = 0
 // with the long-frame sets' tag prepass over 8 / 16 / 32 / 64 packets (tag_prepass); 61 / 62 = 56 (every
 // per-packet set in the copy-loop tag form) with the prepass over 16 / 32 packets; 63 / 64 = 0, 65 / 66 =
-// 58, 67 / 68 = 59 held to 4 waves per SIMD, amdgpu_waves_per_eu(4, 8) / (4, 4); 69..74 = 0 with a tail
-// of small sets (encode_grid TS; 69..83: sets of 8 / 16 / 8 / 16 / 8 / 32 / 8 / 4 / 8 / 16 / 8 / 8 /
-// 8 / 16 / 16 packets over the last 128K / 128K / 256K / 256K / 64K / 256K / 32K / 64K / 96K / 64K / 8K /
-// 4K / 16K / 32K / 16K packets).  Rounds 1-2
+// 58, 67 / 68 = 59 held to 4 waves per SIMD, amdgpu_waves_per_eu(4, 8) / (4, 4); tail shaping (small sets
+// for the last packets, round 3) in the git history (profiles/r03_ab_encode_tail.json).  Rounds 1-2
 // measured ~45 more variants (profiles/r01_ab_*, r02_ab_*); their code is in the git history.
 // v + 100 * cap (cap 1..4): the same kernel held to `cap` blocks per CU by unused LDS.
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
     const int k = v % 100;
-    if (!c || v < 0 || v / 100 > 4 || !(k == 0 || k == 12 || k == 13 || k == 37 || k == 47 || (k >= 50 && k <= 83)))
+    if (!c || v < 0 || v / 100 > 4 || !(k == 0 || k == 12 || k == 13 || k == 37 || k == 47 || (k >= 50 && k <= 68)))
         return RSK_EINVAL;
     c->enc_variant = v;
     return RSK_OK;
@@ -3004,7 +2953,6 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
     std::memcpy(&a.id_hi, in->id_uniform + 4, 4);
     a.n = n;
     a.pad = (out->flags & RSK_ENC_ZERO_PAD128) ? 7u : (out->flags & RSK_ENC_ZERO_PAD16) ? 4u : 0u;
-    a.tail0 = n;
     const uint64_t waves = (n + 63ull) / 64ull;
     const unsigned grid = (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
     hipStream_t st = (hipStream_t)stream;
@@ -3038,22 +2986,6 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         case 66: hipLaunchKernelGGL((k_encode_w4<11, 4, 4, -1, 8, 1024, 16, 4>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
         case 67: hipLaunchKernelGGL((k_encode_w4<11, 4, 4, -1, 8, 1024, 32, 8>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
         case 68: hipLaunchKernelGGL((k_encode_w4<11, 4, 4, -1, 8, 1024, 32, 4>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-        case 69: case 70: case 71: case 72: case 73: case 74: case 75: case 76: case 77: case 78: case 79: case 80:
-        case 81: case 82: case 83: {
-            // tail shaping: <TS, tail packets>
-            static const uint32_t tp[15] = {128u << 10, 128u << 10, 256u << 10, 256u << 10, 64u << 10, 256u << 10,
-                                            32u << 10,  64u << 10,  96u << 10,  64u << 10,  8u << 10,  4u << 10,
-                                            16u << 10,  32u << 10,  16u << 10};
-            static const uint32_t ts[15] = {8, 16, 8, 16, 8, 32, 8, 4, 8, 16, 8, 8, 8, 16, 16};
-            const int j = c->enc_variant % 100 - 69;
-            a.tail0 = enc_tail0(n, tp[j]);
-            const dim3 g2(enc_grid_tail(n, a.tail0, ts[j]));
-            if (ts[j] == 4) hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024, false, 0, 4>), g2, bd, lds, st, a, c->ks);
-            else if (ts[j] == 8) hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024, false, 0, 8>), g2, bd, lds, st, a, c->ks);
-            else if (ts[j] == 16) hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024, false, 0, 16>), g2, bd, lds, st, a, c->ks);
-            else hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024, false, 0, 32>), g2, bd, lds, st, a, c->ks);
-            break;
-        }
         default: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
     }
 #else
@@ -3085,7 +3017,6 @@ int rsk_encode_wire_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const
     std::memcpy(&a.id_hi, in->id_uniform + 4, 4);
     a.n = n;
     a.pad = (out->flags & RSK_ENC_ZERO_PAD128) ? 7u : (out->flags & RSK_ENC_ZERO_PAD16) ? 4u : 0u;
-    a.tail0 = n;
     WireArgs w;
     w.src = wire->src; w.dst = wire->dst; w.sp = wire->sp; w.dp = wire->dp; w.seq = wire->seq;
     w.ack = wire->ack; w.flag = wire->flag; w.ip_id = wire->ip_id;

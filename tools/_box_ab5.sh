@@ -4,7 +4,7 @@ set -o pipefail
 O=gpurun_out/${1:-r03l}
 mkdir -p $O
 for cfg in c3 c4 c2; do
-timeout -k 10 240 python tools/ab_encode.py --config $cfg --variants 0,73,75,81,80 --pads 16 --rounds 8 > $O/enc_$cfg.json 2>> $O/ab.err || { echo ab_encode failed; tail $O/ab.err; exit 1; }
+timeout -k 10 240 python tools/ab_encode.py --config $cfg --variants 0,300,75,84,85,86 --pads 16 --rounds 8 > $O/enc_$cfg.json 2>> $O/ab.err || { echo ab_encode failed; tail $O/ab.err; exit 1; }
 cat $O/enc_$cfg.json
 done
 cd /tmp && export TMPDIR=/tmp
