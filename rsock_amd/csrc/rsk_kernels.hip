@@ -3,17 +3,18 @@
 // Kernels (DESIGN.md §4 has the roofline and the algorithmic bytes of each):
 //   k_encode        RConn::Output framing (conn/RConn.cpp:87-105): per 64-packet set (8 groups of 8
 //                   consecutive packets, interleaved across 1024 waves), one lane per packet computes
-//                   status and the 31 header bytes (the tag from the key's 256-entry table, staged in
-//                   LDS); then, per wave, the software-pipelined per-packet copy (4-packet batches of
-//                   16-B chunks, one aligned payload load per chunk, funnel partner from the next lane
-//                   by DPP) or the flat chunk list for short frames.  The tiled mapping, the
+//                   status and the 31 header bytes (the tag: one MD5 compression per lane, or in
+//                   RSK_TAG_TABLE mode the key's 256-entry table staged in LDS); then, per wave,
+//                   the software-pipelined per-packet copy (4-packet batches of 16-B chunks, one
+//                   aligned payload load per chunk, funnel partner from the next lane by DPP) or
+//                   the flat chunk list for short frames.  The tiled mapping, the
 //                   unpipelined copy and k_copy_probe: A/B build only.
 //   k_encode_wire   RConn::Output + RawTcp::SendRawTcp (conn/RawTcp.cpp:280-341): frames plus the
 //                   IPv4/TCP headers and checksums libnet writes, two-launch hybrid.
 //   k_encode_hdr /  header-only framing / verification on 32-B slots (host-resident deployments:
 //   k_decode_hdr    the payload never crosses PCIe).
 //   k_decode        RConn::OnRecv (conn/RConn.cpp:64-85): one lane per frame, 32-B header window,
-//                   tag verify (LDS table), SoA field stores, per-wave VALID ballot for k_compact.
+//                   tag verify (MD5 per lane / LDS table), SoA field stores, per-wave VALID ballot for k_compact.
 //   k_parse_decode  RawTcp::RawInput (conn/RawTcp.cpp:138-244) fused with k_decode's body.
 //   k_capture_filter the pcap predicate of BuildFilterStr (cap/cap_util.cpp:67-144), SURVEY §8f-4.
 //   k_compact       order-stable VALID index list from the decode launches' per-wave ballots, one
