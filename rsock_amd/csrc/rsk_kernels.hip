@@ -844,10 +844,23 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
     // Measured (A/B, profiles/r02_ab_head.json): C3 2.34 vs 2.55 ms with the first; C4 0.389 vs
     // 0.420 ms with the second.
     if constexpr (MODE == 9 || MODE == 10 || MODE == 11) {  // software-pipelined per-packet copy (shipped: 9)
+        // Byte-packed long frames (no pad; a frame ends mid-chunk and the next packet's frame
+        // starts there): the TAG-form copy with the boundary-chunk merge (TailCarry), which writes
+        // each shared chunk as one 16-B store.  Only sets that really have such a pair take it: the
+        // carry costs ~8 % where nothing merges (C3 frames at odd offsets 0.769 -> 0.704 ms, C3
+        // slots without padding 0.682 -> 0.630 ms, gpurun_out/r03lay).  Short-frame sets keep
+        // their copy: the TAG form with the tag from phase 1 (TG = -1) was slower on C4's
+        // byte-packed frames (0.486 vs 0.466 ms).
+        bool mrg = false;
+        if (a.pad == 0u && defer) {
+            const uint64_t fe = reinterpret_cast<uintptr_t>(a.frame + L.fo) + (uint32_t)L.st;
+            const uint64_t nfo = (uint64_t)(uint32_t)__shfl_down((int)(uint32_t)L.fo, 1) |
+                                 ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(L.fo >> 32), 1) << 32);
+            const bool nvec = __shfl_down((int)vec, 1) != 0;
+            mrg = __ballot(vec && nvec && lane % GRP != GRP - 1u && (fe & 15u) != 0u &&
+                           reinterpret_cast<uintptr_t>(a.frame + nfo) == fe) != 0ull;
+        }
         if (defer) {
-            // byte-packed frames (no pad, some frame ends mid-chunk): the boundary-chunk merge
-            const bool mrg = a.pad == 0u &&
-                             __ballot(vec && ((reinterpret_cast<uintptr_t>(a.frame + L.fo) + (uint32_t)L.st) & 15u)) != 0ull;
             if (mrg) copy_pkt_pipe<PU, 0, true, TG, true>(a, ks, L, lane, vm);
             else if (nt) copy_pkt_pipe<PU, 2, true, TG>(a, ks, L, lane, vm);
             else copy_pkt_pipe<PU, 0, true, TG>(a, ks, L, lane, vm);
