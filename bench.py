@@ -21,7 +21,8 @@ to C5 (BASELINE configs[4]: 64M x 1400-B packets in total, contiguous shards, st
 N > 1: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set) this process is one rank;
 without a launcher, `--gpus N` starts the N rank processes itself (from this parent, which never
 touches the GPU) and relays rank 0's line.  No data-path collective: the only collectives are the
-timing barrier and the max over ranks.  Rank 0 prints ONE JSON line.
+timing barrier and the max over ranks, and both run over gloo on the CPU by default (RCCL is not
+used: --dist-backend nccl is opt-in).  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -225,7 +226,10 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1 << 20)
     ap.add_argument("--cpu-seconds", type=float, default=6.0)
-    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal)")
+    ap.add_argument("--dist-backend", default="gloo",
+                    help="gloo (default): the ranks exchange only the timing barrier and one float, on the CPU; "
+                         "nccl (= RCCL, opt-in): the same two operations over the GPUs. There is no "
+                         "data-path collective either way (SURVEY.md §8e)")
     ap.add_argument("--eager", action="store_true",
                     help="launch the step's kernels one by one in the timed region instead of replaying a "
                          "captured HIP graph of the step")

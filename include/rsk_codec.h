@@ -147,14 +147,17 @@ int rsk_reserve_stream(rsk_ctx *ctx, uint32_t n_max, void *stream);
  * stream whose handle value a later stream may reuse).  A batch call issued while `stream` is being
  * captured into a hipGraph cannot allocate, grow or initialise that scratch (RSK_EINVAL): reserve
  * the stream and run one eager call on it before the capture.  A graph's scratch is its capture
- * stream's: replay it on that stream, or on streams ordered with it. */
+ * stream's: replay it on that stream, or on streams ordered with it.  Graphs captured on `stream`
+ * point at that scratch: destroy them before rsk_release_stream (a replay afterwards would use freed
+ * device memory). */
 int rsk_release_stream(rsk_ctx *ctx, void *stream);
 
 /* Device-side error flags, sticky per context.  RSK_DEVERR_LOOKBACK: a decoupled look-back (the
  * VALID-list compaction of the decode entry points, the demux) gave up waiting for a predecessor
- * tile after ~4M polls, so that call's valid_idx / n_valid / demux outputs are wrong (the stalled
- * compaction tile also writes n_valid = 0xFFFFFFFF); the spin limit exists so that such a stall can
- * never hang the GPU.  rsk_check_device_errors waits for the device, stores the flags in *flags
+ * tile after ~4M polls, so that call's valid_idx / n_valid / demux outputs are wrong (a compaction
+ * that gave up anywhere writes n_valid = 0xFFFFFFFF); the spin limit exists so that such a stall can
+ * never hang the GPU.  rsk_check_device_errors waits for the context's streams (those it has
+ * scratch on, and its shim stream; not the whole device), stores the flags in *flags
  * (may be NULL) and clears them; when any flag was set it returns RSK_EDEVICE and re-initialises
  * the context's look-back state on every stream at its next call there (graphs captured earlier
  * must be captured again). */

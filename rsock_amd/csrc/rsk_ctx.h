@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <array>
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <mutex>
@@ -42,7 +43,9 @@ struct rsk_ctx {
     ShimIO *shim_dev = nullptr;
     uint2 *tag_dev = nullptr;  // 256-entry tag table (rsk::KeySched::tab)
     uint32_t *err_dev = nullptr;  // sticky device error flags (RSK_DEVERR_*, rsk_check_device_errors)
-    uint32_t compact_stall_tile = ~0u;  // see rsk__inject_compact_stall (tests)
+    // see rsk__inject_compact_stall (tests): consumed by exchange, so host threads driving one
+    // context on several streams never race on it
+    std::atomic<uint32_t> compact_stall_tile{~0u};
     ShimIO *shim_host = nullptr;
     hipStream_t shim_stream = nullptr;
     std::mutex shim_mu;
@@ -149,7 +152,24 @@ inline void invalidate_compact(rsk_ctx *c) {
     for (auto &kv : c->ws) kv.second[WS_COMPACT].zeroed = false;
 }
 
-// Sync s, then free its scratch (rsk_release_stream).
+// Sync every stream this context has scratch on (the streams its look-back kernels ran on) and its
+// shim stream: rsk_check_device_errors waits for the context's own work only, not the device.
+inline hipError_t sync_ctx_streams(rsk_ctx *c) {
+    std::vector<hipStream_t> ss;
+    {
+        std::lock_guard<std::mutex> lk(c->ws_mu);
+        for (auto &kv : c->ws) ss.push_back(kv.first);
+    }
+    if (c->shim_stream) ss.push_back(c->shim_stream);
+    for (hipStream_t s : ss) {
+        hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+// Sync s, then free its scratch (rsk_release_stream).  Graphs captured on s point at that scratch:
+// they must be destroyed first (rsk_codec.h, rsk_release_stream).
 inline int release_ws(rsk_ctx *c, hipStream_t s) {
     std::lock_guard<std::mutex> lk(c->ws_mu);
     auto it = c->ws.find(s);

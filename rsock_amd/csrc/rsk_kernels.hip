@@ -2004,18 +2004,25 @@ __device__ __forceinline__ void store_dec(const DecOut &d, uint64_t i, const Dec
 // it counts them, scans them in one wave, finds the tile's prefix by decoupled look-back over the
 // tiles before it, and its lanes write their indices at prefix + rank (valid_idx in index order).
 // Tiles are dispatched in index order, so a tile only waits for tiles that are resident or done.
-// State word per tile: bits 63..33 the call's epoch, bit 32 inclusive, bits 31..0 the count; a
-// word from another call is not ready, so the state needs no per-call reset.  The epoch is a
-// device-side counter (workspace word 0) that every tile reads first and the last tile advances
-// when it is done — by then every tile has published (the inclusive chain reaches tile 0), so all
+// State word per tile: bits 63..34 the call's epoch, bit 33 taint, bit 32 inclusive, bits 31..0
+// the count; a word from another call is not ready, so the state needs no per-call reset.  The
+// epoch is a device-side counter (workspace word 0) that every tile reads first and the last tile
+// advances when every tile has published its inclusive word (it checks them all, below), so all
 // read the same value; the next call on the stream, or the next replay of a captured graph, sees
-// the next epoch.  Epochs run 1 .. 2^31 - 1 (0 is the zeroed state).  Device-scope relaxed
+// the next epoch.  Epochs run 1 .. 2^30 - 1 (0 is the zeroed state).  Device-scope relaxed
 // atomics (acquire / release would add an L2 write-back / invalidate per access, rsk_demux.hip);
 // a spin that outlives kCmpSpinMax reads gives up (no hang): it sets RSK_DEVERR_LOOKBACK in the
-// context's sticky error word and the tile poisons n_valid (rsk_check_device_errors).  Round 1 used k_scan (one
+// context's sticky error word and publishes its inclusive word with the taint bit.  The last tile
+// waits for every tile's inclusive word of this epoch and writes n_valid = 0xFFFFFFFF instead of the
+// count when one is tainted or never arrives, so a wrong VALID list never comes with a count that
+// looks valid, whichever tile gave up and whenever (rsk_check_device_errors).  The
+// information travels in the words themselves, so relaxed atomics order it.  Round 1 used k_scan (one
 // workgroup) + k_scatter; a look-back inside the decode launch itself (one word per 256-packet
 // block) was measured slower than both (C2: 40 us vs 31): the block-granular chain is the cost.
 constexpr unsigned long long kCmpIncl = 1ull << 32;
+constexpr unsigned long long kCmpTaint = 1ull << 33;
+constexpr int kCmpEpochShift = 34;
+constexpr uint32_t kCmpEpochMod = 0x3fffffffu;  // epochs 1 .. 2^30 - 1
 constexpr uint32_t kCmpSpinMax = 1u << 22;
 
 __device__ __forceinline__ unsigned long long cmp_wait(unsigned long long *s, uint32_t epoch, bool &timed_out) {
@@ -2023,17 +2030,28 @@ __device__ __forceinline__ unsigned long long cmp_wait(unsigned long long *s, ui
     uint32_t spins = 0;
     do {
         v = __hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } while ((uint32_t)(v >> 33) != epoch && ++spins < kCmpSpinMax);
-    if ((uint32_t)(v >> 33) == epoch) return v;
+    } while ((uint32_t)(v >> kCmpEpochShift) != epoch && ++spins < kCmpSpinMax);
+    if ((uint32_t)(v >> kCmpEpochShift) == epoch) return v;
     timed_out = true;
     return kCmpIncl;
+}
+
+// the same for a word that must be INCLUSIVE for this epoch (the last tile's check); false when it
+// never became so or carries the taint
+__device__ __forceinline__ bool cmp_wait_incl_clean(unsigned long long *s, uint32_t epoch) {
+    unsigned long long v;
+    uint32_t spins = 0;
+    do {
+        v = __hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } while (((uint32_t)(v >> kCmpEpochShift) != epoch || !(v & kCmpIncl)) && ++spins < kCmpSpinMax);
+    return (uint32_t)(v >> kCmpEpochShift) == epoch && (v & kCmpIncl) && !(v & kCmpTaint);
 }
 
 // all 64 lanes of one wave of tile b; agg uniform; returns b's exclusive prefix (uniform); `to`
 // (uniform) is set when a predecessor's word never arrived
 __device__ uint32_t cmp_lookback(unsigned long long *st, uint32_t b, uint32_t agg, uint32_t lane, uint32_t epoch,
                                  bool &to) {
-    const unsigned long long tag = (unsigned long long)epoch << 33;
+    const unsigned long long tag = (unsigned long long)epoch << kCmpEpochShift;
     if (b == 0u) {
         if (lane == 0u) __hip_atomic_store(st, tag | kCmpIncl | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return 0u;
@@ -2053,8 +2071,9 @@ __device__ uint32_t cmp_lookback(unsigned long long *st, uint32_t b, uint32_t ag
         excl += val;
         if (im) break;
     }
-    if (lane == 0u)
-        __hip_atomic_store(st + b, tag | kCmpIncl | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0u)  // a tile that gave up publishes its (wrong) prefix with the taint bit
+        __hip_atomic_store(st + b, tag | kCmpIncl | (to ? kCmpTaint : 0ull) | (excl + agg), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     return excl;
 }
 
@@ -2501,12 +2520,13 @@ __global__ __launch_bounds__(kBlock) void k_compact(const uint64_t *masks, uint3
                                                     uint32_t stall_tile) {
     __shared__ uint64_t ms[64];
     __shared__ uint32_t mex[64];
-    __shared__ uint32_t pre;
+    __shared__ uint32_t pre, s_agg, s_epoch, s_to;
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     const uint64_t mb = (uint64_t)blockIdx.x * 64u;
+    const bool last = blockIdx.x == gridDim.x - 1u;
     if (w == 0u) {
         const uint32_t e0 = (uint32_t)__hip_atomic_load(st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t epoch = e0 % 0x7fffffffu + 1u;
+        const uint32_t epoch = e0 % kCmpEpochMod + 1u;
         const uint64_t m = mb + lane < nw ? masks[mb + lane] : 0ull;
         const uint32_t c = (uint32_t)__popcll(m);
         uint32_t inc = c;
@@ -2524,17 +2544,28 @@ __global__ __launch_bounds__(kBlock) void k_compact(const uint64_t *masks, uint3
         const uint32_t p = blockIdx.x == stall_tile ? 0u : cmp_lookback(st + 1, blockIdx.x, agg, lane, epoch, to);
         if (lane == 0u) {
             pre = p;
-            if (blockIdx.x == gridDim.x - 1u) {  // every tile has read the epoch (see above)
-                if (n_valid) *n_valid = p + agg;
-                __hip_atomic_store(st, (unsigned long long)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            if (to) {  // wrong prefix: flag it (sticky) and poison the count
-                __hip_atomic_fetch_or(err, RSK_DEVERR_LOOKBACK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (n_valid) __hip_atomic_store(n_valid, 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
+            s_agg = agg;
+            s_epoch = epoch;
+            s_to = to ? 1u : 0u;
+            // wrong prefix: flag it (sticky); the last tile poisons the count (below)
+            if (to) __hip_atomic_fetch_or(err, RSK_DEVERR_LOOKBACK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     __syncthreads();
+    if (last && blockIdx.x != stall_tile) {
+        // every earlier tile's word must be inclusive, of this epoch and untainted; the block's 256
+        // threads poll them in parallel (bounded, as every spin here).  Only then is the count
+        // trustworthy and the epoch advanced: every tile has read it by then.
+        bool bad = s_to != 0u;
+        for (uint32_t j = t; j + 1u < gridDim.x; j += kBlock)
+            if (!cmp_wait_incl_clean(st + 1 + j, s_epoch)) bad = true;
+        bad = __syncthreads_or(bad);
+        if (t == 0u) {
+            if (n_valid) *n_valid = bad ? 0xFFFFFFFFu : pre + s_agg;
+            if (bad) __hip_atomic_fetch_or(err, RSK_DEVERR_LOOKBACK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(st, (unsigned long long)s_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
     if (!valid_idx) return;
 #pragma unroll 4
     for (uint32_t r = 0; r < 16u; ++r) {
@@ -2754,8 +2785,7 @@ int ensure_compact(rsk_ctx *c, uint32_t n, hipStream_t s, Compact &k) {
 }
 
 int run_compaction(rsk_ctx *c, const Compact &k, uint32_t *valid_idx, uint32_t *n_valid, hipStream_t s) {
-    const uint32_t stall = c->compact_stall_tile;
-    c->compact_stall_tile = ~0u;
+    const uint32_t stall = c->compact_stall_tile.exchange(~0u, std::memory_order_relaxed);
     hipLaunchKernelGGL(k_compact, dim3(k.ntiles), dim3(kBlock), 0, s, k.masks, k.nw, k.st, valid_idx, n_valid,
                        c->err_dev, stall);
     return launch_check("k_compact");
@@ -2930,7 +2960,9 @@ int rsk_check_device_errors(rsk_ctx *c, uint32_t *flags) {
     DeviceGuard g(c->device);
     if (!g.ok) return RSK_EDEVICE;
     uint32_t f = 0;
-    hipError_t e = hipDeviceSynchronize();
+    // the context's streams only: the flags are raised by look-back kernels, which run on
+    // streams the context has scratch for; other contexts' and torch's work is not waited for
+    hipError_t e = rsk::sync_ctx_streams(c);
     if (e == hipSuccess) e = hipMemcpy(&f, c->err_dev, sizeof f, hipMemcpyDeviceToHost);
     if (e == hipSuccess && f) e = hipMemset(c->err_dev, 0, sizeof f);
     if (e != hipSuccess) { set_error("rsk_check_device_errors", e); return RSK_EDEVICE; }

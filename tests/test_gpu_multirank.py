@@ -31,8 +31,10 @@ def _free_port():
 
 
 def test_bench_self_launches_two_ranks(gpu):
+    # no --dist-backend: the default the driver's multi-GPU run takes (gloo; bench.py never uses RCCL
+    # unless asked)
     cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--same-device",
-           "--dist-backend", "gloo", "--config", "c5", "--packets", str(1 << 16), "--steps", "3", "--warmup", "1"]
+           "--config", "c5", "--packets", str(1 << 16), "--steps", "3", "--warmup", "1"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

@@ -75,8 +75,8 @@ def assert_dec_equal(got: dict, exp: dict):
 
 
 # ---- configs (reduced n) ----------------------------------------------------------------------
-# the last three sizes are past two super-blocks + the tail, so k_encode frames their last packets in
-# the tail tiles (encode_grid TS): C3 / C4 long-frame tiles split across waves, C2 flat tiles, C4 both
+# the last three sizes are past two super-blocks (65,536 packets each) and end in a partial one, so
+# k_encode's last waves own fewer than 64 packets: C3 / C4 long-frame sets, C2 flat sets, C4 both
 @pytest.mark.parametrize("cfg,n", [("c2", 100_000), ("c3", 20_000), ("c4", 50_000),
                                    ("c3", 170_001), ("c4", 196_613), ("c2", 200_003)])
 def test_config_roundtrip_bitexact(vcodec, gpu, oracle, cfg, n):

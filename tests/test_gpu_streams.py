@@ -172,6 +172,8 @@ def test_compaction_stall_is_flagged_and_recovered(gpu):
         fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
         assert fn(cx._ctx, 1) == 0
         assert not decode_and_check()  # tiles 2.. took a wrong prefix
+        # the count is poisoned whatever tile gave up (the last tile checks every word)
+        assert int(o.n_valid.item()) & 0xFFFFFFFF == 0xFFFFFFFF  # int32 storage of the u32
         with pytest.raises(RskError, match="0x1"):
             cx.check_device_errors()
         assert cx.check_device_errors() == 0  # read and cleared
