@@ -128,7 +128,7 @@ __device__ __forceinline__ void tag_of(const KeySched &ks, uint32_t b, uint32_t 
 #ifdef RSK_MD5_K_LDS
     rsk::md5_tag(ks, b & 255u, t0, t1, KLds());
 #else
-    rsk::md5_tag(ks, b & 255u, t0, t1);
+    rsk::md5_tag_lane(ks, b & 255u, t0, t1);
 #endif
 }
 
@@ -957,6 +957,242 @@ __global__ __launch_bounds__(kBlock) void k_encode_tiled(EncArgs a, KeySched ks)
     }
 }
 
+#endif  // RSK_AB
+
+#ifdef RSK_AB
+// A/B build only (round 4): block-cooperative copy.  A block of 16 waves owns 16 * PPW consecutive
+// packets; each wave copies PPW of them (packet base + w + 16 p), one frame per wave-slot pair, and
+// the block's waves are short-lived, so the chip streams a compact window of the arenas (the
+// one-shot 1-KB-per-wave copy is this chip's fastest copy shape, profiles/r01_hbm_probe.json) instead
+// of ~4 K long-lived waves each streaming its own 64-packet set.  The MD5 stays per lane: wave 0's
+// lanes run phase 1 (descriptors, payload[0], tag, header words) for the block's packets while the
+// other waves already have their chunk loads in flight, and hand the header words over in LDS (one
+// block barrier between the loads and the stores).
+template <int PPW, int NT>
+__global__ __launch_bounds__(1024) void k_encode_bc(EncArgs a, KeySched ks) {
+    constexpr int NP = 16 * PPW;
+    __shared__ uint32_t s_h[NP][9];  // header words of the block's packets (+1: no bank conflicts)
+    if (ks.tag_mode == RSK_TAG_TABLE) {
+        if (threadIdx.x < 256u) s_tags[threadIdx.x] = ks.tab[threadIdx.x];
+        __syncthreads();
+    }
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint64_t base = (uint64_t)blockIdx.x * NP;
+    // per wave: its packets' geometry and chunk loads (descriptor loads at a uniform index: scalar)
+    uint4 A[PPW][2];
+    FrameGeo G[PPW];
+    uint32_t fl[PPW];
+#pragma unroll
+    for (int p = 0; p < PPW; ++p) {
+        const uint64_t i = base + w + 16u * p;
+        fl[p] = 0;
+        A[p][0] = A[p][1] = make_uint4(0u, 0u, 0u, 0u);
+        if (i >= a.n) continue;
+        const uint32_t P = a.pay_len[i];
+        if (P == 0u || P > (uint32_t)RSK_MAX_PAYLOAD) continue;
+        fl[p] = RSK_HEAD_SIZE + P;
+        G[p] = frame_geo(a.payload + a.pay_off[i], a.frame + a.frame_off[i], fl[p], a.pad);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            if (q == 1 && G[p].nst < 64u) continue;  // uniform
+            const int32_t m = (int32_t)(lane + 64u * q) - 2;
+            if (m >= 0 && src_chunk_live(m, G[p].first_rel, G[p].last_rel)) A[p][q] = ld16<NT>(G[p].srcp + 16 * m);
+        }
+    }
+    if (w == 0u) {  // phase 1 of the block's packets, one lane each (status written here)
+        const uint64_t i = lane < (uint32_t)NP && base + lane < a.n ? base + lane : a.n;
+        const Lane1 L = encode_phase1<true>(a, ks, i);
+        if (lane < (uint32_t)NP) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) s_h[lane][t] = L.H[t];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < PPW; ++p) {
+        if (fl[p] == 0u) continue;  // uniform
+        const uint32_t j = w + 16u * p;
+        uint32_t Hj[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) Hj[t] = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_h[j][t]);
+        const FrameGeo &g = G[p];
+        const uint32_t flen = fl[p] + g.r, nst = g.nst;
+        uint4 B[2];
+        B[0] = make_uint4(wave_shl1(A[p][0].x), wave_shl1(A[p][0].y), wave_shl1(A[p][0].z), wave_shl1(A[p][0].w));
+        B[1] = make_uint4(0u, 0u, 0u, 0u);
+        if (nst >= 64u) {
+            const uint4 l0 = rdl4(A[p][1], 0);
+            if (lane == 63u) B[0] = l0;
+            if (nst > 64u)
+                B[1] = make_uint4(wave_shl1(A[p][1].x), wave_shl1(A[p][1].y), wave_shl1(A[p][1].z),
+                                  wave_shl1(A[p][1].w));
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const uint32_t k = lane + 64u * q;
+            if (q == 1 && nst <= 64u) continue;  // uniform
+            const uint4 V = rsk::funnel16(A[p][q], B[q], g.sh);
+            const uint4 v = k < (g.r >= 2u ? 3u : 2u) ? head_chunk(Hj, k, g.r, V) : V;
+            if (k >= nst) continue;
+            store_piece<NT>(g.d0 + 16u * k, v, k == 0u ? g.r : 0u, (int)flen - 16 * (int)k, a.pad != 0u);
+        }
+    }
+}
+#endif  // RSK_AB
+
+#ifdef RSK_AB
+// A/B build only (round 4): the two-pass form.  Pass A (k_enc_heads): phase 1 one lane per packet,
+// the 8 header words into a 32-B-per-packet workspace (+ status).  Pass B (k_enc_copy1): one wave per
+// packet and nothing else -- descriptors and header words by scalar loads, the packet's chunk loads,
+// funnel and stores -- so waves are short-lived and independent (no barrier, no MD5 in the copy).
+__global__ __launch_bounds__(kBlock) void k_enc_heads(EncArgs a, KeySched ks, uint4 *heads) {
+    stage_tags(ks);
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const Lane1 L = encode_phase1<true>(a, ks, i < a.n ? i : a.n);
+    if (i < a.n && L.st > 0) {
+        heads[2 * i] = make_uint4(L.H[0], L.H[1], L.H[2], L.H[3]);
+        heads[2 * i + 1] = make_uint4(L.H[4], L.H[5], L.H[6], L.H[7]);
+    }
+}
+
+template <int NT>
+__global__ __launch_bounds__(kBlock) void k_enc_copy1(EncArgs a, const uint32_t *heads) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint64_t i = (uint64_t)blockIdx.x * kWavesPerBlock + w;
+    if (i >= a.n) return;
+    const uint32_t P = a.pay_len[i];
+    if (P == 0u || P > (uint32_t)RSK_MAX_PAYLOAD) return;
+    const uint32_t fl = RSK_HEAD_SIZE + P;
+    const FrameGeo g = frame_geo(a.payload + a.pay_off[i], a.frame + a.frame_off[i], fl, a.pad);
+    uint4 A[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        A[q] = make_uint4(0u, 0u, 0u, 0u);
+        if (q == 1 && g.nst < 64u) continue;  // uniform
+        const int32_t m = (int32_t)(lane + 64u * q) - 2;
+        if (m >= 0 && src_chunk_live(m, g.first_rel, g.last_rel)) A[q] = ld16<NT>(g.srcp + 16 * m);
+    }
+    uint32_t Hj[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) Hj[t] = heads[8 * i + t];  // uniform address: scalar loads
+    const uint32_t flen = fl + g.r, nst = g.nst;
+    uint4 B[2];
+    B[0] = make_uint4(wave_shl1(A[0].x), wave_shl1(A[0].y), wave_shl1(A[0].z), wave_shl1(A[0].w));
+    B[1] = make_uint4(0u, 0u, 0u, 0u);
+    if (nst >= 64u) {
+        const uint4 l0 = rdl4(A[1], 0);
+        if (lane == 63u) B[0] = l0;
+        if (nst > 64u) B[1] = make_uint4(wave_shl1(A[1].x), wave_shl1(A[1].y), wave_shl1(A[1].z), wave_shl1(A[1].w));
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const uint32_t k = lane + 64u * q;
+        if (q == 1 && nst <= 64u) continue;  // uniform
+        const uint4 V = rsk::funnel16(A[q], B[q], g.sh);
+        const uint4 v = k < (g.r >= 2u ? 3u : 2u) ? head_chunk(Hj, k, g.r, V) : V;
+        if (k >= nst) continue;
+        store_piece<NT>(g.d0 + 16u * k, v, k == 0u ? g.r : 0u, (int)flen - 16 * (int)k, a.pad != 0u);
+    }
+}
+
+// A/B build only (round 4): memory-pattern probes for C3's ceiling (wrong bytes: aligned source
+// chunk k -> aligned frame chunk k, no funnel, header or tag).  GI: the shipped grouped-interleave
+// mapping and 4-packet pipelined batches; ONE: one wave per packet.
+__device__ __forceinline__ void probe_geo(const EncArgs &a, uint64_t po, uint64_t fo, uint32_t P, const uint8_t *&src,
+                                          uint8_t *&dst, uint32_t &nsrc, uint32_t &nch) {
+    const uintptr_t s0 = reinterpret_cast<uintptr_t>(a.payload + po), d0 = reinterpret_cast<uintptr_t>(a.frame + fo);
+    nsrc = (uint32_t)(((s0 & 15u) + P + 15u) >> 4);
+    nch = (uint32_t)(((d0 & 15u) + P + RSK_HEAD_SIZE + 15u) >> 4);
+    src = reinterpret_cast<const uint8_t *>(s0 & ~(uintptr_t)15);
+    dst = reinterpret_cast<uint8_t *>(d0 & ~(uintptr_t)15);
+}
+
+__global__ __launch_bounds__(kBlock) void k_probe_one(EncArgs a) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint64_t i = (uint64_t)blockIdx.x * kWavesPerBlock + w;
+    if (i >= a.n) return;
+    const uint32_t P = a.pay_len[i];
+    if (P == 0u || P > (uint32_t)RSK_MAX_PAYLOAD) return;
+    const uint8_t *src;
+    uint8_t *dst;
+    uint32_t nsrc, nch;
+    probe_geo(a, a.pay_off[i], a.frame_off[i], P, src, dst, nsrc, nch);
+    uint4 A[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const uint32_t k = lane + 64u * q;
+        A[q] = make_uint4(0u, 0u, 0u, 0u);
+        if (k < nsrc) A[q] = ld16<0>(src + 16u * k);
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const uint32_t k = lane + 64u * q;
+        if (k < nch) st16<0>(dst + 16u * k, A[q]);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_probe_gi(EncArgs a) {
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint64_t wg = (uint64_t)blockIdx.x * kWavesPerBlock + w;
+    const uint64_t sb = wg / 1024u, wl = wg % 1024u;
+    if (sb * 1024u * 64u + wl * 8u >= a.n) return;
+    const uint64_t i = sb * 1024u * 64u + ((uint64_t)(lane / 8u) * 1024u + wl) * 8u + lane % 8u;
+    uint64_t po = 0, fo = 0;
+    uint32_t P = 0;
+    if (i < a.n) {
+        po = a.pay_off[i];
+        fo = a.frame_off[i];
+        P = a.pay_len[i];
+        a.status[i] = (int32_t)(RSK_HEAD_SIZE + P);
+    }
+    uint64_t vm = __ballot(i < a.n && P > 0u && P <= (uint32_t)RSK_MAX_PAYLOAD);
+    constexpr int PU = 4;
+    uint4 A0[PU][2], A1[PU][2];
+    uint8_t *d0[PU], *d1[PU];
+    uint32_t n0[PU], n1[PU];
+    auto issue = [&](uint64_t bm, uint4 (&A)[PU][2], uint8_t *(&dd)[PU], uint32_t (&nn)[PU]) {
+#pragma unroll
+        for (int p = 0; p < PU; ++p) {
+            const bool on = bm != 0ull;
+            const uint32_t j = on ? (uint32_t)__builtin_ctzll(bm) : 0u;
+            if (on) bm &= bm - 1ull;
+            const uint8_t *src;
+            uint32_t nsrc;
+            probe_geo(a, rdl64(po, j), rdl64(fo, j), rdl(P, j), src, dd[p], nsrc, nn[p]);
+            if (!on) nn[p] = 0u, nsrc = 0u;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const uint32_t k = lane + 64u * q;
+                A[p][q] = ld16<0>(k < nsrc ? src + 16u * k : src);
+            }
+        }
+    };
+    auto store = [&](const uint4 (&A)[PU][2], uint8_t *const (&dd)[PU], const uint32_t (&nn)[PU]) {
+#pragma unroll
+        for (int p = 0; p < PU; ++p)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const uint32_t k = lane + 64u * q;
+                if (k < nn[p]) st16<0>(dd[p] + 16u * k, A[p][q]);
+            }
+    };
+    uint64_t cur = take_batch<PU>(vm);
+    if (!cur) return;
+    issue(cur, A0, d0, n0);
+    while (true) {
+        const uint64_t nxt = take_batch<PU>(vm);
+        if (nxt) issue(nxt, A1, d1, n1);
+        store(A0, d0, n0);
+        if (!nxt) break;
+        cur = take_batch<PU>(vm);
+        if (cur) issue(cur, A0, d0, n0);
+        store(A1, d1, n1);
+        if (!cur) break;
+    }
+}
 #endif  // RSK_AB
 
 // Grouped-interleave mapping (shipped: GRP 8, SBW 1024).  A super-block of SBW consecutive waves owns
@@ -2751,6 +2987,7 @@ void build_sched(const uint8_t *key, uint32_t klen, KeySched &ks) {
     ks.bword = (int32_t)(rem / 4u);
     ks.bshift = (int32_t)(8u * (rem % 4u));
     ks.two_blocks = two ? 1 : 0;
+    rsk::md5_prefix_steps(ks.mid, ks.blk, ks.bword, ks.pre);  // rsk::md5_tag_bw starts at step bword
 }
 
 inline unsigned grid_for(uint64_t threads) { return (unsigned)((threads + kBlock - 1) / kBlock); }
@@ -2856,12 +3093,16 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 // with the long-frame sets' tag prepass over 8 / 16 / 32 / 64 packets (tag_prepass); 61 / 62 = 56 (every
 // per-packet set in the copy-loop tag form) with the prepass over 16 / 32 packets; 63 / 64 = 0, 65 / 66 =
 // 58, 67 / 68 = 59 held to 4 waves per SIMD, amdgpu_waves_per_eu(4, 8) / (4, 4); tail shaping (small sets
-// for the last packets, round 3) in the git history (profiles/r03_ab_encode_tail.json).  Rounds 1-2
+// for the last packets, round 3) in the git history (profiles/r03_ab_encode_tail.json); 69 / 70 / 71 =
+// the block-cooperative copy k_encode_bc (16 waves per block, 1 / 2 / 4 packets per wave), 72 = 69 with
+// nontemporal stores; 73 / 74 = memory-pattern probes (wrong bytes: k_probe_gi, the shipped mapping and
+// batches; k_probe_one, one wave per packet); 75 / 76 = the two-pass form (k_enc_heads then
+// k_enc_copy1, normal / nontemporal stores) (round 4).  Rounds 1-2
 // measured ~45 more variants (profiles/r01_ab_*, r02_ab_*); their code is in the git history.
 // v + 100 * cap (cap 1..4): the same kernel held to `cap` blocks per CU by unused LDS.
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
     const int k = v % 100;
-    if (!c || v < 0 || v / 100 > 4 || !(k == 0 || k == 12 || k == 13 || k == 37 || k == 47 || (k >= 50 && k <= 68)))
+    if (!c || v < 0 || v / 100 > 4 || !(k == 0 || k == 12 || k == 13 || k == 37 || k == 47 || (k >= 50 && k <= 76)))
         return RSK_EINVAL;
     c->enc_variant = v;
     return RSK_OK;
@@ -2955,6 +3196,17 @@ int rsk__inject_compact_stall(rsk_ctx *c, uint32_t tile) {
     return RSK_OK;
 }
 
+// Internal (CPU tests): the per-lane tag path of the device kernels (KeySched from build_sched,
+// rsk::md5_tag_lane: the payload-word-specialised step schedule starting from KeySched::pre) run on
+// the host, so its schedule is checked against the oracle without a GPU.
+int rsk__host_tag(const uint8_t *key, uint32_t key_len, uint32_t b, uint32_t *t01) {
+    if ((!key && key_len) || !t01 || b > 255u) return RSK_EINVAL;
+    KeySched ks;
+    build_sched(key, key_len, ks);
+    rsk::md5_tag_lane(ks, b, t01[0], t01[1]);
+    return RSK_OK;
+}
+
 int rsk_check_device_errors(rsk_ctx *c, uint32_t *flags) {
     if (!c) return RSK_EINVAL;
     DeviceGuard g(c->device);
@@ -3032,6 +3284,31 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         case 66: hipLaunchKernelGGL((k_encode_w4<11, 4, 4, -1, 8, 1024, 16, 4>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
         case 67: hipLaunchKernelGGL((k_encode_w4<11, 4, 4, -1, 8, 1024, 32, 8>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
         case 68: hipLaunchKernelGGL((k_encode_w4<11, 4, 4, -1, 8, 1024, 32, 4>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
+        case 69: hipLaunchKernelGGL((k_encode_bc<1, 0>), dim3((unsigned)((n + 15ull) / 16ull)), dim3(1024), lds, st, a, c->ks); break;
+        case 70: hipLaunchKernelGGL((k_encode_bc<2, 0>), dim3((unsigned)((n + 31ull) / 32ull)), dim3(1024), lds, st, a, c->ks); break;
+        case 71: hipLaunchKernelGGL((k_encode_bc<4, 0>), dim3((unsigned)((n + 63ull) / 64ull)), dim3(1024), lds, st, a, c->ks); break;
+        case 72: hipLaunchKernelGGL((k_encode_bc<1, 2>), dim3((unsigned)((n + 15ull) / 16ull)), dim3(1024), lds, st, a, c->ks); break;
+        case 73: hipLaunchKernelGGL(k_probe_gi, dim3(enc_grid(n, 8, 1024)), bd, lds, st, a); break;
+        case 74: hipLaunchKernelGGL(k_probe_one, dim3((unsigned)((n + 3ull) / 4ull)), bd, lds, st, a); break;
+        case 75:
+        case 76: {
+            static uint4 *heads = nullptr;  // A/B only: the two-pass form's header workspace, never freed
+            static uint64_t heads_n = 0;
+            if (heads_n < n) {
+                if (heads) (void)hipFree(heads);
+                heads = nullptr;
+                if (hipMalloc(&heads, 32ull * n) != hipSuccess) return RSK_ENOMEM;
+                heads_n = n;
+            }
+            hipLaunchKernelGGL(k_enc_heads, dim3(grid_for(n)), bd, 0, st, a, c->ks, heads);
+            if (c->enc_variant % 100 == 75)
+                hipLaunchKernelGGL(k_enc_copy1<0>, dim3((unsigned)((n + 3ull) / 4ull)), bd, lds, st, a,
+                                   reinterpret_cast<const uint32_t *>(heads));
+            else
+                hipLaunchKernelGGL(k_enc_copy1<2>, dim3((unsigned)((n + 3ull) / 4ull)), bd, lds, st, a,
+                                   reinterpret_cast<const uint32_t *>(heads));
+            break;
+        }
         default: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
     }
 #else

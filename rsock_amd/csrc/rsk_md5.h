@@ -87,6 +87,7 @@ struct KeySched {
     uint32_t mid[4];   // chaining state after every block that holds only key bytes
     uint32_t blk[16];  // words of the block that holds payload[0], with that byte = 0
     uint32_t pad[16];  // the following padding/length block (used when two_blocks)
+    uint32_t pre[4];   // (a, b, c, d) after steps 0 .. bword - 1 of the last compression (md5_prefix_steps)
     int32_t bword;     // word index of payload[0] inside blk
     int32_t bshift;    // bit position of payload[0] inside that word
     int32_t two_blocks;
@@ -98,6 +99,69 @@ struct KeySched {
     // (t0, t1) for payload[0] = b, built on the GPU by k_tag_table at rsk_create.
     const uint2 *tab;
 };
+
+// ---- the per-lane form (round 4): payload[0]'s word index BW is a template parameter, so every
+// message word but one is uniform.  A step whose word is uniform folds K[i] + m[g] into one scalar
+// add and costs 4 VALU (the round function as one v_bitop3_b32, v_add3_u32(a, f, K + m),
+// v_alignbit_b32, v_add_u32); only the 4 steps that read word BW (one per round) add the per-lane
+// word.  Steps 0 .. BW - 1 read key words only and start from the key's midstate, so the host runs
+// them (build_sched -> KeySched::pre) and the device starts at step BW.  The generic md5_tag above
+// had every message word in a VGPR (word BW selected at run time): 5 VALU per step
+// (profiles/r04_ab_md5_isa.json).
+template <int I>
+struct Md5Step {
+    static constexpr int R = I / 16;
+    static constexpr int G = R == 0 ? I : R == 1 ? (5 * I + 1) & 15 : R == 2 ? (3 * I + 5) & 15 : (7 * I) & 15;
+    static constexpr int S = R == 0 ? (I % 4 == 0 ? 7 : I % 4 == 1 ? 12 : I % 4 == 2 ? 17 : 22)
+                           : R == 1 ? (I % 4 == 0 ? 5 : I % 4 == 1 ? 9 : I % 4 == 2 ? 14 : 20)
+                           : R == 2 ? (I % 4 == 0 ? 4 : I % 4 == 1 ? 11 : I % 4 == 2 ? 16 : 23)
+                                    : (I % 4 == 0 ? 6 : I % 4 == 1 ? 10 : I % 4 == 2 ? 15 : 21);
+    __host__ __device__ static __forceinline__ uint32_t f(uint32_t b, uint32_t c, uint32_t d) {
+        if constexpr (R == 0) return d ^ (b & (c ^ d));
+        else if constexpr (R == 1) return c ^ (d & (b ^ c));
+        else if constexpr (R == 2) return b ^ c ^ d;
+        else return c ^ (b | ~d);
+    }
+};
+
+// steps I .. 63 on (a, b, c, d); mw = the per-lane word BW; returns the final c and d (the tag's words
+// before the feed-forward; step 63's b is not needed and the compiler drops it)
+template <int I, int BW>
+__host__ __device__ __forceinline__ void md5_steps_bw(uint32_t a, uint32_t b, uint32_t c, uint32_t d,
+                                                      const uint32_t *blk, uint32_t mw, uint32_t &oc, uint32_t &od) {
+    if constexpr (I == 64) {
+        oc = c;
+        od = d;
+    } else {
+        using St = Md5Step<I>;
+        const uint32_t fv = St::f(b, c, d);
+        uint32_t x;
+        if constexpr (St::G == BW) x = a + fv + mw + Md5Consts::K[I];
+        else x = a + fv + (Md5Consts::K[I] + blk[St::G]);  // K + m: one scalar add
+        const uint32_t nb = b + rotl(x, St::S);
+        md5_steps_bw<I + 1, BW>(d, nb, b, c, blk, mw, oc, od);  // (a, b, c, d) <- (d, new, b, c)
+    }
+}
+
+// host: state (a, b, c, d) after steps 0 .. bw - 1 from the midstate (round 0 reads m[i] at step i,
+// all key words for i < bw)
+inline void md5_prefix_steps(const uint32_t mid[4], const uint32_t blk[16], int bw, uint32_t out[4]) {
+    uint32_t a = mid[0], b = mid[1], c = mid[2], d = mid[3];
+    static const int S0[4] = {7, 12, 17, 22};
+    for (int i = 0; i < bw; ++i) {
+        const uint32_t f = d ^ (b & (c ^ d));
+        const uint32_t x = a + f + Md5Consts::K[i] + blk[i];
+        const uint32_t nb = b + ((x << S0[i & 3]) | (x >> (32 - S0[i & 3])));
+        a = d;
+        d = c;
+        c = b;
+        b = nb;
+    }
+    out[0] = a;
+    out[1] = b;
+    out[2] = c;
+    out[3] = d;
+}
 
 // Tag words (digest bytes 8..11 and 12..15, little-endian) for payload byte b.
 template <class KS = KImm>
@@ -120,6 +184,52 @@ __host__ __device__ __forceinline__ void md5_tag(const KeySched &ks, uint32_t b,
     }
     t0 = st[2];
     t1 = st[3];
+}
+
+// The per-lane tag with payload[0] in word BW (== ks.bword): starts from ks.pre at step BW.
+template <int BW>
+__host__ __device__ __forceinline__ void md5_tag_bw(const KeySched &ks, uint32_t b, uint32_t &t0, uint32_t &t1) {
+    const uint32_t mw = ks.blk[BW] | (b << ks.bshift);
+    uint32_t c, d;
+    if (BW < 13 || !ks.two_blocks) {  // a two-block tail puts payload[0] in byte 55..63: word 13..15
+        md5_steps_bw<BW, BW>(ks.pre[0], ks.pre[1], ks.pre[2], ks.pre[3], ks.blk, mw, c, d);
+        t0 = ks.mid[2] + c;
+        t1 = ks.mid[3] + d;
+        return;
+    }
+    // 55..63 key bytes past the last whole block (BW = 13 .. 15): the full state of the first
+    // compression feeds the padding block's
+    uint32_t m[16];
+#pragma unroll
+    for (int w = 0; w < 16; ++w) m[w] = w == BW ? mw : ks.blk[w];
+    uint32_t st[4] = {ks.mid[0], ks.mid[1], ks.mid[2], ks.mid[3]};
+    md5_compress(st, m);
+    uint32_t p[16];
+#pragma unroll
+    for (int w = 0; w < 16; ++w) p[w] = (w == 0 || w >= 14) ? ks.pad[w] : 0u;
+    md5_compress(st, p);
+    t0 = st[2];
+    t1 = st[3];
+}
+
+// Dispatch on the key's payload word (uniform per launch: one scalar branch).
+__host__ __device__ __forceinline__ void md5_tag_lane(const KeySched &ks, uint32_t b, uint32_t &t0, uint32_t &t1) {
+#if defined(RSK_AB) && defined(__HIP_DEVICE_COMPILE__)
+    // A/B build (tools only): the tools' key "hello135" (word 2) specialised, every other key on the
+    // generic schedule, so the ~60 encode variants compile in minutes, not tens of minutes
+    if (ks.bword == 2) md5_tag_bw<2>(ks, b, t0, t1);
+    else md5_tag(ks, b, t0, t1);
+    return;
+#endif
+    switch (ks.bword) {
+#define RSK_MD5_BW(W) \
+    case W: md5_tag_bw<W>(ks, b, t0, t1); return;
+        RSK_MD5_BW(0) RSK_MD5_BW(1) RSK_MD5_BW(2) RSK_MD5_BW(3) RSK_MD5_BW(4) RSK_MD5_BW(5) RSK_MD5_BW(6)
+        RSK_MD5_BW(7) RSK_MD5_BW(8) RSK_MD5_BW(9) RSK_MD5_BW(10) RSK_MD5_BW(11) RSK_MD5_BW(12) RSK_MD5_BW(13)
+        RSK_MD5_BW(14)
+#undef RSK_MD5_BW
+        default: md5_tag_bw<15>(ks, b, t0, t1); return;
+    }
 }
 
 }  // namespace rsk
