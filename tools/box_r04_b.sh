@@ -9,6 +9,8 @@ OUT=$R/gpurun_out/r04b
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 AB="$R/tools/ab_encode.py"
+# the shipped library first: every GPU test (MD5 schedule, compaction taint, bench backend default)
+(cd "$R" && timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1) &&
 RSK_LIB=librsk_ab.so timeout -k 10 300 python3 "$AB" --config c3 --variants 0,73,74,75,76,13 --pads 16 --rounds 6 --reps 5 > "$OUT/ab_c3.json" 2> "$OUT/ab_c3.err" &&
 RSK_LIB=librsk_ab.so timeout -k 10 200 python3 "$AB" --config c4 --variants 0,73,74,75,76 --pads 128 --rounds 6 --reps 10 > "$OUT/ab_c4.json" 2> "$OUT/ab_c4.err" &&
 RSK_LIB=librsk_ab.so timeout -k 10 200 python3 "$AB" --config c2 --variants 0,75 --pads 16 --rounds 6 --reps 10 > "$OUT/ab_c2.json" 2> "$OUT/ab_c2.err" &&
@@ -18,6 +20,10 @@ RSK_LIB=librsk_r03md5.so timeout -k 10 200 python3 "$R/tools/ab_tag.py" --config
 RSK_LIB=librsk.so timeout -k 10 200 python3 "$R/tools/ab_tag.py" --config c4 --rounds 6 --reps 10 > "$OUT/tag_new_c4.json" 2> "$OUT/tag_new_c4.err" &&
 RSK_LIB=librsk_r03md5.so timeout -k 10 200 python3 "$R/tools/ab_tag.py" --config c3 --rounds 4 --reps 5 > "$OUT/tag_old_c3.json" 2> "$OUT/tag_old_c3.err" &&
 RSK_LIB=librsk.so timeout -k 10 200 python3 "$R/tools/ab_tag.py" --config c3 --rounds 4 --reps 5 > "$OUT/tag_new_c3.json" 2> "$OUT/tag_new_c3.err" &&
+RSK_LIB=librsk_r03md5.so timeout -k 10 200 python3 "$R/tools/bench_paths.py" --config c3 --only demux,demux_64conn --rounds 3 --reps 3 > "$OUT/dm_old_c3.json" 2> "$OUT/dm_old_c3.err" &&
+RSK_LIB=librsk.so timeout -k 10 200 python3 "$R/tools/bench_paths.py" --config c3 --only demux,demux_64conn --rounds 3 --reps 3 > "$OUT/dm_new_c3.json" 2> "$OUT/dm_new_c3.err" &&
+RSK_LIB=librsk_r03md5.so timeout -k 10 200 python3 "$R/tools/bench_paths.py" --config c4 --only demux,demux_64conn --rounds 3 --reps 5 > "$OUT/dm_old_c4.json" 2> "$OUT/dm_old_c4.err" &&
+RSK_LIB=librsk.so timeout -k 10 200 python3 "$R/tools/bench_paths.py" --config c4 --only demux,demux_64conn --rounds 3 --reps 5 > "$OUT/dm_new_c4.json" 2> "$OUT/dm_new_c4.err" &&
 RSK_LIB=librsk_ab.so timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE -T -d "$OUT/pmc_fetch" -o pmc --output-format csv -- \
     python3 "$AB" --config c3 --variants 0,74,75 --pads 16 --rounds 1 --reps 2 > "$OUT/fetch.log" 2>&1 &&
 RSK_LIB=librsk_ab.so timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE -T -d "$OUT/pmc_write" -o pmc --output-format csv -- \
