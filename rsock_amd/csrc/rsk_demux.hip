@@ -683,16 +683,20 @@ __device__ void small_sort(uint32_t nf, const uint32_t *keys, const uint32_t *va
     }
 }
 
-// One radix pass, onesweep: tile t (= block t, dispatch order) counts its digits, gets the count of
-// each digit in tiles before it by per-digit decoupled look-back, adds the digit's global start
-// (exclusive scan of the pass's global histogram), ranks its items stably in LDS and writes the tile
-// out digit run by digit run (consecutive threads, consecutive addresses).
+// One radix pass, onesweep: tile t (= block t, dispatch order) ranks its items stably, gets the count
+// of each digit in tiles before it by per-digit decoupled look-back, adds the digit's global start
+// (exclusive scan of the pass's global histogram) and writes the tile out digit run by digit run
+// (consecutive threads, consecutive addresses).  Round 4: wave w owns items [w * 1024, w * 1024 + 1024)
+// of the tile and ranks them row by row (64 items) against its own running digit counts in LDS, so
+// the ranking needs no block barrier per row (rounds 2-3: rows across the 4 waves, three block
+// barriers per row, 48 per tile); one barrier then turns the per-wave counts into per-wave offsets.
 __global__ __launch_bounds__(kBlock) void k_dm_onesweep(uint32_t pass, const uint32_t *nvp, const uint32_t *nsegp,
                                                         const uint32_t *kin, const uint32_t *vin, const uint32_t *ghist,
                                                         unsigned long long *st, uint32_t *kout, uint32_t *vout,
                                                         uint32_t *err) {
-    __shared__ uint32_t run[256], lbase[256], dbase[256];
-    __shared__ uint32_t wcnt[kWaves][256];
+    constexpr uint32_t kPerWave = kTile / kWaves;  // 1024 items, kItems rows of 64
+    __shared__ uint32_t wcnt[kWaves][256];  // wave's running digit counts, then its exclusive offsets
+    __shared__ uint32_t lbase[256], dbase[256];
     __shared__ uint32_t sk[kTile], sv[kTile];
     const uint32_t ns = *nsegp, nv = *nvp - ns, tile = blockIdx.x;  // nv: the followers being sorted
     if (nv <= kSmallF) {  // block-uniform
@@ -700,37 +704,49 @@ __global__ __launch_bounds__(kBlock) void k_dm_onesweep(uint32_t pass, const uin
         return;
     }
     if (pass >= n_passes(ns) || tile * kTile >= nv) return;  // block-uniform; no later tile waits
-    const uint32_t width = 8u, sh = width * pass, dm = 255u;  // the histograms' fixed 8-bit digits
+    const uint32_t sh = 8u * pass;  // the histograms' fixed 8-bit digits
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
-    const uint32_t base = tile * kTile;
+    const uint32_t base = tile * kTile, wbase = base + w * kPerWave;
     const uint32_t cnt = nv - base < kTile ? nv - base : kTile;
-    run[t] = 0;
 #pragma unroll
     for (int q = 0; q < kWaves; ++q) wcnt[q][t] = 0;
-    __syncthreads();
-    uint32_t kk[kItems], vv[kItems];
+    uint32_t kk[kItems], vv[kItems], rk[kItems];
 #pragma unroll
     for (uint32_t r = 0; r < kItems; ++r) {
-        const uint32_t k = base + r * kBlock + t;
+        const uint32_t k = wbase + r * 64u + lane;
         kk[r] = k < nv ? kin[k] : 0u;
         vv[r] = k < nv ? vin[k] : 0u;
     }
+    __syncthreads();
+    const uint64_t lt = lanemask_lt(lane);
 #pragma unroll
-    for (uint32_t r = 0; r < kItems; ++r) {
-        const bool v = base + r * kBlock + t < nv;
-        const uint32_t d = (kk[r] >> sh) & dm;
-        const uint64_t peers = digit_peers(v, d, width);
-        if (v && (peers & lanemask_lt(lane)) == 0) atomicAdd(&run[d], (uint32_t)__popcll(peers));
+    for (uint32_t r = 0; r < kItems; ++r) {  // wave-local: the wave's rows in item order
+        const bool v = wbase + r * 64u + lane < nv;
+        const uint32_t d = (kk[r] >> sh) & 255u;
+        const uint64_t peers = digit_peers(v, d, 8u);
+        const uint32_t below = (uint32_t)__popcll(peers & lt);
+        const uint32_t c = v ? wcnt[w][d] : 0u;
+        rk[r] = c + below;
+        if (v && below == 0u) wcnt[w][d] = c + (uint32_t)__popcll(peers);  // after every lane's read (in order)
     }
     __syncthreads();
+    uint32_t tot = 0;  // digit t: the tile's count, and each wave's exclusive offset
+#pragma unroll
+    for (int q = 0; q < kWaves; ++q) {
+        const uint32_t c = wcnt[q][t];
+        wcnt[q][t] = tot;
+        tot += c;
+    }
+    lbase[t] = tot;
     // global position of this tile's first digit-t item: digits before t overall + digit t before this tile
-    const uint32_t before = dlb_digit(st + (uint64_t)pass * 256u * gridDim.x, tile, t, run[t], err);
+    const uint32_t before = dlb_digit(st + (uint64_t)pass * 256u * gridDim.x, tile, t, tot, err);
+    __syncthreads();
     if (w == 0) {  // exclusive scans of the global histogram and of the tile's bins (4 per lane)
         uint32_t g[4], c[4], gs = 0, cs = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             g[q] = ghist[256u * pass + 4u * lane + q];
-            c[q] = run[4 * lane + q];
+            c[q] = lbase[4 * lane + q];
             gs += g[q];
             cs += c[q];
         }
@@ -754,35 +770,17 @@ __global__ __launch_bounds__(kBlock) void k_dm_onesweep(uint32_t pass, const uin
     }
     __syncthreads();
     dbase[t] += before;
-    run[t] = 0;
-    __syncthreads();
 #pragma unroll
     for (uint32_t r = 0; r < kItems; ++r) {
-        const bool v = base + r * kBlock + t < nv;
-        const uint32_t key = kk[r];
-        const uint32_t d = (key >> sh) & dm;
-        const uint64_t peers = digit_peers(v, d, width);
-        const uint32_t lt = (uint32_t)__popcll(peers & lanemask_lt(lane));
-        if (v && lt == 0) wcnt[w][d] = (uint32_t)__popcll(peers);
-        __syncthreads();
-        if (v) {
-            uint32_t pos = lbase[d] + run[d] + lt;
-            for (uint32_t q = 0; q < w; ++q) pos += wcnt[q][d];
-            sk[pos] = key;
-            sv[pos] = vv[r];
-        }
-        __syncthreads();
-        uint32_t add = 0;
-#pragma unroll
-        for (int q = 0; q < kWaves; ++q) {
-            add += wcnt[q][t];
-            wcnt[q][t] = 0;
-        }
-        run[t] += add;
-        __syncthreads();
+        if (wbase + r * 64u + lane >= nv) continue;
+        const uint32_t d = (kk[r] >> sh) & 255u;
+        const uint32_t pos = lbase[d] + wcnt[w][d] + rk[r];
+        sk[pos] = kk[r];
+        sv[pos] = vv[r];
     }
+    __syncthreads();
     for (uint32_t p = t; p < cnt; p += kBlock) {
-        const uint32_t key = sk[p], d = (key >> sh) & dm;
+        const uint32_t key = sk[p], d = (key >> sh) & 255u;
         const uint32_t g = dbase[d] + (p - lbase[d]);
         kout[g] = key;
         vout[g] = sv[p];
@@ -910,8 +908,8 @@ extern "C" int rsk_demux_batch(rsk_ctx *c, uint32_t n, const rsk_demux_in *in, u
     a.dst = in->dst;
     a.n = n;
     a.fields = fields;
-    // one fill: the key table and every look-back state word start as all-ones
-    hipError_t e = hipMemsetAsync(w.slots, 0xff, w.fill_bytes, s);
+    // one fill: rank_at, the key table and every look-back state word start as all-ones
+    hipError_t e = hipMemsetAsync(w.rank_at, 0xff, w.fill_bytes, s);  // rank_at .. the last state word
     if (e != hipSuccess) { rsk::set_error("hipMemsetAsync(table)", e); return RSK_EDEVICE; }
     const uint32_t nb = w.nb;
     hipLaunchKernelGGL(k_dm_flags_prep, dim3(w.nt), dim3(kBlock), 0, s, a, w.st_v, w.st_c, w.cidx, w.cep, w.nv,

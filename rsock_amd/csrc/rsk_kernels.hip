@@ -118,6 +118,12 @@ __device__ __forceinline__ void stage_tags(const KeySched &ks) {
 #endif
 }
 
+// LANE (the decode kernels): the payload-word-specialised schedule (rsk_md5.h md5_tag_lane: 4 VALU per
+// step instead of 5, 16 instantiations behind one scalar branch).  The framing kernels keep the generic
+// schedule: in k_encode the specialised one raised the register budget past 128 VGPRs (3 waves per
+// SIMD instead of 4, 2x the SGPR spills) and cost C2 / C4 13-16 % in both tag modes
+// (profiles/r04_ab_md5_isa.json); the decode kernels have registers to spare and gain ~1 %.
+template <bool LANE = false>
 __device__ __forceinline__ void tag_of(const KeySched &ks, uint32_t b, uint32_t &t0, uint32_t &t1) {
     if (ks.tag_mode == RSK_TAG_TABLE) {
         const uint2 t = s_tags[b & 255u];
@@ -128,7 +134,8 @@ __device__ __forceinline__ void tag_of(const KeySched &ks, uint32_t b, uint32_t 
 #ifdef RSK_MD5_K_LDS
     rsk::md5_tag(ks, b & 255u, t0, t1, KLds());
 #else
-    rsk::md5_tag_lane(ks, b & 255u, t0, t1);
+    if constexpr (LANE) rsk::md5_tag_lane(ks, b & 255u, t0, t1);
+    else rsk::md5_tag(ks, b & 255u, t0, t1);
 #endif
 }
 
@@ -1095,6 +1102,22 @@ __global__ __launch_bounds__(kBlock) void k_enc_copy1(EncArgs a, const uint32_t 
         if (k >= nst) continue;
         store_piece<NT>(g.d0 + 16u * k, v, k == 0u ? g.r : 0u, (int)flen - 16 * (int)k, a.pad != 0u);
     }
+}
+
+// A/B build only (round 4): few packets per wave.  Wave w frames packets [PPW w, PPW w + PPW) (linear
+// mapping, short-lived waves: the access shape of k_probe_one) with the shipped long-frame copy
+// (copy_pkt_pipe, TAG form: payload[0] and one MD5 pass per batch of PU packets, header chunks in the
+// packets' own slot stores).
+template <int PPW, int PU, int NT>
+__global__ __launch_bounds__(kBlock) void k_enc_few(EncArgs a, KeySched ks) {
+    stage_tags(ks);
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint64_t first = ((uint64_t)blockIdx.x * kWavesPerBlock + w) * PPW;
+    if (first >= a.n) return;  // wave-uniform
+    const uint64_t i = lane < (uint32_t)PPW && first + lane < a.n ? first + lane : a.n;
+    Lane1 L = encode_phase1<false>(a, ks, i);
+    const uint64_t vm = __ballot(L.st > 0);
+    copy_pkt_pipe<PU, NT, true>(a, ks, L, lane, vm);
 }
 
 // A/B build only (round 4): memory-pattern probes for C3's ceiling (wrong bytes: aligned source
@@ -2191,7 +2214,7 @@ __device__ __forceinline__ Dec decode_frame_t(const uint8_t *base, int nread, bo
         if ((int)len <= nread - 8 && dl > 0) {              // DecodeBuf ok, hash_equal len > 0
             const uint32_t b = (SLOT || len == (uint32_t)RSK_ENC_HEAD_SIZE) ? (w[7] >> 24) : base[8 + len];
             uint32_t t0, t1;
-            tag_of(ks, b, t0, t1);
+            tag_of<true>(ks, b, t0, t1);
             if (t0 == w[0] && t1 == w[1]) {
                 o.st = RSK_RECV_VALID;
                 o.hlen = len;
@@ -3097,12 +3120,13 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 // the block-cooperative copy k_encode_bc (16 waves per block, 1 / 2 / 4 packets per wave), 72 = 69 with
 // nontemporal stores; 73 / 74 = memory-pattern probes (wrong bytes: k_probe_gi, the shipped mapping and
 // batches; k_probe_one, one wave per packet); 75 / 76 = the two-pass form (k_enc_heads then
-// k_enc_copy1, normal / nontemporal stores) (round 4).  Rounds 1-2
+// k_enc_copy1, normal / nontemporal stores); 77 / 78 / 79 / 80 / 81 = k_enc_few, 1 / 2 / 4 / 8 / 16 packets
+// per wave, 82 = 78 with nontemporal stores (round 4).  Rounds 1-2
 // measured ~45 more variants (profiles/r01_ab_*, r02_ab_*); their code is in the git history.
 // v + 100 * cap (cap 1..4): the same kernel held to `cap` blocks per CU by unused LDS.
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
     const int k = v % 100;
-    if (!c || v < 0 || v / 100 > 4 || !(k == 0 || k == 12 || k == 13 || k == 37 || k == 47 || (k >= 50 && k <= 76)))
+    if (!c || v < 0 || v / 100 > 4 || !(k == 0 || k == 12 || k == 13 || k == 37 || k == 47 || (k >= 50 && k <= 82)))
         return RSK_EINVAL;
     c->enc_variant = v;
     return RSK_OK;
@@ -3289,6 +3313,12 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         case 71: hipLaunchKernelGGL((k_encode_bc<4, 0>), dim3((unsigned)((n + 63ull) / 64ull)), dim3(1024), lds, st, a, c->ks); break;
         case 72: hipLaunchKernelGGL((k_encode_bc<1, 2>), dim3((unsigned)((n + 15ull) / 16ull)), dim3(1024), lds, st, a, c->ks); break;
         case 73: hipLaunchKernelGGL(k_probe_gi, dim3(enc_grid(n, 8, 1024)), bd, lds, st, a); break;
+        case 77: hipLaunchKernelGGL((k_enc_few<1, 1, 0>), dim3((unsigned)((n + 3ull) / 4ull)), bd, lds, st, a, c->ks); break;
+        case 78: hipLaunchKernelGGL((k_enc_few<2, 2, 0>), dim3((unsigned)((n + 7ull) / 8ull)), bd, lds, st, a, c->ks); break;
+        case 79: hipLaunchKernelGGL((k_enc_few<4, 4, 0>), dim3((unsigned)((n + 15ull) / 16ull)), bd, lds, st, a, c->ks); break;
+        case 80: hipLaunchKernelGGL((k_enc_few<8, 4, 0>), dim3((unsigned)((n + 31ull) / 32ull)), bd, lds, st, a, c->ks); break;
+        case 81: hipLaunchKernelGGL((k_enc_few<16, 4, 0>), dim3((unsigned)((n + 63ull) / 64ull)), bd, lds, st, a, c->ks); break;
+        case 82: hipLaunchKernelGGL((k_enc_few<2, 2, 2>), dim3((unsigned)((n + 7ull) / 8ull)), bd, lds, st, a, c->ks); break;
         case 74: hipLaunchKernelGGL(k_probe_one, dim3((unsigned)((n + 3ull) / 4ull)), bd, lds, st, a); break;
         case 75:
         case 76: {
