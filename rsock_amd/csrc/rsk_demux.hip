@@ -9,9 +9,9 @@
 // the host does one lookup per segment.
 //
 // Pipeline (all stream-ordered, no host sync; n_valid and the segment count stay on the device),
-// 4 + passes launches after one fill (round 2: the block scans are decoupled look-backs inside the
+// 5 + passes launches after one fill (round 2: the block scans are decoupled look-backs inside the
 // kernels that produce the counts, and the radix sort is onesweep, one launch per pass):
-//   fill            rank_at, key table + look-back state words to all-ones
+//   fill            key table + look-back state words to all-ones
 //   k_dm_flags_prep per-wave ballots of VALID and VALID-control packets, block offsets by look-back;
 //                   cidx[j] = packet of compacted slot j, cep[j] = its epoch (CTRL for singletons)
 //   k_dm_insert     open-addressing table: a slot holds a key fingerprint and the compacted index of
@@ -21,11 +21,11 @@
 //   k_dm_leader_rank leader of j = the slot's index (or j for a control packet); leader ranks = dense
 //                   segment ids in first-occurrence order by look-back; rank_at, seg_first, n_seg;
 //                   the followers (non-leaders) compacted with their leader
-//                   and (round 4: the former k_dm_segof_hist) their radix keys = their leader's
-//                   segment id + the global 8-bit digit histograms of every pass
-//   k_dm_onesweep   stable LSD pass of the FOLLOWERS by segment id (8-bit digits, as many passes as
-//                   the segment count needs; passes beyond that, and tiles past the follower count,
-//                   return at once), per-digit look-back; <= 1024 followers: sorted by pass 0's block 0
+//   k_dm_segof_hist radix keys = segment id of each follower, global digit histograms of every pass
+//                   (<= 1024 followers: sorted here by one block)
+//   k_dm_onesweep   stable LSD pass of the FOLLOWERS by segment id (8-bit or narrower digits, as many
+//                   passes as the segment count needs; passes beyond that, and tiles past the
+//                   follower count, return at once), per-digit look-back; ranking wave-local (round 4)
 //   k_dm_final      leaders merged with the sorted followers: perm, seg_off, n_seg / n_valid
 // (round 2, second half: only followers are sorted — leaders already stand in segment order — so a
 // batch of mostly single-packet segments skips the sort's work)
@@ -265,16 +265,9 @@ __device__ __forceinline__ uint64_t key_hash(const Key &k) {
 // Global table probe: a slot is one u64, fingerprint (hash bits 32..63) << 32 | the compacted index
 // of the key's first packet so far.  A slot with another fingerprint is skipped without touching that
 // packet's fields, a matching fingerprint is confirmed on the full key, and the index is lowered by
-// compare-and-swap (the fingerprint half never changes once claimed).  A load comes first: a hot
-// key's slot is read, not written, by every later tile (no RMW unless the index drops); a new key
-// costs the load and one CAS (round 2, first half: a load, a CAS and a separate atomicMin word).
-// Round 4: that load is a plain (L2-cached) load, not a device-scope atomic one (which misses every
-// XCD's L2 and goes to the memory side: every tile's representative of a hot key queued on the same
-// word there).  A stale L2 copy is harmless because a slot only ever moves EMPTY -> (fp, index) ->
-// (fp, lower index): a stale EMPTY goes to the CAS, which returns the real word; a stale fingerprint
-// is the real one; a stale index is >= the real one, so "no lowering needed" stays true and a
-// lowering CAS with the stale word fails and retries with the real one; and every index ever stored
-// in a slot is a packet of that slot's key, so confirming against a stale owner is still exact.
+// compare-and-swap (the fingerprint half never changes once claimed).  A relaxed load comes first:
+// a hot key's slot is read, not written, by every later tile (no RMW unless the index drops); a new
+// key costs the load and one CAS (round 2, first half: a load, a CAS and a separate atomicMin word).
 __device__ __forceinline__ uint32_t global_probe(const DmIn &a, const uint32_t *cidx, const uint32_t *cep,
                                                  unsigned long long *slots, uint32_t mask, const Key &k,
                                                  uint64_t hv, uint32_t j) {
@@ -282,7 +275,7 @@ __device__ __forceinline__ uint32_t global_probe(const DmIn &a, const uint32_t *
     const unsigned long long mine = ((unsigned long long)fp << 32) | j;
     uint32_t h = (uint32_t)hv & mask;
     for (;;) {
-        unsigned long long e = slots[h];  // plain load: see above
+        unsigned long long e = __hip_atomic_load(slots + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (e == ~0ull) {
             e = atomicCAS(slots + h, ~0ull, mine);
             if (e == ~0ull) return h;  // claimed
@@ -412,9 +405,13 @@ __global__ __launch_bounds__(kBlock) void k_dm_insert(DmIn a, const uint32_t *nv
 __device__ __forceinline__ uint32_t bits_for(uint32_t nseg) {  // bits of the largest key (< nseg)
     return nseg <= 1u ? 1u : 32u - (uint32_t)__builtin_clz(nseg - 1u);
 }
-// passes = ceil(bits / 8), 8-bit digits (round 4: fixed, so k_dm_leader_rank can histogram the digits
-// before the segment count is known; rounds 1-3 spread the bits evenly, 18 bits as 3 x 6)
+// passes = ceil(bits / 8); the digit width spreads the bits evenly over them (18 bits: 3 x 6, not
+// 8 + 8 + 2), so each pass has as few buckets as it can -> longer contiguous runs per tile
 __device__ __forceinline__ uint32_t n_passes(uint32_t nseg) { return (bits_for(nseg) + 7u) / 8u; }
+__device__ __forceinline__ uint32_t digit_width(uint32_t nseg) {
+    const uint32_t b = bits_for(nseg), p = (b + 7u) / 8u;
+    return (b + p - 1u) / p;
+}
 
 // lanes of this wave holding the same digit (valid lanes only)
 __device__ __forceinline__ uint64_t digit_peers(bool v, uint32_t d, uint32_t width) {
@@ -430,36 +427,16 @@ __device__ __forceinline__ uint64_t digit_peers(bool v, uint32_t d, uint32_t wid
 // look-back steps in its chain instead of 16384.
 constexpr uint32_t kRows = kTile / kBlock;
 
-// per-row ballots of the block -> this lane's wave offset within each row (rows before it included)
-__device__ __forceinline__ void tile_offsets(const uint64_t (*m)[kWaves], uint32_t w, uint32_t (&off)[kRows],
-                                             uint32_t &total) {
-    uint32_t acc = 0;
-#pragma unroll
-    for (uint32_t r = 0; r < kRows; ++r) {
-        uint32_t o = acc;
-#pragma unroll
-        for (uint32_t q = 0; q < (uint32_t)kWaves; ++q) {
-            const uint32_t c = (uint32_t)__popcll(m[r][q]);
-            if (q < w) o += c;
-            acc += c;
-        }
-        off[r] = o;
-    }
-    total = acc;
-}
-
 // flags + both block scans + prep in one pass: per-row ballots of VALID and VALID-control packets,
 // the tile's exclusive offsets by decoupled look-back (wave 0: compacted index, wave 1: epoch), then
 // cidx[j] = packet of compacted slot j, cep[j] = its epoch (CTRL for singletons); the last tile
 // writes n_valid.
 __global__ __launch_bounds__(kBlock) void k_dm_flags_prep(DmIn a, unsigned long long *st_v,
                                                           unsigned long long *st_c, uint32_t *cidx, uint32_t *cep,
-                                                          uint32_t *nvp, uint32_t *ghist, uint32_t *err) {
+                                                          uint32_t *nvp, uint32_t *err) {
     __shared__ uint64_t mv[kRows][kWaves], mc[kRows][kWaves];
     __shared__ uint32_t pre[2];
     const uint32_t b = blockIdx.x, t = threadIdx.x, w = t >> 6, lane = t & 63u;
-    if (b == 0u)  // the radix histograms k_dm_leader_rank accumulates (two launches later)
-        for (uint32_t q = t; q < 4u * 256u; q += kBlock) ghist[q] = 0u;
     uint32_t flags = 0;  // bit r: row r's item valid; bit 16 + r: control
     int8_t stv[kRows];  // every row's loads in flight before the first ballot
     uint8_t cmv[kRows];
@@ -482,9 +459,15 @@ __global__ __launch_bounds__(kBlock) void k_dm_flags_prep(DmIn a, unsigned long 
         flags |= (valid ? 1u << r : 0u) | (ctrl ? 1u << (16 + r) : 0u);
     }
     __syncthreads();
-    uint32_t ov[kRows], oc[kRows], av, ac;
-    tile_offsets(mv, w, ov, av);
-    tile_offsets(mc, w, oc, ac);
+    uint32_t av = 0, ac = 0;  // the tile's totals; row offsets are recomputed from LDS below (round 4:
+                              // holding 2 x 16 of them cost VGPRs, 181 in all -> 2 waves per SIMD)
+#pragma unroll
+    for (uint32_t r = 0; r < kRows; ++r)
+#pragma unroll
+        for (uint32_t q = 0; q < (uint32_t)kWaves; ++q) {
+            av += (uint32_t)__popcll(mv[r][q]);
+            ac += (uint32_t)__popcll(mc[r][q]);
+        }
     if (w == 0u) {
         const uint32_t e = dlb_wave(st_v, b, av, lane, err);
         if (lane == 0u) {
@@ -497,88 +480,74 @@ __global__ __launch_bounds__(kBlock) void k_dm_flags_prep(DmIn a, unsigned long 
     }
     __syncthreads();
     const uint64_t lt = lanemask_lt(lane);
+    uint32_t accv = pre[0], accc = pre[1];  // + items of the rows before r
 #pragma unroll
     for (uint32_t r = 0; r < kRows; ++r) {
-        if (!((flags >> r) & 1u)) continue;
-        const uint32_t i = b * kTile + r * kBlock + t;
-        const uint32_t j = pre[0] + ov[r] + (uint32_t)__popcll(mv[r][w] & lt);
-        cidx[j] = i;
-        cep[j] = ((flags >> (16 + r)) & 1u) ? kCtrl : pre[1] + oc[r] + (uint32_t)__popcll(mc[r][w] & lt);
+        uint32_t bv = 0, bc = 0, tv = 0, tc = 0;  // waves before w in row r; the whole row
+#pragma unroll
+        for (uint32_t q = 0; q < (uint32_t)kWaves; ++q) {
+            const uint32_t cv = (uint32_t)__popcll(mv[r][q]), cc = (uint32_t)__popcll(mc[r][q]);
+            if (q < w) {
+                bv += cv;
+                bc += cc;
+            }
+            tv += cv;
+            tc += cc;
+        }
+        if ((flags >> r) & 1u) {
+            const uint32_t i = b * kTile + r * kBlock + t;
+            const uint32_t j = accv + bv + (uint32_t)__popcll(mv[r][w] & lt);
+            cidx[j] = i;
+            cep[j] = ((flags >> (16 + r)) & 1u) ? kCtrl : accc + bc + (uint32_t)__popcll(mc[r][w] & lt);
+        }
+        accv += tv;
+        accc += tc;
     }
 }
 
-// leader + scan + rank + the radix keys and histograms in one pass (round 4: k_dm_segof_hist folded
-// in).  The leader of compacted packet j is the first packet of its key (the index half of its table
-// slot, or j for a control packet); the leaders' dense ranks (segment ids in first-occurrence order)
-// by decoupled look-back; rank_at[leader], seg_first[rank]; the last tile writes the segment count.
-// Followers (every other packet) are compacted by the same count: follower f = j - (leaders before
-// j) gets fkey[f] = its leader's SEGMENT ID and fval[f] = its packet index, and the tile adds its
-// followers' radix digits (fixed 8-bit digits) into the global histograms of every pass.
-// A follower's leader is in this tile (its rank comes from the tile's own ballots in LDS) or in an
-// earlier one, which published rank_at[leader] with a device-scope store right after its look-back:
-// a plain load finds it (an L2 copy from before the store shows kNone, never a wrong rank: the words
-// are written once per call, from the fill), else a device-scope load, spun on (bounded) while the
-// earlier tile -- resident or done, tiles run in dispatch order -- has not stored it yet.
-__device__ __forceinline__ uint32_t leader_rank_of(const uint32_t *rank_at, uint32_t lead, uint32_t *err) {
-    uint32_t v = rank_at[lead];
-    if (v != kNone) return v;
-    uint32_t spins = 0;
-    do {
-        v = __hip_atomic_load(rank_at + lead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } while (v == kNone && ++spins < kDlbSpinMax);
-    if (v == kNone) {
-        __hip_atomic_fetch_or(err, RSK_DEVERR_LOOKBACK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        v = 0u;
-    }
-    return v;
-}
-
+// leader + scan + rank in one pass: the leader of compacted packet j is the first packet of its key
+// (the index half of its table slot, or j for a control packet); the leaders' dense ranks (segment
+// ids in first-occurrence order) by decoupled look-back; rank_at[leader], seg_first[rank]; the last
+// tile writes the segment count.  Followers (every other packet) are compacted by the same count:
+// follower f = j - (leaders before j) gets fkey[f] = its leader, fval[f] = its packet index.  Block 0
+// also clears the radix digit histograms the next launch accumulates.
 __global__ __launch_bounds__(kBlock) void k_dm_leader_rank(const uint32_t *nvp, const uint32_t *hslot,
                                                            const unsigned long long *slots, const uint32_t *cidx,
                                                            unsigned long long *st_l, uint32_t *fkey, uint32_t *fval,
                                                            uint32_t *rank_at, uint32_t *seg_first, uint32_t *nsegp,
                                                            uint32_t *ghist, uint32_t *err) {
     __shared__ uint64_t ml[kRows][kWaves];
-    __shared__ uint32_t woff[kRows * kWaves];  // leaders of the tile before (row, wave)
-    __shared__ uint32_t lh[4][256];
-    __shared__ uint32_t pre, tmax, tfol;
+    __shared__ uint32_t pre;
     const uint32_t nv = *nvp;
     const uint32_t b = blockIdx.x, t = threadIdx.x, w = t >> 6, lane = t & 63u;
-    const uint32_t base = b * kTile;
+    if (b == 0u)
+        for (uint32_t q = t; q < 4u * 256u; q += kBlock) ghist[q] = 0u;
     uint32_t isl = 0;  // bit r: row r's item is its key's leader
     uint32_t hs[kRows], lead[kRows];
 #pragma unroll
     for (uint32_t r = 0; r < kRows; ++r) {
-        const uint32_t j = base + r * kBlock + t;
+        const uint32_t j = b * kTile + r * kBlock + t;
         hs[r] = j < nv ? hslot[j] : kNone;
     }
 #pragma unroll
     for (uint32_t r = 0; r < kRows; ++r) {
-        const uint32_t j = base + r * kBlock + t;
+        const uint32_t j = b * kTile + r * kBlock + t;
         lead[r] = hs[r] == kNone ? j : (hs[r] & kLeadTag) ? hs[r] & ~kLeadTag : (uint32_t)slots[hs[r]];
     }
 #pragma unroll
     for (uint32_t r = 0; r < kRows; ++r) {
-        const uint32_t j = base + r * kBlock + t;
+        const uint32_t j = b * kTile + r * kBlock + t;
         const bool l = j < nv && lead[r] == j;
         const uint64_t bl = __ballot(l);
         if (lane == 0u) ml[r][w] = bl;
         isl |= l ? 1u << r : 0u;
     }
-#pragma unroll
-    for (int p = 0; p < 4; ++p) lh[p][t] = 0u;
-    if (t == 0u) {
-        tmax = 0u;
-        tfol = 0u;
-    }
     __syncthreads();
-    uint32_t ol[kRows], al;
-    tile_offsets(ml, w, ol, al);
-    if (t < kRows * kWaves) {  // (row, wave) t: leaders before it in the tile
-        uint32_t o = 0;
-        for (uint32_t q = 0; q < t; ++q) o += (uint32_t)__popcll(ml[q / kWaves][q % kWaves]);
-        woff[t] = o;
-    }
+    uint32_t al = 0;  // the tile's leaders; row offsets recomputed from LDS below (as k_dm_flags_prep)
+#pragma unroll
+    for (uint32_t r = 0; r < kRows; ++r)
+#pragma unroll
+        for (uint32_t q = 0; q < (uint32_t)kWaves; ++q) al += (uint32_t)__popcll(ml[r][q]);
     if (w == 0u) {
         const uint32_t e = dlb_wave(st_l, b, al, lane, err);
         if (lane == 0u) {
@@ -588,99 +557,113 @@ __global__ __launch_bounds__(kBlock) void k_dm_leader_rank(const uint32_t *nvp, 
     }
     __syncthreads();
     const uint64_t lt = lanemask_lt(lane);
-    // leaders first: their ranks are what the followers (here and in later tiles) read
+    uint32_t acc = pre;  // + leaders of the rows before r
 #pragma unroll
     for (uint32_t r = 0; r < kRows; ++r) {
-        const uint32_t j = base + r * kBlock + t;
-        if (j >= nv || !((isl >> r) & 1u)) continue;
-        const uint32_t before = pre + ol[r] + (uint32_t)__popcll(ml[r][w] & lt);
-        __hip_atomic_store(rank_at + j, before, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        seg_first[before] = cidx[j];
-    }
-    uint32_t kk[kRows];
-    uint32_t mymax = 0, myf = 0;
+        const uint32_t j = b * kTile + r * kBlock + t;
+        uint32_t bw = 0, tw = 0;
 #pragma unroll
-    for (uint32_t r = 0; r < kRows; ++r) {
-        const uint32_t j = base + r * kBlock + t;
-        kk[r] = 0u;
-        if (j >= nv || ((isl >> r) & 1u)) continue;
-        const uint32_t ld = lead[r];
-        if (ld >= base) {  // leader in this tile
-            const uint32_t li = ld - base, rr = li / kBlock, tt = li % kBlock;
-            kk[r] = pre + woff[rr * kWaves + tt / 64u] + (uint32_t)__popcll(ml[rr][tt / 64u] & lanemask_lt(tt % 64u));
+        for (uint32_t q = 0; q < (uint32_t)kWaves; ++q) {
+            const uint32_t c = (uint32_t)__popcll(ml[r][q]);
+            if (q < w) bw += c;
+            tw += c;
+        }
+        const uint32_t before = acc + bw + (uint32_t)__popcll(ml[r][w] & lt);  // leaders before j
+        acc += tw;
+        if (j >= nv) continue;
+        const uint32_t pk = cidx[j];
+        if ((isl >> r) & 1u) {
+            rank_at[j] = before;
+            seg_first[before] = pk;
         } else {
-            kk[r] = leader_rank_of(rank_at, ld, err);
-        }
-        const uint32_t before = pre + ol[r] + (uint32_t)__popcll(ml[r][w] & lt);
-        fkey[j - before] = kk[r];
-        fval[j - before] = cidx[j];
-        mymax = max(mymax, kk[r]);
-        ++myf;
-    }
-#pragma unroll
-    for (int off = 32; off; off >>= 1) {
-        mymax = max(mymax, (uint32_t)__shfl_xor((int)mymax, off));
-        myf += (uint32_t)__shfl_xor((int)myf, off);
-    }
-    if (lane == 0u) {
-        atomicMax(&tmax, mymax);
-        atomicAdd(&tfol, myf);
-    }
-    __syncthreads();
-    if (tfol == 0u) return;  // block-uniform
-    // digits of the followers' segment ids, 8 bits per pass: passes past the tile's largest id only
-    // see digit 0 (one add of the tile's follower count)
-    const uint32_t tp = (bits_for(tmax + 1u) + 7u) / 8u;
-    for (uint32_t p = 0; p < tp; ++p) {  // tp is block-uniform
-#pragma unroll
-        for (uint32_t r = 0; r < kRows; ++r) {
-            const uint32_t j = base + r * kBlock + t;
-            const bool v = j < nv && !((isl >> r) & 1u);
-            const uint32_t d = (kk[r] >> (8u * p)) & 255u;
-            const uint64_t peers = digit_peers(v, d, 8u);
-            if (v && (peers & lt) == 0) atomicAdd(&lh[p][d], (uint32_t)__popcll(peers));
+            fkey[j - before] = lead[r];
+            fval[j - before] = pk;
         }
     }
-    __syncthreads();
-    for (uint32_t p = 0; p < tp; ++p)
-        if (lh[p][t]) atomicAdd(ghist + 256u * p + t, lh[p][t]);
-    if (t == 0u)
-        for (uint32_t p = tp; p < 4u; ++p) atomicAdd(ghist + 256u * p, tfol);
 }
 
-// At most kSmallF followers (a batch of mostly single-packet segments): k_dm_onesweep's pass-0 block 0
-// sorts them alone, A -> B, by counting for each follower the followers that precede it in
-// (segment id, arrival) order, and the radix passes return at once.
+// The followers' radix keys + the global digit histograms of every radix pass: fkey[f] (its leader,
+// written by k_dm_leader_rank) becomes the leader's segment id in place; one tile of kTile followers
+// per block, LDS histograms per pass, one global atomic per non-empty bin.  Leaders are not sorted:
+// they already stand in segment order (k_dm_final).
+// At most kSmallF followers (a batch of mostly single-packet segments): block 0 sorts them alone, in
+// place, by counting for each follower the followers that precede it in (segment id, arrival) order,
+// and the radix passes return at once.
 constexpr uint32_t kSmallF = 1024;
-__device__ void small_sort(uint32_t nf, const uint32_t *keys, const uint32_t *vals, uint32_t *kout, uint32_t *vout,
-                           uint32_t *sk, uint32_t *sv) {
-    const uint32_t t = threadIdx.x;  // sk, sv: LDS arrays of >= kSmallF entries
-    constexpr uint32_t kPer = kSmallF / kBlock;
-    uint32_t kk[kPer], vv[kPer];
+__global__ __launch_bounds__(kBlock) void k_dm_segof_hist(const uint32_t *nvp, const uint32_t *nsegp,
+                                                          const uint32_t *rank_at, uint32_t *keys, uint32_t *vals,
+                                                          uint32_t *ghist) {
+    __shared__ uint32_t lh[4][256];
+    __shared__ uint32_t sk[kSmallF], sv[kSmallF];
+    const uint32_t ns = *nsegp, nf = *nvp - ns, t = threadIdx.x, lane = t & 63u;
+    const uint32_t base = blockIdx.x * kTile;
+    if (base >= nf) return;  // block-uniform
+    if (nf <= kSmallF) {  // block 0 only (base = 0)
+        constexpr uint32_t kPer = kSmallF / kBlock;
+        uint32_t ld[kPer], kk[kPer], vv[kPer];
 #pragma unroll
-    for (uint32_t r = 0; r < kPer; ++r) {
-        const uint32_t f = r * kBlock + t;
-        kk[r] = f < nf ? keys[f] : 0u;
-        vv[r] = f < nf ? vals[f] : 0u;
-        if (f < nf) {
-            sk[f] = kk[r];
-            sv[f] = vv[r];
+        for (uint32_t r = 0; r < kPer; ++r) {
+            const uint32_t f = r * kBlock + t;
+            ld[r] = f < nf ? keys[f] : 0u;
+            vv[r] = f < nf ? vals[f] : 0u;
+        }
+#pragma unroll
+        for (uint32_t r = 0; r < kPer; ++r) {
+            const uint32_t f = r * kBlock + t;
+            kk[r] = f < nf ? rank_at[ld[r]] : 0u;
+            if (f < nf) {  // every global read is consumed before the barrier: the writes below are in place
+                sk[f] = kk[r];
+                sv[f] = vv[r];
+            }
+        }
+        __syncthreads();
+        uint32_t pos[kPer] = {};
+        for (uint32_t g = 0; g < nf; ++g) {  // sk[g] is an LDS broadcast
+            const uint32_t kg = sk[g];
+#pragma unroll
+            for (uint32_t r = 0; r < kPer; ++r) pos[r] += kg < kk[r] || (kg == kk[r] && g < r * kBlock + t);
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t r = 0; r < kPer; ++r) {
+            if (r * kBlock + t >= nf) continue;
+            keys[pos[r]] = kk[r];
+            vals[pos[r]] = sv[r * kBlock + t];
+        }
+        return;
+    }
+    const uint32_t np = n_passes(ns), width = digit_width(ns), dm = (1u << width) - 1u;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) lh[p][t] = 0u;
+    __syncthreads();
+    uint32_t kk[kItems], ld[kItems];  // all leader loads, then all rank_at gathers, in flight at once
+#pragma unroll
+    for (uint32_t r = 0; r < kItems; ++r) {
+        const uint32_t f = base + r * kBlock + t;
+        ld[r] = f < nf ? keys[f] : 0u;
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < kItems; ++r) {
+        const uint32_t f = base + r * kBlock + t;
+        kk[r] = f < nf ? rank_at[ld[r]] : 0u;
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < kItems; ++r) {
+        const uint32_t f = base + r * kBlock + t;
+        if (f < nf) keys[f] = kk[r];
+    }
+    for (uint32_t p = 0; p < np; ++p) {  // np is block-uniform
+#pragma unroll
+        for (uint32_t r = 0; r < kItems; ++r) {
+            const bool v = base + r * kBlock + t < nf;
+            const uint32_t d = (kk[r] >> (width * p)) & dm;
+            const uint64_t peers = digit_peers(v, d, width);
+            if (v && (peers & lanemask_lt(lane)) == 0) atomicAdd(&lh[p][d], (uint32_t)__popcll(peers));
         }
     }
     __syncthreads();
-    uint32_t pos[kPer] = {};
-    for (uint32_t g = 0; g < nf; ++g) {  // sk[g] is an LDS broadcast
-        const uint32_t kg = sk[g];
-#pragma unroll
-        for (uint32_t r = 0; r < kPer; ++r) pos[r] += kg < kk[r] || (kg == kk[r] && g < r * kBlock + t);
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t r = 0; r < kPer; ++r) {
-        if (r * kBlock + t >= nf) continue;
-        kout[pos[r]] = kk[r];
-        vout[pos[r]] = sv[r * kBlock + t];
-    }
+    for (uint32_t p = 0; p < np; ++p)
+        if (lh[p][t]) atomicAdd(ghist + 256u * p + t, lh[p][t]);
 }
 
 // One radix pass, onesweep: tile t (= block t, dispatch order) ranks its items stably, gets the count
@@ -699,12 +682,8 @@ __global__ __launch_bounds__(kBlock) void k_dm_onesweep(uint32_t pass, const uin
     __shared__ uint32_t lbase[256], dbase[256];
     __shared__ uint32_t sk[kTile], sv[kTile];
     const uint32_t ns = *nsegp, nv = *nvp - ns, tile = blockIdx.x;  // nv: the followers being sorted
-    if (nv <= kSmallF) {  // block-uniform
-        if (pass == 0u && tile == 0u && nv > 0u) small_sort(nv, kin, vin, kout, vout, sk, sv);
-        return;
-    }
-    if (pass >= n_passes(ns) || tile * kTile >= nv) return;  // block-uniform; no later tile waits
-    const uint32_t sh = 8u * pass;  // the histograms' fixed 8-bit digits
+    if (pass >= n_passes(ns) || tile * kTile >= nv || nv <= kSmallF) return;  // block-uniform; no later tile waits
+    const uint32_t width = digit_width(ns), sh = width * pass, dm = (1u << width) - 1u;
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     const uint32_t base = tile * kTile, wbase = base + w * kPerWave;
     const uint32_t cnt = nv - base < kTile ? nv - base : kTile;
@@ -722,8 +701,8 @@ __global__ __launch_bounds__(kBlock) void k_dm_onesweep(uint32_t pass, const uin
 #pragma unroll
     for (uint32_t r = 0; r < kItems; ++r) {  // wave-local: the wave's rows in item order
         const bool v = wbase + r * 64u + lane < nv;
-        const uint32_t d = (kk[r] >> sh) & 255u;
-        const uint64_t peers = digit_peers(v, d, 8u);
+        const uint32_t d = (kk[r] >> sh) & dm;
+        const uint64_t peers = digit_peers(v, d, width);
         const uint32_t below = (uint32_t)__popcll(peers & lt);
         const uint32_t c = v ? wcnt[w][d] : 0u;
         rk[r] = c + below;
@@ -773,14 +752,14 @@ __global__ __launch_bounds__(kBlock) void k_dm_onesweep(uint32_t pass, const uin
 #pragma unroll
     for (uint32_t r = 0; r < kItems; ++r) {
         if (wbase + r * 64u + lane >= nv) continue;
-        const uint32_t d = (kk[r] >> sh) & 255u;
+        const uint32_t d = (kk[r] >> sh) & dm;
         const uint32_t pos = lbase[d] + wcnt[w][d] + rk[r];
         sk[pos] = kk[r];
         sv[pos] = vv[r];
     }
     __syncthreads();
     for (uint32_t p = t; p < cnt; p += kBlock) {
-        const uint32_t key = sk[p], d = (key >> sh) & 255u;
+        const uint32_t key = sk[p], d = (key >> sh) & dm;
         const uint32_t g = dbase[d] + (p - lbase[d]);
         kout[g] = key;
         vout[g] = sv[p];
@@ -797,7 +776,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_final(const uint32_t *nvp, const 
                                                      uint32_t *n_seg, uint32_t *n_valid) {
     const uint32_t nv = *nvp, ns = *nsegp, nf = nv - ns;
     const uint32_t passes = n_passes(ns);  // effective passes; pass p writes B when p is even
-    const bool inB = nf <= kSmallF || ((passes - 1u) & 1u) == 0u;  // small: sorted by pass 0 into B
+    const bool inB = nf > kSmallF && ((passes - 1u) & 1u) == 0u;  // small: sorted in place in A
     const uint32_t *keys = inB ? kB : kA;
     const uint32_t *vals = inB ? vB : vA;
     const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
@@ -849,6 +828,7 @@ size_t dm_layout(uint32_t n, uint8_t *base, DmWs *w) {
     d.cidx = (uint32_t *)take(4ull * n);
     d.cep = (uint32_t *)take(4ull * n);
     d.hslot = (uint32_t *)take(4ull * n);
+    d.rank_at = (uint32_t *)take(4ull * n);
     d.kA = (uint32_t *)take(4ull * n);
     d.vA = (uint32_t *)take(4ull * n);
     d.kB = (uint32_t *)take(4ull * n);
@@ -857,7 +837,6 @@ size_t dm_layout(uint32_t n, uint8_t *base, DmWs *w) {
     d.nv = (uint32_t *)take(8);
     d.nseg = (uint32_t *)take(8);
     const size_t fill0 = off;
-    d.rank_at = (uint32_t *)take(4ull * n);  // filled: kNone until the leader's tile stores its rank
     d.slots = (unsigned long long *)take(8ull * T);
     d.st_v = (unsigned long long *)take(8ull * nt);
     d.st_c = (unsigned long long *)take(8ull * nt);
@@ -908,17 +887,19 @@ extern "C" int rsk_demux_batch(rsk_ctx *c, uint32_t n, const rsk_demux_in *in, u
     a.dst = in->dst;
     a.n = n;
     a.fields = fields;
-    // one fill: rank_at, the key table and every look-back state word start as all-ones
-    hipError_t e = hipMemsetAsync(w.rank_at, 0xff, w.fill_bytes, s);  // rank_at .. the last state word
+    // one fill: the key table and every look-back state word start as all-ones
+    hipError_t e = hipMemsetAsync(w.slots, 0xff, w.fill_bytes, s);
     if (e != hipSuccess) { rsk::set_error("hipMemsetAsync(table)", e); return RSK_EDEVICE; }
     const uint32_t nb = w.nb;
     hipLaunchKernelGGL(k_dm_flags_prep, dim3(w.nt), dim3(kBlock), 0, s, a, w.st_v, w.st_c, w.cidx, w.cep, w.nv,
-                       w.ghist, c->err_dev);
+                       c->err_dev);
     hipLaunchKernelGGL(k_dm_insert, dim3((n + kInsTile - 1) / kInsTile), dim3(kBlock), 0, s, a, w.nv, w.cidx,
                        w.cep, w.slots, w.tsize - 1u, w.hslot);
     hipLaunchKernelGGL(k_dm_leader_rank, dim3(w.nt), dim3(kBlock), 0, s, w.nv, w.hslot, w.slots, w.cidx, w.st_l,
                        w.kA, w.vA, w.rank_at, out->seg_first, w.nseg, w.ghist, c->err_dev);
-    if ((r = rsk::launch_check("k_dm_leader_rank"))) return r;
+    hipLaunchKernelGGL(k_dm_segof_hist, dim3(w.nt), dim3(kBlock), 0, s, w.nv, w.nseg, w.rank_at, w.kA, w.vA,
+                       w.ghist);
+    if ((r = rsk::launch_check("k_dm_segof_hist"))) return r;
     // passes for the largest possible segment count (n); surplus passes return at once
     uint32_t maxbits = 1;
     while (maxbits < 32 && (1ull << maxbits) < n) ++maxbits;
