@@ -31,6 +31,7 @@
 // batch of mostly single-packet segments skips the sort's work)
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 
 #include "../../include/rsk_codec.h"
@@ -268,6 +269,7 @@ __device__ __forceinline__ uint64_t key_hash(const Key &k) {
 // compare-and-swap (the fingerprint half never changes once claimed).  A relaxed load comes first:
 // a hot key's slot is read, not written, by every later tile (no RMW unless the index drops); a new
 // key costs the load and one CAS (round 2, first half: a load, a CAS and a separate atomicMin word).
+template <int V = 0>
 __device__ __forceinline__ uint32_t global_probe(const DmIn &a, const uint32_t *cidx, const uint32_t *cep,
                                                  unsigned long long *slots, uint32_t mask, const Key &k,
                                                  uint64_t hv, uint32_t j) {
@@ -275,14 +277,14 @@ __device__ __forceinline__ uint32_t global_probe(const DmIn &a, const uint32_t *
     const unsigned long long mine = ((unsigned long long)fp << 32) | j;
     uint32_t h = (uint32_t)hv & mask;
     for (;;) {
-        unsigned long long e = __hip_atomic_load(slots + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned long long e = V == 2 ? slots[h] : __hip_atomic_load(slots + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (e == ~0ull) {
             e = atomicCAS(slots + h, ~0ull, mine);
             if (e == ~0ull) return h;  // claimed
         }
         if ((uint32_t)(e >> 32) == fp) {
             const uint32_t o = (uint32_t)e;
-            if (key_eq(load_key(a, cidx[o], cep[o]), k)) {
+            if (V == 3 || key_eq(load_key(a, cidx[o], cep[o]), k)) {  // V 3 (A/B timing only): no confirmation
                 while ((uint32_t)e > j) {  // lower the key's first index to j
                     const unsigned long long f = atomicCAS(slots + h, e, mine);
                     if (f == e) break;
@@ -310,6 +312,9 @@ constexpr uint32_t kLeadTag = 0x80000000u;  // hslot: leader index (table slots 
 constexpr uint32_t kInsTile = kBlock * kInsItems;  // 1024 packets (24 KB LDS: 6 waves per SIMD)
 constexpr uint32_t kLtab = 2 * kInsTile;           // LDS table slots (power of 2)
 
+// V (A/B build, RSK_DM_VARIANT, timing only -- 1 and 3 give wrong segments): 1 = no global probe,
+// 2 = the probe's first load a plain (L2-cached) load, 3 = no key confirmation.
+template <int V = 0>
 __global__ __launch_bounds__(kBlock) void k_dm_insert(DmIn a, const uint32_t *nvp, const uint32_t *cidx,
                                                       const uint32_t *cep, unsigned long long *slots,
                                                       uint32_t mask, uint32_t *hslot) {
@@ -390,8 +395,9 @@ __global__ __launch_bounds__(kBlock) void k_dm_insert(DmIn a, const uint32_t *nv
         if (!((rep >> it) & 1u)) continue;
         const uint32_t j = base + it * kBlock + t;
         const Key &k = kr[it];
-        lmin[lpos[it]] = k.ep == elo || k.ep == ehi ? global_probe(a, cidx, cep, slots, mask, k, key_hash(k), j)
-                                                    : kLeadTag | j;
+        lmin[lpos[it]] = V != 1 && (k.ep == elo || k.ep == ehi)
+                             ? global_probe<V>(a, cidx, cep, slots, mask, k, key_hash(k), j)
+                             : kLeadTag | j;
     }
     __syncthreads();
 #pragma unroll
@@ -893,8 +899,19 @@ extern "C" int rsk_demux_batch(rsk_ctx *c, uint32_t n, const rsk_demux_in *in, u
     const uint32_t nb = w.nb;
     hipLaunchKernelGGL(k_dm_flags_prep, dim3(w.nt), dim3(kBlock), 0, s, a, w.st_v, w.st_c, w.cidx, w.cep, w.nv,
                        c->err_dev);
-    hipLaunchKernelGGL(k_dm_insert, dim3((n + kInsTile - 1) / kInsTile), dim3(kBlock), 0, s, a, w.nv, w.cidx,
+#ifdef RSK_AB
+    static const int dmv = getenv("RSK_DM_VARIANT") ? atoi(getenv("RSK_DM_VARIANT")) : 0;
+#define RSK_DM_INS(V) hipLaunchKernelGGL(k_dm_insert<V>, dim3((n + kInsTile - 1) / kInsTile), dim3(kBlock), 0, s, a, \
+                                         w.nv, w.cidx, w.cep, w.slots, w.tsize - 1u, w.hslot)
+    if (dmv == 1) RSK_DM_INS(1);
+    else if (dmv == 2) RSK_DM_INS(2);
+    else if (dmv == 3) RSK_DM_INS(3);
+    else RSK_DM_INS(0);
+#undef RSK_DM_INS
+#else
+    hipLaunchKernelGGL(k_dm_insert<0>, dim3((n + kInsTile - 1) / kInsTile), dim3(kBlock), 0, s, a, w.nv, w.cidx,
                        w.cep, w.slots, w.tsize - 1u, w.hslot);
+#endif
     hipLaunchKernelGGL(k_dm_leader_rank, dim3(w.nt), dim3(kBlock), 0, s, w.nv, w.hslot, w.slots, w.cidx, w.st_l,
                        w.kA, w.vA, w.rank_at, out->seg_first, w.nseg, w.ghist, c->err_dev);
     hipLaunchKernelGGL(k_dm_segof_hist, dim3(w.nt), dim3(kBlock), 0, s, w.nv, w.nseg, w.rank_at, w.kA, w.vA,

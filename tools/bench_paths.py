@@ -68,9 +68,8 @@ def main():
         "decode": lambda: cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, w.dec, stream=s),
         "parse_decode": lambda: cx.rawinput_batch(wiree, offe, ste, ste, 1, 0, tcp, pdec, stream=s),
     }
-    # the A/B build (RSK_LIB=librsk_ab.so) exposes the wire variants: 1 per-packet, 2 flat, 3 one-launch
-    ab = os.environ.get("RSK_LIB", "") == "librsk_ab.so"
-    for v in ([1, 2, 3] if ab else []) + [int(x) for x in args.wire_variants.split(",") if x]:
+    # the A/B build (RSK_LIB=librsk_ab.so) exposes rsk__set_wire_variant (0, 8, 10): --wire-variants
+    for v in [int(x) for x in args.wire_variants.split(",") if x]:
         ops[f"encode_wire_raw4_v{v}"] = (lambda v=v: (cx.set_wire_variant(v), cx.output_wire_batch(
             *common, src, dst, sp, dp, seq, ack, flag, ipid, wire4, off4, st4, id_uniform=workload.ID_UNIFORM,
             stream=s, **wpad), cx.set_wire_variant(0)))
