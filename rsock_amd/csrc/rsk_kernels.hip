@@ -1554,6 +1554,7 @@ __device__ __forceinline__ void copy_wire_pkt_dpp(const EncArgs &a, const KeySch
         uint4 A[PU][2];
         uint32_t wlen[PU], shp[PU];
         uint8_t *dstp[PU];
+        bool ld1[PU];  // source chunk 64 holds payload bytes (slot 1 loaded; lane 63's funnel partner)
 #pragma unroll
         for (int p = 0; p < PU; ++p) {
             wlen[p] = on[p] ? (uint32_t)rdl((uint32_t)wst, js[p]) : 0u;
@@ -1563,10 +1564,13 @@ __device__ __forceinline__ void copy_wire_pkt_dpp(const EncArgs &a, const KeySch
             shp[p] = (uint32_t)((reinterpret_cast<uintptr_t>(pay) + G::D0) & 15u);
             const uint8_t *src_al = pay + G::D0 - shp[p];
             const int32_t last_rel = (int32_t)P - 1 - G::D0 + (int32_t)shp[p];
+            ld1[p] = on[p] && last_rel >= 16 * 64;
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
                 const uint32_t m = lane + 64u * q;  // source chunk of frame chunk NPRE + m
                 A[p][q] = make_uint4(0u, 0u, 0u, 0u);
+                // slot 1 only for payloads reaching source chunk 64 (uniform: most C4 packets do not)
+                if (q == 1 && !ld1[p]) continue;
                 if (on[p] && (int32_t)(16u * m) <= last_rel) A[p][q] = ld16<0>(src_al + 16u * m);
             }
         }
@@ -1595,14 +1599,23 @@ __device__ __forceinline__ void copy_wire_pkt_dpp(const EncArgs &a, const KeySch
         for (int p = 0; p < PU; ++p) {
             uint4 B[2];
             B[0] = make_uint4(wave_shl1(A[p][0].x), wave_shl1(A[p][0].y), wave_shl1(A[p][0].z), wave_shl1(A[p][0].w));
-            B[1] = make_uint4(wave_shl1(A[p][1].x), wave_shl1(A[p][1].y), wave_shl1(A[p][1].z), wave_shl1(A[p][1].w));
-            const uint4 l0 = make_uint4(rdl(A[p][1].x, 0), rdl(A[p][1].y, 0), rdl(A[p][1].z, 0),
-                                        rdl(A[p][1].w, 0));  // read in uniform flow (see k_encode)
-            if (lane == 63u) B[0] = l0;
+            B[1] = make_uint4(0u, 0u, 0u, 0u);
             const uint32_t nch = (wlen[p] + 15u) >> 4;
+            // round 4: slot 1's shifts, funnels and sums only for packets that reach it (uniform); a
+            // dead slot 1 holds zeros, which is what the zero-pad stores below need
+            const bool s1 = nch > (uint32_t)G::NPRE + 64u;  // implies ld1[p]
+            if (ld1[p]) {
+                const uint4 l0 = make_uint4(rdl(A[p][1].x, 0), rdl(A[p][1].y, 0), rdl(A[p][1].z, 0),
+                                            rdl(A[p][1].w, 0));  // read in uniform flow (see k_encode)
+                if (lane == 63u) B[0] = l0;
+            }
+            if (s1)
+                B[1] = make_uint4(wave_shl1(A[p][1].x), wave_shl1(A[p][1].y), wave_shl1(A[p][1].z), wave_shl1(A[p][1].w));
             uint32_t part = 0;
+            v[p][1] = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
+                if (q == 1 && !s1) continue;  // uniform
                 const uint32_t k = G::NPRE + lane + 64u * q;
                 v[p][q] = rsk::funnel16(A[p][q], B[q], shp[p]);
                 const int lim = (int)wlen[p] - 16 * (int)k;
@@ -1631,6 +1644,7 @@ __device__ __forceinline__ void copy_wire_pkt_dpp(const EncArgs &a, const KeySch
                 }
 #pragma unroll
                 for (int q = 0; q < 2; ++q) {
+                    if (q == 1 && nst <= (uint32_t)G::NPRE + 64u) continue;  // uniform
                     const uint32_t k = G::NPRE + lane + 64u * q;
                     if (k < nst) store_last16<NT>(dstp[p] + 16u * k, v[p][q], (int)wlen[p] - 16 * (int)k, a.pad != 0u);
                 }
