@@ -1564,7 +1564,10 @@ __device__ __forceinline__ void copy_wire_pkt_dpp(const EncArgs &a, const KeySch
             shp[p] = (uint32_t)((reinterpret_cast<uintptr_t>(pay) + G::D0) & 15u);
             const uint8_t *src_al = pay + G::D0 - shp[p];
             const int32_t last_rel = (int32_t)P - 1 - G::D0 + (int32_t)shp[p];
-            ld1[p] = on[p] && last_rel >= 16 * 64;
+            // round 4: slot 1 skipped for packets that do not reach it -- RAW4 only: measured on
+            // Ethernet packets it cost more (SGPR spills 392 -> 450, C4 0.421 -> 0.451 ms) than it saved
+            // (RAW4 C4 0.455 -> 0.413 ms, C3 2.339 -> 2.295; profiles/r04_paths_wire.json)
+            ld1[p] = E != 0 || (on[p] && last_rel >= 16 * 64);
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
                 const uint32_t m = lane + 64u * q;  // source chunk of frame chunk NPRE + m
@@ -1603,7 +1606,7 @@ __device__ __forceinline__ void copy_wire_pkt_dpp(const EncArgs &a, const KeySch
             const uint32_t nch = (wlen[p] + 15u) >> 4;
             // round 4: slot 1's shifts, funnels and sums only for packets that reach it (uniform); a
             // dead slot 1 holds zeros, which is what the zero-pad stores below need
-            const bool s1 = nch > (uint32_t)G::NPRE + 64u;  // implies ld1[p]
+            const bool s1 = E != 0 || nch > (uint32_t)G::NPRE + 64u;  // implies ld1[p]
             if (ld1[p]) {
                 const uint4 l0 = make_uint4(rdl(A[p][1].x, 0), rdl(A[p][1].y, 0), rdl(A[p][1].z, 0),
                                             rdl(A[p][1].w, 0));  // read in uniform flow (see k_encode)
@@ -1644,7 +1647,7 @@ __device__ __forceinline__ void copy_wire_pkt_dpp(const EncArgs &a, const KeySch
                 }
 #pragma unroll
                 for (int q = 0; q < 2; ++q) {
-                    if (q == 1 && nst <= (uint32_t)G::NPRE + 64u) continue;  // uniform
+                    if (E == 0 && q == 1 && nst <= (uint32_t)G::NPRE + 64u) continue;  // uniform
                     const uint32_t k = G::NPRE + lane + 64u * q;
                     if (k < nst) store_last16<NT>(dstp[p] + 16u * k, v[p][q], (int)wlen[p] - 16 * (int)k, a.pad != 0u);
                 }
