@@ -1251,6 +1251,16 @@ __global__ __launch_bounds__(kBlock) void k_encode(EncArgs a, KeySched ks) {
     encode_grid<MODE, PU, U, NT, GRP, SBW, XCD, TG>(a, ks);
 }
 
+#ifdef RSK_AB
+// A/B build only (round 4): the same kernel forced to MINW waves per SIMD (its register budget cut to
+// 512 / MINW VGPRs): how much C2's flat sets, which need few registers, gain from occupancy (the
+// long-frame copy spills at this budget, so C3 / C4 are expected to lose).
+template <int MINW>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MINW, 8))) void k_encode_occ(EncArgs a, KeySched ks) {
+    encode_grid<11, 4, 4, -1, 8, 1024, false, 0>(a, ks);
+}
+#endif
+
 // the same kernel held to 128 VGPRs (4 waves per SIMD): W = 8 lets the compiler aim higher, W = 4 not
 template <int MODE, int PU, int U, int NT, int GRP, int SBW, int TG, int W>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, W))) void k_encode_w4(EncArgs a, KeySched ks) {
@@ -3138,12 +3148,13 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 // nontemporal stores; 73 / 74 = memory-pattern probes (wrong bytes: k_probe_gi, the shipped mapping and
 // batches; k_probe_one, one wave per packet); 75 / 76 = the two-pass form (k_enc_heads then
 // k_enc_copy1, normal / nontemporal stores); 77 / 78 / 79 / 80 / 81 = k_enc_few, 1 / 2 / 4 / 8 / 16 packets
-// per wave, 82 = 78 with nontemporal stores (round 4).  Rounds 1-2
+// per wave, 82 = 78 with nontemporal stores; 83 / 84 = k_encode_occ (0 forced to 8 / 6 waves per
+// SIMD) (round 4).  Rounds 1-2
 // measured ~45 more variants (profiles/r01_ab_*, r02_ab_*); their code is in the git history.
 // v + 100 * cap (cap 1..4): the same kernel held to `cap` blocks per CU by unused LDS.
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
     const int k = v % 100;
-    if (!c || v < 0 || v / 100 > 4 || !(k == 0 || k == 12 || k == 13 || k == 37 || k == 47 || (k >= 50 && k <= 82)))
+    if (!c || v < 0 || v / 100 > 4 || !(k == 0 || k == 12 || k == 13 || k == 37 || k == 47 || (k >= 50 && k <= 84)))
         return RSK_EINVAL;
     c->enc_variant = v;
     return RSK_OK;
@@ -3330,6 +3341,8 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         case 71: hipLaunchKernelGGL((k_encode_bc<4, 0>), dim3((unsigned)((n + 63ull) / 64ull)), dim3(1024), lds, st, a, c->ks); break;
         case 72: hipLaunchKernelGGL((k_encode_bc<1, 2>), dim3((unsigned)((n + 15ull) / 16ull)), dim3(1024), lds, st, a, c->ks); break;
         case 73: hipLaunchKernelGGL(k_probe_gi, dim3(enc_grid(n, 8, 1024)), bd, lds, st, a); break;
+        case 83: hipLaunchKernelGGL((k_encode_occ<8>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
+        case 84: hipLaunchKernelGGL((k_encode_occ<6>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
         case 77: hipLaunchKernelGGL((k_enc_few<1, 1, 0>), dim3((unsigned)((n + 3ull) / 4ull)), bd, lds, st, a, c->ks); break;
         case 78: hipLaunchKernelGGL((k_enc_few<2, 2, 0>), dim3((unsigned)((n + 7ull) / 8ull)), bd, lds, st, a, c->ks); break;
         case 79: hipLaunchKernelGGL((k_enc_few<4, 4, 0>), dim3((unsigned)((n + 15ull) / 16ull)), bd, lds, st, a, c->ks); break;
