@@ -1157,6 +1157,85 @@ __global__ __launch_bounds__(kBlock) void k_probe_one(EncArgs a) {
     }
 }
 
+// persistent: NW waves, wave w copies packets w, w + NW, ... one per iteration; PIPE: the next
+// packet's loads issued before the current packet's stores.  CH > 1: wave w copies CH consecutive
+// packets [CH w, CH w + CH), one at a time (one-shot waves, linear mapping).
+template <bool PIPE>
+__global__ __launch_bounds__(kBlock) void k_probe_persist(EncArgs a) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t w0 = (uint64_t)blockIdx.x * kWavesPerBlock + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
+    auto issue = [&](uint64_t i, uint4 (&A)[2], uint8_t *&dst, uint32_t &nch) {
+        const uint32_t P = i < a.n ? a.pay_len[i] : 0u;
+        const uint8_t *src;
+        uint32_t nsrc;
+        probe_geo(a, i < a.n ? a.pay_off[i] : 0u, i < a.n ? a.frame_off[i] : 0u, P, src, dst, nsrc, nch);
+        if (i >= a.n) nsrc = nch = 0u;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const uint32_t k = lane + 64u * q;
+            A[q] = ld16<0>(k < nsrc ? src + 16u * k : src);
+        }
+    };
+    auto store = [&](const uint4 (&A)[2], uint8_t *dst, uint32_t nch) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const uint32_t k = lane + 64u * q;
+            if (k < nch) st16<0>(dst + 16u * k, A[q]);
+        }
+    };
+    if constexpr (!PIPE) {
+        for (uint64_t i = w0; i < a.n; i += nw) {
+            uint4 A[2];
+            uint8_t *dst;
+            uint32_t nch;
+            issue(i, A, dst, nch);
+            store(A, dst, nch);
+        }
+    } else {
+        uint4 A0[2], A1[2];
+        uint8_t *d0, *d1;
+        uint32_t c0, c1;
+        uint64_t i = w0;
+        if (i >= a.n) return;
+        issue(i, A0, d0, c0);
+        while (true) {
+            const uint64_t j = i + nw;
+            if (j < a.n) issue(j, A1, d1, c1);
+            store(A0, d0, c0);
+            if (j >= a.n) break;
+            i = j + nw;
+            if (i < a.n) issue(i, A0, d0, c0);
+            store(A1, d1, c1);
+            if (i >= a.n) break;
+        }
+    }
+}
+
+template <int CH>
+__global__ __launch_bounds__(kBlock) void k_probe_chunk(EncArgs a) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t w = (uint64_t)blockIdx.x * kWavesPerBlock + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    for (uint64_t i = w * CH; i < a.n && i < w * CH + CH; ++i) {
+        const uint8_t *src;
+        uint8_t *dst;
+        uint32_t nsrc, nch;
+        probe_geo(a, a.pay_off[i], a.frame_off[i], a.pay_len[i], src, dst, nsrc, nch);
+        uint4 A[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const uint32_t k = lane + 64u * q;
+            A[q] = make_uint4(0u, 0u, 0u, 0u);
+            if (k < nsrc) A[q] = ld16<0>(src + 16u * k);
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const uint32_t k = lane + 64u * q;
+            if (k < nch) st16<0>(dst + 16u * k, A[q]);
+        }
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void k_probe_gi(EncArgs a) {
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     const uint64_t wg = (uint64_t)blockIdx.x * kWavesPerBlock + w;
@@ -3149,12 +3228,13 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 // batches; k_probe_one, one wave per packet); 75 / 76 = the two-pass form (k_enc_heads then
 // k_enc_copy1, normal / nontemporal stores); 77 / 78 / 79 / 80 / 81 = k_enc_few, 1 / 2 / 4 / 8 / 16 packets
 // per wave, 82 = 78 with nontemporal stores; 83 / 84 = k_encode_occ (0 forced to 8 / 6 waves per
-// SIMD) (round 4).  Rounds 1-2
+// SIMD); 85 / 86 / 88 = k_probe_persist (2048 blocks / 2048 pipelined / 4096 blocks), 87 / 89 =
+// k_probe_chunk<8 / 2> (plain-copy probes, wrong bytes) (round 4).  Rounds 1-2
 // measured ~45 more variants (profiles/r01_ab_*, r02_ab_*); their code is in the git history.
 // v + 100 * cap (cap 1..4): the same kernel held to `cap` blocks per CU by unused LDS.
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
     const int k = v % 100;
-    if (!c || v < 0 || v / 100 > 4 || !(k == 0 || k == 12 || k == 13 || k == 37 || k == 47 || (k >= 50 && k <= 84)))
+    if (!c || v < 0 || v / 100 > 4 || !(k == 0 || k == 12 || k == 13 || k == 37 || k == 47 || (k >= 50 && k <= 89)))
         return RSK_EINVAL;
     c->enc_variant = v;
     return RSK_OK;
@@ -3341,6 +3421,11 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         case 71: hipLaunchKernelGGL((k_encode_bc<4, 0>), dim3((unsigned)((n + 63ull) / 64ull)), dim3(1024), lds, st, a, c->ks); break;
         case 72: hipLaunchKernelGGL((k_encode_bc<1, 2>), dim3((unsigned)((n + 15ull) / 16ull)), dim3(1024), lds, st, a, c->ks); break;
         case 73: hipLaunchKernelGGL(k_probe_gi, dim3(enc_grid(n, 8, 1024)), bd, lds, st, a); break;
+        case 85: hipLaunchKernelGGL(k_probe_persist<false>, dim3(2048), bd, lds, st, a); break;
+        case 86: hipLaunchKernelGGL(k_probe_persist<true>, dim3(2048), bd, lds, st, a); break;
+        case 87: hipLaunchKernelGGL(k_probe_chunk<8>, dim3((unsigned)((n + 31ull) / 32ull)), bd, lds, st, a); break;
+        case 88: hipLaunchKernelGGL(k_probe_persist<false>, dim3(4096), bd, lds, st, a); break;
+        case 89: hipLaunchKernelGGL(k_probe_chunk<2>, dim3((unsigned)((n + 7ull) / 8ull)), bd, lds, st, a); break;
         case 83: hipLaunchKernelGGL((k_encode_occ<8>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
         case 84: hipLaunchKernelGGL((k_encode_occ<6>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
         case 77: hipLaunchKernelGGL((k_enc_few<1, 1, 0>), dim3((unsigned)((n + 3ull) / 4ull)), bd, lds, st, a, c->ks); break;
