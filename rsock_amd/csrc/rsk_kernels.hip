@@ -530,6 +530,10 @@ __device__ __forceinline__ void pkt_issue(const EncArgs &a, const Lane1 &L, uint
             const int32_t m = (int32_t)(lane + 64u * q) - 2;
             const bool live = on[p] && m >= 0 && src_chunk_live(m, g.first_rel, g.last_rel);
             const uint4 v = ld16<NT>(live ? g.srcp + 16 * m : dummy);
+            // zeroed here, which makes the compiler wait for the batch's loads at issue: round 4 moved
+            // the zeroing after the wait (true two-batch overlap, vmcnt(6-7) instead of vmcnt(0)) and
+            // measured C3 unchanged, C4 +2 % (profiles/r04_ab_pipeline.json): the memory system, not
+            // the per-wave depth, sets the pace
             A[p][q] = live ? v : make_uint4(0u, 0u, 0u, 0u);
         }
     }
@@ -582,15 +586,15 @@ __device__ __forceinline__ void pkt_store(const EncArgs &a, const KeySched &ks, 
         const uint32_t fl = rdl((uint32_t)L.st, js[p]);
         const FrameGeo g = frame_geo(a.payload + rdl64(L.po, js[p]), a.frame + rdl64(L.fo, js[p]), fl, a.pad);
         const uint32_t flen = fl + g.r, nst = g.nst;
+        const uint4 (&Ap)[2] = A[p];
         uint4 B[2];
-        B[0] = make_uint4(wave_shl1(A[p][0].x), wave_shl1(A[p][0].y), wave_shl1(A[p][0].z), wave_shl1(A[p][0].w));
+        B[0] = make_uint4(wave_shl1(Ap[0].x), wave_shl1(Ap[0].y), wave_shl1(Ap[0].z), wave_shl1(Ap[0].w));
         B[1] = make_uint4(0u, 0u, 0u, 0u);
         if (nst >= 64u) {  // uniform: the frame reaches slot 1
-            const uint4 l0 = make_uint4(rdl(A[p][1].x, 0), rdl(A[p][1].y, 0), rdl(A[p][1].z, 0), rdl(A[p][1].w, 0));
+            const uint4 l0 = make_uint4(rdl(Ap[1].x, 0), rdl(Ap[1].y, 0), rdl(Ap[1].z, 0), rdl(Ap[1].w, 0));
             if (lane == 63u) B[0] = l0;
             if (nst > 64u)
-                B[1] = make_uint4(wave_shl1(A[p][1].x), wave_shl1(A[p][1].y), wave_shl1(A[p][1].z),
-                                  wave_shl1(A[p][1].w));
+                B[1] = make_uint4(wave_shl1(Ap[1].x), wave_shl1(Ap[1].y), wave_shl1(Ap[1].z), wave_shl1(Ap[1].w));
         }
         uint32_t Hj[8];
         bool hmerge = false, tmerge = false;
@@ -627,7 +631,7 @@ __device__ __forceinline__ void pkt_store(const EncArgs &a, const KeySched &ks, 
             const uint32_t k = lane + 64u * q;
             if (q == 1 && nst <= 64u) continue;  // uniform
             if constexpr (TAG) {
-                const uint4 V = rsk::funnel16(A[p][q], B[q], g.sh);
+                const uint4 V = rsk::funnel16(Ap[q], B[q], g.sh);
                 uint4 v = k < (g.r >= 2u ? 3u : 2u) ? head_chunk(Hj, k, g.r, V) : V;
                 uint32_t lo = k == 0u ? g.r : 0u;
                 if constexpr (MRG) {
@@ -645,7 +649,7 @@ __device__ __forceinline__ void pkt_store(const EncArgs &a, const KeySched &ks, 
                 store_piece<NT>(g.d0 + 16u * k, v, lo, (int)flen - 16 * (int)k, a.pad != 0u);
             } else {
                 if (k >= nst || k < 2u) continue;
-                const uint4 V = rsk::funnel16(A[p][q], B[q], g.sh);
+                const uint4 V = rsk::funnel16(Ap[q], B[q], g.sh);
                 store_piece<NT>(g.d0 + 16u * k, V, k == 2u ? chunk2_lo(g.r) : 0u, (int)flen - 16 * (int)k,
                                 a.pad != 0u);
             }
@@ -1783,8 +1787,7 @@ __device__ __forceinline__ void wire_issue(const EncArgs &a, const Lane1 &L, int
         for (int q = 0; q < 2; ++q) {
             const uint32_t m = lane + 64u * q;  // source chunk of frame chunk NPRE + m
             const bool live = on[p] && (int32_t)(16u * m) <= last_rel;
-            const uint4 v = ld16<0>(live ? src_al + 16u * m : dummy);
-            A[p][q] = live ? v : make_uint4(0u, 0u, 0u, 0u);
+            A[p][q] = ld16<0>(live ? src_al + 16u * m : dummy);  // dead lanes zeroed in wire_store (as pkt_issue)
         }
     }
 }
@@ -1833,11 +1836,16 @@ __device__ __forceinline__ void wire_store(const EncArgs &a, const KeySched &ks,
         const uint32_t wlen = on[p] ? (uint32_t)rdl((uint32_t)wst, js[p]) : 0u;
         uint8_t *dst = a.frame + rdl64(L.fo, js[p]);
         const uint32_t shp = (uint32_t)((reinterpret_cast<uintptr_t>(a.payload + rdl64(L.po, js[p])) + G::D0) & 15u);
+        const int32_t last_rel = (int32_t)(wlen - G::HB) - 1 - G::D0 + (int32_t)shp;
+        uint4 Ap[2];  // the issued loads, dead lanes zeroed (after the wait: see pkt_issue)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+            Ap[q] = on[p] && (int32_t)(16u * (lane + 64u * q)) <= last_rel ? A[p][q] : make_uint4(0u, 0u, 0u, 0u);
         uint4 B[2];
-        B[0] = make_uint4(wave_shl1(A[p][0].x), wave_shl1(A[p][0].y), wave_shl1(A[p][0].z), wave_shl1(A[p][0].w));
-        B[1] = make_uint4(wave_shl1(A[p][1].x), wave_shl1(A[p][1].y), wave_shl1(A[p][1].z), wave_shl1(A[p][1].w));
-        const uint4 l0 = make_uint4(rdl(A[p][1].x, 0), rdl(A[p][1].y, 0), rdl(A[p][1].z, 0),
-                                    rdl(A[p][1].w, 0));  // read in uniform flow (see k_encode)
+        B[0] = make_uint4(wave_shl1(Ap[0].x), wave_shl1(Ap[0].y), wave_shl1(Ap[0].z), wave_shl1(Ap[0].w));
+        B[1] = make_uint4(wave_shl1(Ap[1].x), wave_shl1(Ap[1].y), wave_shl1(Ap[1].z), wave_shl1(Ap[1].w));
+        const uint4 l0 = make_uint4(rdl(Ap[1].x, 0), rdl(Ap[1].y, 0), rdl(Ap[1].z, 0),
+                                    rdl(Ap[1].w, 0));  // read in uniform flow (see k_encode)
         if (lane == 63u) B[0] = l0;
         const uint32_t nch = (wlen + 15u) >> 4;
         const uint32_t nst = on[p] ? (padded_len(dst, wlen, a.pad) + 15u) >> 4 : 0u;
@@ -1845,7 +1853,7 @@ __device__ __forceinline__ void wire_store(const EncArgs &a, const KeySched &ks,
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
             const uint32_t k = G::NPRE + lane + 64u * q;
-            uint4 v = rsk::funnel16(A[p][q], B[q], shp);
+            uint4 v = rsk::funnel16(Ap[q], B[q], shp);
             const int lim = (int)wlen - 16 * (int)k;
             if (k < nch) {
                 if (lim < 16) v = rsk::keep_bytes16(v, lim);
@@ -3243,9 +3251,10 @@ int rsk__set_encode_variant(rsk_ctx *c, int v) {
 // Internal (A/B and tests): wire-build copy path.  0 = two-launch hybrid whose per-packet half uses the
 // one-load DPP copy, 8 packets per iteration, tag + payload prefix in the copy loop for sets of long
 // frames (default), 8 = 0 with the tag in phase 1, 10 = 0 on the tiled mapping (64 consecutive
-// packets per wave).  Rounds 1-2's other variants: profiles/r0*_ab_wire_*, code in the git history.
+// packets per wave), 11 / 12 = the software-pipelined per-packet copy (copy_wire_pkt_pipe, 4 / 3
+// packets per batch; round 4: its loads no longer waited for at issue).  Rounds 1-2's other variants: profiles/r0*_ab_wire_*, code in the git history.
 int rsk__set_wire_variant(rsk_ctx *c, int v) {
-    if (!c || !(v == 0 || v == 8 || v == 10)) return RSK_EINVAL;
+    if (!c || !(v == 0 || v == 8 || v == 10 || v == 11 || v == 12)) return RSK_EINVAL;
     c->wire_variant = v;
     return RSK_OK;
 }
@@ -3503,10 +3512,14 @@ int rsk_encode_wire_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const
     if (wire->with_eth) {
         if (v == 8) { RSK_WIRE(14, 3, 108, 2); RSK_WIRE(14, 4, 2, 2); }
         else if (v == 10) { RSK_WIRE4T(14, 5, 108, 2); RSK_WIRET(14, 4, 2, 2); }
+        else if (v == 11) { RSK_WIRE4(14, 5, 204, 2); RSK_WIRE(14, 4, 2, 2); }
+        else if (v == 12) { RSK_WIRE4(14, 5, 203, 2); RSK_WIRE(14, 4, 2, 2); }
         else { RSK_WIRE4(14, 5, 108, 2); RSK_WIRE(14, 4, 2, 2); }
     } else {
         if (v == 8) { RSK_WIRE(0, 3, 108, 2); RSK_WIRE(0, 4, 2, 2); }
         else if (v == 10) { RSK_WIRE4T(0, 5, 108, 2); RSK_WIRET(0, 4, 2, 2); }
+        else if (v == 11) { RSK_WIRE4(0, 5, 204, 2); RSK_WIRE(0, 4, 2, 2); }
+        else if (v == 12) { RSK_WIRE4(0, 5, 203, 2); RSK_WIRE(0, 4, 2, 2); }
         else { RSK_WIRE4(0, 5, 108, 2); RSK_WIRE(0, 4, 2, 2); }
     }
 #else
