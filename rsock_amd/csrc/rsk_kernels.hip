@@ -1108,6 +1108,152 @@ __global__ __launch_bounds__(kBlock) void k_enc_copy1(EncArgs a, const uint32_t 
     }
 }
 
+// A/B build only (round 4): look-ahead headers -- the one-wave-per-packet copy of k_enc_copy1 in ONE
+// launch.  Tile t = 64 consecutive packets = 16 blocks.  Wave 0 of tile t's first
+// block runs phase 1 + MD5 lane-per-packet for tile t + LA (for t < LA first for tile t itself) and
+// publishes the 32-B header records write-through (sc1 buffer stores, drained by s_waitcnt vmcnt(0))
+// behind one sc1 flag per tile; a packet's wave issues its chunk loads, polls its tile's flag (relaxed,
+// agent scope) and reads its record with sc1 loads (MI355X_MICROARCH.md, inter-workgroup visibility,
+// Valid forms, row 1).  A bounded spin falls back to the packet's own phase 1 + MD5, so the result
+// never depends on dispatch order.  The flags are zeroed per call (memset node before the kernel).
+constexpr uint32_t kLaSpinMax = 1u << 14;
+
+// Scalar loads of read-only descriptors behind the producer's stores (the compiler keeps loads that
+// follow a store in the kernel on the vector path, each one a dependent round trip): the constant
+// address space says the bytes are not written during the launch.
+#define RSK_CONST __attribute__((address_space(4)))
+template <typename T>
+__device__ __forceinline__ T ld_const(const T *p) {
+    return *(const RSK_CONST T *)p;
+}
+__device__ __forceinline__ uint32_t ld_const_u16(const uint16_t *p) {  // the dword holding it
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint32_t w = ld_const(reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3));
+    return (w >> (8u * (uint32_t)(a & 2u))) & 0xffffu;
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t la_rsrc(uint4 *heads, uint32_t t) {
+    return __builtin_amdgcn_make_buffer_rsrc(heads + 128ull * t, (short)0, 2048, 0x00020000);
+}
+
+// KV: the key schedule comes from a device copy, read by vector loads at an opaque (inline-asm) zero
+// offset, so its words live in VGPRs inside the producer / fallback only -- as kernel arguments they
+// are SGPRs for the whole kernel (106, which admits 6 blocks of 256 threads per CU instead of 8).
+__device__ __forceinline__ KeySched ks_vgpr(const KeySched *kd) {
+    uint32_t z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(kd) + z;
+    KeySched v;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        v.mid[q] = w[offsetof(KeySched, mid) / 4 + q];
+        v.pre[q] = w[offsetof(KeySched, pre) / 4 + q];
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        v.blk[q] = w[offsetof(KeySched, blk) / 4 + q];
+        v.pad[q] = w[offsetof(KeySched, pad) / 4 + q];
+    }
+    v.bword = kd->bword;  // uniform: scalar
+    v.bshift = kd->bshift;
+    v.two_blocks = kd->two_blocks;
+    v.tag_mode = kd->tag_mode;
+    v.tab = kd->tab;
+    return v;
+}
+
+__device__ __forceinline__ void la_produce(const EncArgs &a, const KeySched &ks, uint32_t t, uint4 *heads,
+                                           uint32_t *flags, uint32_t lane) {
+    const uint64_t i = 64ull * t + lane;
+    const Lane1 L = encode_phase1<true>(a, ks, i < a.n ? i : a.n);
+    if (L.st > 0) {  // 0 past n
+        const __amdgpu_buffer_rsrc_t r = la_rsrc(heads, t);
+        const u32x4 lo = {L.H[0], L.H[1], L.H[2], L.H[3]}, hi = {L.H[4], L.H[5], L.H[6], L.H[7]};
+        __builtin_amdgcn_raw_buffer_store_b128(lo, r, (int)(32u * lane), 0, 16);  // aux 16 = sc1
+        __builtin_amdgcn_raw_buffer_store_b128(hi, r, (int)(32u * lane + 16u), 0, 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0u) __hip_atomic_store(flags + t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// FF: the tile's flag is loaded once BEFORE the chunk loads (its round trip runs beside theirs; the spin,
+// if needed, after them).  FF = 2: timing probe, no flag at all (the record is read unchecked).
+template <int NT, uint32_t LA, int FF = 0, bool KV = false>
+__global__ __launch_bounds__(kBlock) void k_encode_la(EncArgs a, KeySched ks0, uint4 *heads, uint32_t *flags,
+                                                      const KeySched *kd) {
+    if constexpr (KV) {
+        if (kd->tag_mode == RSK_TAG_TABLE) {
+            s_tags[threadIdx.x] = kd->tab[threadIdx.x];
+            __syncthreads();
+        }
+    } else {
+        stage_tags(ks0);
+    }
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint32_t T = (uint32_t)(((uint64_t)a.n + 63ull) >> 6);
+    if ((blockIdx.x & 15u) == 0u && w == 0u) {
+        const KeySched ks = KV ? ks_vgpr(kd) : ks0;
+        const uint32_t t = blockIdx.x >> 4;
+        if (t < LA) la_produce(a, ks, t, heads, flags, lane);
+        if (t + LA < T) la_produce(a, ks, t + LA, heads, flags, lane);
+    }
+    const uint64_t i = (uint64_t)blockIdx.x * kWavesPerBlock + w;
+    if (i >= a.n) return;
+    const uint32_t P = ld_const_u16(a.pay_len + i);
+    const uint64_t po = ld_const(a.pay_off + i), fo = ld_const(a.frame_off + i);
+    if (P == 0u || P > (uint32_t)RSK_MAX_PAYLOAD) return;
+    const uint32_t fl = RSK_HEAD_SIZE + P;
+    const FrameGeo g = frame_geo(a.payload + po, a.frame + fo, fl, a.pad);
+    const uint32_t t = (uint32_t)(i >> 6);
+    uint32_t f0 = 0u;
+    if constexpr (FF == 1) f0 = __hip_atomic_load(flags + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint4 A[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        A[q] = make_uint4(0u, 0u, 0u, 0u);
+        if (q == 1 && g.nst < 64u) continue;  // uniform
+        const int32_t m = (int32_t)(lane + 64u * q) - 2;
+        if (m >= 0 && src_chunk_live(m, g.first_rel, g.last_rel)) A[q] = ld16<NT>(g.srcp + 16 * m);
+    }
+    uint32_t f = FF == 2 ? 1u : (uint32_t)__builtin_amdgcn_readfirstlane((int)f0);
+    for (uint32_t spins = 0; FF != 2 && f == 0u && spins < kLaSpinMax; ++spins) {
+        if (FF == 1 || spins > 0) __builtin_amdgcn_s_sleep(1);
+        f = (uint32_t)__builtin_amdgcn_readfirstlane(
+            (int)__hip_atomic_load(flags + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+    uint32_t Hj[8];
+    if (f != 0u) {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(la_rsrc(heads, t),
+                                                              (int)(32u * (uint32_t)(i & 63u) + 16u * (lane & 1u)), 0, 16);
+        Hj[0] = rdl(v.x, 0); Hj[1] = rdl(v.y, 0); Hj[2] = rdl(v.z, 0); Hj[3] = rdl(v.w, 0);
+        Hj[4] = rdl(v.x, 1); Hj[5] = rdl(v.y, 1); Hj[6] = rdl(v.z, 1); Hj[7] = rdl(v.w, 1);
+    } else {  // the producer has not published: frame the packet's header here
+        const KeySched ks = KV ? ks_vgpr(kd) : ks0;
+        const Lane1 L = encode_phase1<true>(a, ks, i);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) Hj[q] = (uint32_t)__builtin_amdgcn_readfirstlane((int)L.H[q]);
+    }
+    const uint32_t flen = fl + g.r, nst = g.nst;
+    uint4 B[2];
+    B[0] = make_uint4(wave_shl1(A[0].x), wave_shl1(A[0].y), wave_shl1(A[0].z), wave_shl1(A[0].w));
+    B[1] = make_uint4(0u, 0u, 0u, 0u);
+    if (nst >= 64u) {
+        const uint4 l0 = rdl4(A[1], 0);
+        if (lane == 63u) B[0] = l0;
+        if (nst > 64u) B[1] = make_uint4(wave_shl1(A[1].x), wave_shl1(A[1].y), wave_shl1(A[1].z), wave_shl1(A[1].w));
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const uint32_t k = lane + 64u * q;
+        if (q == 1 && nst <= 64u) continue;  // uniform
+        const uint4 V = rsk::funnel16(A[q], B[q], g.sh);
+        const uint4 vv = k < (g.r >= 2u ? 3u : 2u) ? head_chunk(Hj, k, g.r, V) : V;
+        if (k >= nst) continue;
+        store_piece<NT>(g.d0 + 16u * k, vv, k == 0u ? g.r : 0u, (int)flen - 16 * (int)k, a.pad != 0u);
+    }
+}
+
 // A/B build only (round 4): few packets per wave.  Wave w frames packets [PPW w, PPW w + PPW) (linear
 // mapping, short-lived waves: the access shape of k_probe_one) with the shipped long-frame copy
 // (copy_pkt_pipe, TAG form: payload[0] and one MD5 pass per batch of PU packets, header chunks in the
@@ -3237,12 +3383,18 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 // k_enc_copy1, normal / nontemporal stores); 77 / 78 / 79 / 80 / 81 = k_enc_few, 1 / 2 / 4 / 8 / 16 packets
 // per wave, 82 = 78 with nontemporal stores; 83 / 84 = k_encode_occ (0 forced to 8 / 6 waves per
 // SIMD); 85 / 86 / 88 = k_probe_persist (2048 blocks / 2048 pipelined / 4096 blocks), 87 / 89 =
-// k_probe_chunk<8 / 2> (plain-copy probes, wrong bytes) (round 4).  Rounds 1-2
+// k_probe_chunk<8 / 2> (plain-copy probes, wrong bytes); 90 / 91 = k_encode_la (look-ahead header
+// records, one wave per packet) with LA = 256 / 1024 tiles, 92 / 93 / 94 / 95 = LA 256 / 1024 / 64 / 4096
+// with nontemporal stores, 96 / 97 = 93 / 92 with the tile flag loaded before the chunk loads, 98 = 93
+// without the flag (timing probe: the record is read unchecked) (round 4).  Rounds 1-2
 // measured ~45 more variants (profiles/r01_ab_*, r02_ab_*); their code is in the git history.
-// v + 100 * cap (cap 1..4): the same kernel held to `cap` blocks per CU by unused LDS.
+// 99 = k_enc_copy1<2> alone on the records a previous 75 / 76 call left (timing probe), 100 = 76 with
+// the two kernels on two streams, concurrently (timing probe: the copy does not wait for the records);
+// 101 / 102 / 103 = 93 / 98 / 92 with the producer's key schedule in VGPRs (ks_vgpr).
+// v + 1000 * cap (cap 1..8): the same kernel held to `cap` blocks per CU by unused LDS.
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
-    const int k = v % 100;
-    if (!c || v < 0 || v / 100 > 4 || !(k == 0 || k == 12 || k == 13 || k == 37 || k == 47 || (k >= 50 && k <= 89)))
+    const int k = v % 1000;
+    if (!c || v < 0 || v / 1000 > 8 || !(k == 0 || k == 12 || k == 13 || k == 37 || k == 47 || (k >= 50 && k <= 103)))
         return RSK_EINVAL;
     c->enc_variant = v;
     return RSK_OK;
@@ -3399,9 +3551,10 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
 #ifdef RSK_AB
     // A/B build only (make -C rsock_amd ab -> librsk_ab.so, tools/): variant + 100 * cap limits
     // residency to `cap` blocks per CU through unused dynamic LDS
-    const int cap = c->enc_variant / 100;
-    const size_t lds = cap ? (size_t)(163840 / cap) - 16384 : 0;
-    switch (c->enc_variant % 100) {
+    const int cap = c->enc_variant / 1000;
+    // caps 5..8 (kernels with <= 2 KB of static LDS): just over 1 / (cap + 1) of the CU's LDS per block
+    const size_t lds = !cap ? 0 : cap <= 4 ? (size_t)(163840 / cap) - 16384 : (size_t)(163840 / (cap + 1)) + 64;
+    switch (c->enc_variant % 1000) {
         case 12: hipLaunchKernelGGL((k_copy_probe<12>), gd, bd, lds, st, a); break;
         case 13: hipLaunchKernelGGL((k_copy_probe<4>), gd, bd, lds, st, a); break;
         case 37: hipLaunchKernelGGL((k_encode_tiled<11, 4, 4, -1>), gd, bd, lds, st, a, c->ks); break;
@@ -3445,7 +3598,9 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         case 82: hipLaunchKernelGGL((k_enc_few<2, 2, 2>), dim3((unsigned)((n + 7ull) / 8ull)), bd, lds, st, a, c->ks); break;
         case 74: hipLaunchKernelGGL(k_probe_one, dim3((unsigned)((n + 3ull) / 4ull)), bd, lds, st, a); break;
         case 75:
-        case 76: {
+        case 76:
+        case 99:
+        case 100: {
             static uint4 *heads = nullptr;  // A/B only: the two-pass form's header workspace, never freed
             static uint64_t heads_n = 0;
             if (heads_n < n) {
@@ -3454,13 +3609,66 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
                 if (hipMalloc(&heads, 32ull * n) != hipSuccess) return RSK_ENOMEM;
                 heads_n = n;
             }
-            hipLaunchKernelGGL(k_enc_heads, dim3(grid_for(n)), bd, 0, st, a, c->ks, heads);
-            if (c->enc_variant % 100 == 75)
+            const int k = c->enc_variant % 1000;
+            if (k == 100) {  // fork: the header pass on a second stream beside the copy
+                static hipStream_t s2 = nullptr;
+                static hipEvent_t e0 = nullptr, e1 = nullptr;
+                if (!s2 && (hipStreamCreateWithFlags(&s2, hipStreamNonBlocking) != hipSuccess ||
+                            hipEventCreateWithFlags(&e0, hipEventDisableTiming) != hipSuccess ||
+                            hipEventCreateWithFlags(&e1, hipEventDisableTiming) != hipSuccess))
+                    return launch_check("A/B fork stream");
+                (void)hipEventRecord(e0, st);
+                (void)hipStreamWaitEvent(s2, e0, 0);
+                hipLaunchKernelGGL(k_enc_heads, dim3(grid_for(n)), bd, 0, s2, a, c->ks, heads);
+                hipLaunchKernelGGL(k_enc_copy1<2>, dim3((unsigned)((n + 3ull) / 4ull)), bd, lds, st, a,
+                                   reinterpret_cast<const uint32_t *>(heads));
+                (void)hipEventRecord(e1, s2);
+                (void)hipStreamWaitEvent(st, e1, 0);
+                break;
+            }
+            if (k != 99) hipLaunchKernelGGL(k_enc_heads, dim3(grid_for(n)), bd, 0, st, a, c->ks, heads);
+            if (k == 75)
                 hipLaunchKernelGGL(k_enc_copy1<0>, dim3((unsigned)((n + 3ull) / 4ull)), bd, lds, st, a,
                                    reinterpret_cast<const uint32_t *>(heads));
             else
                 hipLaunchKernelGGL(k_enc_copy1<2>, dim3((unsigned)((n + 3ull) / 4ull)), bd, lds, st, a,
                                    reinterpret_cast<const uint32_t *>(heads));
+            break;
+        }
+        case 90: case 91: case 92: case 93: case 94: case 95: case 96: case 97: case 98: case 101: case 102:
+        case 103: {
+            // A/B only: the look-ahead form's flags (zeroed per call) and header records, never freed
+            static uint8_t *la_ws = nullptr;
+            static uint64_t la_n = 0;
+            const uint64_t tiles = (n + 63ull) / 64ull, fbytes = (4ull * tiles + 255ull) & ~255ull;
+            if (la_n < n) {
+                if (la_ws) (void)hipFree(la_ws);
+                la_ws = nullptr;
+                if (hipMalloc(&la_ws, fbytes + 2048ull * tiles) != hipSuccess) return RSK_ENOMEM;
+                la_n = n;
+            }
+            static KeySched *kd = nullptr;  // the key schedule in device memory (KV variants)
+            if (!kd && hipMalloc(&kd, sizeof(KeySched)) != hipSuccess) return RSK_ENOMEM;
+            if (hipMemcpyAsync(kd, &c->ks, sizeof(KeySched), hipMemcpyHostToDevice, st) != hipSuccess)
+                return launch_check("hipMemcpyAsync(la key schedule)");
+            uint32_t *fl = reinterpret_cast<uint32_t *>(la_ws);
+            uint4 *hd = reinterpret_cast<uint4 *>(la_ws + ((4ull * ((la_n + 63ull) / 64ull) + 255ull) & ~255ull));
+            if (hipMemsetAsync(fl, 0, fbytes, st) != hipSuccess) return launch_check("hipMemsetAsync(la flags)");
+            const dim3 g1((unsigned)((n + 3ull) / 4ull));
+            switch (c->enc_variant % 1000) {
+                case 90: hipLaunchKernelGGL((k_encode_la<0, 256>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
+                case 91: hipLaunchKernelGGL((k_encode_la<0, 1024>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
+                case 92: hipLaunchKernelGGL((k_encode_la<2, 256>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
+                case 93: hipLaunchKernelGGL((k_encode_la<2, 1024>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
+                case 94: hipLaunchKernelGGL((k_encode_la<2, 64>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
+                case 95: hipLaunchKernelGGL((k_encode_la<2, 4096>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
+                case 96: hipLaunchKernelGGL((k_encode_la<2, 1024, 1>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
+                case 97: hipLaunchKernelGGL((k_encode_la<2, 256, 1>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
+                case 98: hipLaunchKernelGGL((k_encode_la<2, 1024, 2>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
+                case 101: hipLaunchKernelGGL((k_encode_la<2, 1024, 0, true>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
+                case 102: hipLaunchKernelGGL((k_encode_la<2, 1024, 2, true>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
+                default: hipLaunchKernelGGL((k_encode_la<2, 256, 0, true>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
+            }
             break;
         }
         default: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;

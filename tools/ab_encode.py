@@ -51,15 +51,16 @@ def main():
         cx.set_encode_variant(v[0])
         cur["pad"] = v[1]
         w.frame.zero_()
+        w.status.fill_(-7)
         enc()
         torch.cuda.synchronize()
-        h = w.frame.clone()
+        h = (w.frame.clone(), w.status.clone())
         if ref is None:
             ref = h
-        elif v[0] in (12, 13, 73, 74, 85, 86, 87, 88, 89):
+        elif v[0] % 1000 in (12, 13, 73, 74, 85, 86, 87, 88, 89, 98, 99, 100):
             pass  # k_copy_probe: the memory-side ceiling probe writes the traffic, not the encoding
-        elif not torch.equal(ref, h):
-            raise SystemExit(f"variant {v} frame arena differs from variant {variants[0]}")
+        elif not (torch.equal(ref[0], h[0]) and torch.equal(ref[1], h[1])):
+            raise SystemExit(f"variant {v} frame arena or status differs from variant {variants[0]}")
     del ref
     for _ in range(args.rounds):
         for v in variants:
