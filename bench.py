@@ -41,6 +41,8 @@ METRIC = "Mpkt/s + GiB/s device-resident EncHead+MD5 encode/decode at 1/2/4/8 GP
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # tag modes (rsk_set_tag_mode): the headline computes MD5 per lane, as the reference does per packet
 TAG_LABEL = {"md5": "md5_per_lane", "table": "tag_table_lut"}
+# rsk__last_encode_path: the library picks the encode path per call (rsk_encode_batch, enc_path)
+ENC_PATH_TEXT = {1: "k_encode", 2: "k_encode_heads + k_encode_copy (two-pass, one wave per packet)"}
 TAG_TEXT = {"md5": "one MD5 compression per packet and lane",
             "table": "lookup in the key's 256-entry tag table staged in LDS (MD5 run once per key, 256 tags)"}
 
@@ -358,6 +360,7 @@ def main() -> None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed_max = float(t.item())
 
+    enc_path = ENC_PATH_TEXT.get(cx.last_encode_path, "?")
     enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
     total_pkts = (n_total if strong else world * d.n) * args.steps
@@ -406,12 +409,13 @@ def main() -> None:
                 "parallelism": f"shard{world} (no collective)",
             },
             "gib_per_s": round(world * bytes_step * args.steps / elapsed_max / 2**30, 2),
-            "kernels_ms": {"k_encode": round(enc_ms, 4), "decode+compact": round(dec_ms, 4)},
-            "launch": ("hipGraph replay of the step (k_encode, k_decode, k_compact); kernel times: HIP events "
+            "kernels_ms": {"encode": round(enc_ms, 4), "decode+compact": round(dec_ms, 4)},
+            "encode_path": enc_path,
+            "launch": ("hipGraph replay of the step (encode, k_decode, k_compact); kernel times: HIP events "
                        "around the same launches issued one by one after the timed region") if graph_mode else
                       "eager launches; kernel times: HIP events in the timed region",
             "roofline": {
-                "kernel": "k_encode",
+                "kernel": enc_path,
                 "bound": "hbm",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
@@ -430,7 +434,7 @@ def main() -> None:
                 "value": round(d.n * args.steps / el_o / 1e6, 2),
                 "unit": "Mpkt/s",
                 "ms_per_step": round(el_o / args.steps * 1e3, 4),
-                "kernels_ms": {"k_encode": round(enc_o, 4), "decode+compact": round(dec_o, 4)},
+                "kernels_ms": {"encode": round(enc_o, 4), "decode+compact": round(dec_o, 4)},
                 "roofline_frac": round(enc_bytes / (enc_o * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             }
         if world == 1 and not args.no_cpu_baseline:

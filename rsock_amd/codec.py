@@ -270,10 +270,25 @@ class Codec:
         except Exception:
             pass
 
+    def set_encode_path(self, path: int) -> None:
+        """Internal knob (tests, tools) for output_batch: 0 = chosen per call from the previous batch's
+        sampled mean payload (default), 1 = the per-set kernel k_encode, 2 = the two-pass form for long
+        frames (k_encode_heads + one wave per packet, k_encode_copy).  Both give identical bytes."""
+        fn = lib().rsk__set_encode_path
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        _check(fn(self._ctx, path), "rsk__set_encode_path")
+
+    @property
+    def last_encode_path(self) -> int:
+        """The path the last output_batch took: 1 = k_encode, 2 = the two-pass form (0 before any)."""
+        fn = lib().rsk__last_encode_path
+        fn.argtypes = [ctypes.c_void_p]
+        return int(fn(self._ctx))
+
     def set_encode_variant(self, v: int) -> None:
         """A/B build only (RSK_LIB=librsk_ab.so, `make -C rsock_amd ab`): selects a k_encode variant
         for in-process A/B runs (tools/ab_encode.py; the list is in rsk_kernels.hip).  The shipped
-        librsk.so has exactly one encode kernel and no such knob."""
+        librsk.so has two encode paths (set_encode_path) and no such knob."""
         fn = _ab_fn("rsk__set_encode_variant")
         _check(fn(self._ctx, v), "rsk__set_encode_variant")
 

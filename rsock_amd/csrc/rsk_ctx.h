@@ -19,7 +19,7 @@ struct ShimIO;  // rsk_kernels.hip
 
 namespace rsk {
 // Device scratch of one kind for the calls ordered on one stream.
-enum WsKind { WS_COMPACT = 0, WS_SEQ = 1, WS_DEMUX = 2, WS_KINDS = 3 };
+enum WsKind { WS_COMPACT = 0, WS_SEQ = 1, WS_DEMUX = 2, WS_ENC = 3, WS_KINDS = 4 };
 struct WsBuf {
     void *p = nullptr;
     size_t bytes = 0;
@@ -31,6 +31,16 @@ struct rsk_ctx {
     int device = 0;
     int enc_variant = 0;   // see rsk__set_encode_variant (A/B build)
     int wire_variant = 0;  // see rsk__set_wire_variant (A/B build)
+    // encode path (rsk_encode_batch): 0 = chosen per call from the previous batch's statistic, 1 = the
+    // per-set kernel, 2 = the two-pass form (rsk__set_encode_path, tests and tools)
+    int enc_path = 0;
+    std::atomic<int> enc_last_path{0};  // the path the last rsk_encode_batch took (rsk__last_encode_path)
+    std::atomic<uint32_t> enc_calls{0};  // per-set encode calls (k_enc_sample cadence)
+    // host-mapped word the batch statistic is stored to (enc_sample: k_encode_heads, k_enc_sample) and
+    // its device address; read without synchronisation by later calls (a stale value only picks the
+    // slower path, never different bytes)
+    uint32_t *enc_stat_host = nullptr;
+    uint32_t *enc_stat_dev = nullptr;
     std::vector<uint8_t> key;
     rsk::KeySched ks;
     // Scratch per stream (compaction look-back state, send-seq tables, demux tables): calls on
@@ -119,6 +129,19 @@ inline int stream_ws(rsk_ctx *c, hipStream_t s, int kind, size_t need, void **ou
     }
     *out = b.p;
     return RSK_OK;
+}
+
+// As stream_ws, but a buffer that would have to grow while s is being captured is refused quietly
+// (RSK_EINVAL, no error text): for scratch whose caller has a path that needs none.
+inline int stream_ws_if(rsk_ctx *c, hipStream_t s, int kind, size_t need, void **out) {
+    if (capturing(s)) {
+        std::lock_guard<std::mutex> lk(c->ws_mu);
+        auto it = c->ws.find(s);
+        if (it == c->ws.end() || !it->second[kind].p || it->second[kind].bytes < need) return RSK_EINVAL;
+        *out = it->second[kind].p;
+        return RSK_OK;
+    }
+    return stream_ws(c, s, kind, need, out);
 }
 
 // Workspace of the compaction for stream s: `words` 64-bit words, zeroed when (re)allocated.  Its

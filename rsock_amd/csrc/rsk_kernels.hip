@@ -204,6 +204,29 @@ __device__ __forceinline__ void encode_tag(const EncArgs &a, const KeySched &ks,
     }
 }
 
+// The batch statistic behind the next calls' choice of encode path (rsk_encode_batch, enc_path): one
+// wave reads pay_len at 64 evenly spaced packets and stores their mean payload length (bit 31 set:
+// valid) to a host-mapped word of the context.  k_encode_heads does it in its block 0; calls that take
+// the per-set kernel launch k_enc_sample now and then (the per-set kernel itself carries no extra
+// argument: one more pointer in its arguments cost C4 12 % through SGPR spills, gpurun_out/r04o).
+constexpr uint32_t kStatValid = 0x80000000u;
+// the two-pass form's batches (enc_path): at least this many packets whose previous batch's sampled
+// mean payload was at least this long (C3's 1400 B take it; C4's mixed lengths, mean ~700 B, and
+// C2's 64 B keep the per-set kernel: one packet per wave idles their lanes, profiles/r04_c3_ceiling.json)
+constexpr uint32_t kTwoPassMinPackets = 16384;
+constexpr uint32_t kTwoPassMinPayload = 1024;
+constexpr uint32_t kSampleEvery = 256;  // per-set calls between two samples (k_enc_sample)
+__device__ __forceinline__ void enc_sample(const uint16_t *pay_len, uint32_t n, uint32_t *stat) {
+    if (blockIdx.x != 0u || threadIdx.x >= 64u) return;
+    uint32_t v = pay_len[((uint64_t)threadIdx.x * n) >> 6];
+#pragma unroll
+    for (int off = 32; off; off >>= 1) v += (uint32_t)__shfl_xor((int)v, off);
+    if (threadIdx.x == 0u) __hip_atomic_store(stat, kStatValid | (v >> 6), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__global__ __launch_bounds__(64) void k_enc_sample(const uint16_t *pay_len, uint32_t n, uint32_t *stat) {
+    enc_sample(pay_len, n, stat);
+}
+
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 template <int NT>
 __device__ __forceinline__ uint4 ld16(const uint8_t *p) {
@@ -714,7 +737,7 @@ __device__ __forceinline__ void copy_pkt_pipe(const EncArgs &a, const KeySched &
 // TAGQ: phase 1 left the tag; `payload[0]` is loaded right after the first iteration's chunk loads
 // (both depend only on the descriptors) and the packet's lane then stores its header chunks, so
 // the set pays one dependent global round trip less than with the tag before the copy.
-template <int U, bool TAGQ = false>
+template <int U, bool TAGQ = false, bool LANE = false>
 __device__ __forceinline__ void flat_head(const EncArgs &a, const KeySched &ks, const Lane1 &L, bool mine) {
     if constexpr (TAGQ) {
         if (mine) {
@@ -722,14 +745,14 @@ __device__ __forceinline__ void flat_head(const EncArgs &a, const KeySched &ks, 
             uint32_t H[8];
 #pragma unroll
             for (int q = 0; q < 8; ++q) H[q] = L.H[q];
-            tag_of(ks, b0, H[0], H[1]);
+            tag_of<LANE>(ks, b0, H[0], H[1]);
             H[7] |= b0 << 24;
             store_head(H, a.frame + L.fo);
         }
     }
 }
 
-template <int U, bool TAGQ = false>
+template <int U, bool TAGQ = false, bool LANE = false>
 __device__ __forceinline__ void copy_flat(const EncArgs &a, const KeySched &ks, const Lane1 &L, uint32_t lane,
                                           bool mine, CopyRec *recs, uint32_t *cend) {
     uint32_t cc = 0;
@@ -789,12 +812,12 @@ __device__ __forceinline__ void copy_flat(const EncArgs &a, const KeySched &ks, 
                 lims[u] = (int32_t)rr.flen - 32 - 16 * m;
             }
         }
-        if (TAGQ && g0 == 0u) flat_head<U, TAGQ>(a, ks, L, mine);
+        if (TAGQ && g0 == 0u) flat_head<U, TAGQ, LANE>(a, ks, L, mine);
 #pragma unroll
         for (int u = 0; u < U; ++u)
             if (act[u]) store_piece<0>(dsts[u], funnel16_lane(A[u], B[u], shs[u]), los[u], lims[u], a.pad != 0u);
     }
-    if (TAGQ && C == 0u) flat_head<U, TAGQ>(a, ks, L, mine);
+    if (TAGQ && C == 0u) flat_head<U, TAGQ, LANE>(a, ks, L, mine);
     wave_lds_sync();  // LDS slice reusable by the caller afterwards
 }
 
@@ -826,14 +849,15 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
     const bool flat = MODE == 7 ? true : MODE == 8 ? false : fl < kFlatBelowMeanBytes * cnt;
     // MODE 10 (A/B): as 9 with the tag in the copy loop for every per-packet set
     const bool defer = MODE != 3 && MODE != 7 && !flat && (MODE == 10 || fl >= kDeferTagMeanBytes * cnt);
-    // MODE 11 (A/B): as 9 with the flat sets' tag and header stores behind the first chunk loads
-    constexpr bool kFlatTagQ = MODE == 11;
+    // MODE 11 (shipped): as 9 with the flat sets' tag and header stores behind the first chunk loads;
+    // MODE 12 (A/B): 11 with the flat sets' MD5 on the payload-word-specialised schedule (md5_tag_lane)
+    constexpr bool kFlatTagQ = MODE == 11 || MODE == 12;
     if constexpr (MODE != 3 && MODE != 7) {  // the tag now, except for the sets whose copy loop takes it
         if (!defer && !(kFlatTagQ && flat)) encode_tag(a, ks, L);
     }
     if (flat) {
         if (!kFlatTagQ && vec) store_head(L.H, a.frame + L.fo);
-        copy_flat<U, kFlatTagQ>(a, ks, L, lane, vec, recs, cend);
+        copy_flat<U, kFlatTagQ, MODE == 12>(a, ks, L, lane, vec, recs, cend);
         return;
     }
     bool nt = NT == 2;
@@ -854,7 +878,7 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
     // first slot store (lanes 0..2, words by readlane); the others by the slot lane (store_head).
     // Measured (A/B, profiles/r02_ab_head.json): C3 2.34 vs 2.55 ms with the first; C4 0.389 vs
     // 0.420 ms with the second.
-    if constexpr (MODE == 9 || MODE == 10 || MODE == 11) {  // software-pipelined per-packet copy (shipped: 9)
+    if constexpr (MODE == 9 || MODE == 10 || MODE == 11 || MODE == 12) {  // software-pipelined per-packet copy
         // Byte-packed long frames (no pad; a frame ends mid-chunk and the next packet's frame
         // starts there): the TAG-form copy with the boundary-chunk merge (TailCarry), which writes
         // each shared chunk as one 16-B store.  Only sets that really have such a pair take it: the
@@ -1052,13 +1076,20 @@ __global__ __launch_bounds__(1024) void k_encode_bc(EncArgs a, KeySched ks) {
 }
 #endif  // RSK_AB
 
-#ifdef RSK_AB
-// A/B build only (round 4): the two-pass form.  Pass A (k_enc_heads): phase 1 one lane per packet,
-// the 8 header words into a 32-B-per-packet workspace (+ status).  Pass B (k_enc_copy1): one wave per
-// packet and nothing else -- descriptors and header words by scalar loads, the packet's chunk loads,
-// funnel and stores -- so waves are short-lived and independent (no barrier, no MD5 in the copy).
-__global__ __launch_bounds__(kBlock) void k_enc_heads(EncArgs a, KeySched ks, uint4 *heads) {
+// ---- the two-pass form for batches of long frames (round 4) ---------------------------------------
+// Pass 1, k_encode_heads: phase 1 one lane per packet (status, the MD5 tag, EncHead, payload[0]; the
+// same code as k_encode's phase 1) into a 32-B record per packet in the stream's workspace.  Pass 2,
+// k_encode_copy: ONE WAVE PER PACKET -- descriptors and the record by scalar loads, the packet's chunk
+// loads, the DPP funnel, the header chunks from the record, nontemporal stores -- so waves are short-lived
+// and independent.  That is the access shape of the fastest plain copy measured on this chip for C3's
+// arenas (one wave per packet: 6.0 TB/s, against 5.2 TB/s for k_encode's 64-packet sets; DESIGN.md §4.1,
+// profiles/r04_c3_ceiling.json), which k_encode cannot take: a one-packet wave would run a whole MD5
+// compression for one packet (~300 VALU whatever its active lanes; 4.5 ms for C3).  Pass 1 runs the
+// compressions 64 to a wave instead.  rsk_encode_batch takes this form for batches of long frames
+// (enc_path); for short frames one packet per wave idles most lanes and the per-set kernel stays.
+__global__ __launch_bounds__(kBlock) void k_encode_heads(EncArgs a, KeySched ks, uint4 *heads, uint32_t *stat) {
     stage_tags(ks);
+    enc_sample(a.pay_len, a.n, stat);
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     const Lane1 L = encode_phase1<true>(a, ks, i < a.n ? i : a.n);
     if (i < a.n && L.st > 0) {
@@ -1067,16 +1098,19 @@ __global__ __launch_bounds__(kBlock) void k_enc_heads(EncArgs a, KeySched ks, ui
     }
 }
 
+// NT: bit 0 nontemporal loads, bit 1 nontemporal stores (shipped: 2)
 template <int NT>
-__global__ __launch_bounds__(kBlock) void k_enc_copy1(EncArgs a, const uint32_t *heads) {
+__global__ __launch_bounds__(kBlock) void k_encode_copy(EncArgs a, const uint32_t *heads) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const uint64_t i = (uint64_t)blockIdx.x * kWavesPerBlock + w;
     if (i >= a.n) return;
-    const uint32_t P = a.pay_len[i];
-    if (P == 0u || P > (uint32_t)RSK_MAX_PAYLOAD) return;
+    const uint32_t P = a.pay_len[i];  // uniform address, read-only in this launch: scalar loads
+    if (P == 0u || P > (uint32_t)RSK_MAX_PAYLOAD) return;  // status written by pass 1
     const uint32_t fl = RSK_HEAD_SIZE + P;
     const FrameGeo g = frame_geo(a.payload + a.pay_off[i], a.frame + a.frame_off[i], fl, a.pad);
+    // lane k loads aligned source chunk k - 2 of slot q (destination chunk k + 64 q); the funnel partner
+    // (chunk k - 1) comes from lane k + 1 by a DPP shift, lane 63 of slot 0 from lane 0 of slot 1
     uint4 A[2];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -1108,7 +1142,8 @@ __global__ __launch_bounds__(kBlock) void k_enc_copy1(EncArgs a, const uint32_t 
     }
 }
 
-// A/B build only (round 4): look-ahead headers -- the one-wave-per-packet copy of k_enc_copy1 in ONE
+#ifdef RSK_AB
+// A/B build only (round 4): look-ahead headers -- the one-wave-per-packet copy of k_encode_copy in ONE
 // launch.  Tile t = 64 consecutive packets = 16 blocks.  Wave 0 of tile t's first
 // block runs phase 1 + MD5 lane-per-packet for tile t + LA (for t < LA first for tile t itself) and
 // publishes the 32-B header records write-through (sc1 buffer stores, drained by s_waitcnt vmcnt(0))
@@ -1178,9 +1213,9 @@ __device__ __forceinline__ void la_produce(const EncArgs &a, const KeySched &ks,
 
 // FF: the tile's flag is loaded once BEFORE the chunk loads (its round trip runs beside theirs; the spin,
 // if needed, after them).  FF = 2: timing probe, no flag at all (the record is read unchecked).
-template <int NT, uint32_t LA, int FF = 0, bool KV = false>
-__global__ __launch_bounds__(kBlock) void k_encode_la(EncArgs a, KeySched ks0, uint4 *heads, uint32_t *flags,
-                                                      const KeySched *kd) {
+template <int NT, uint32_t LA, int FF, bool KV>
+__device__ __forceinline__ void encode_la(const EncArgs &a, const KeySched &ks0, uint4 *heads, uint32_t *flags,
+                                          const KeySched *kd) {
     if constexpr (KV) {
         if (kd->tag_mode == RSK_TAG_TABLE) {
             s_tags[threadIdx.x] = kd->tab[threadIdx.x];
@@ -1252,6 +1287,19 @@ __global__ __launch_bounds__(kBlock) void k_encode_la(EncArgs a, KeySched ks0, u
         if (k >= nst) continue;
         store_piece<NT>(g.d0 + 16u * k, vv, k == 0u ? g.r : 0u, (int)flen - 16 * (int)k, a.pad != 0u);
     }
+}
+
+template <int NT, uint32_t LA, int FF = 0, bool KV = false>
+__global__ __launch_bounds__(kBlock) void k_encode_la(EncArgs a, KeySched ks0, uint4 *heads, uint32_t *flags,
+                                                      const KeySched *kd) {
+    encode_la<NT, LA, FF, KV>(a, ks0, heads, flags, kd);
+}
+// the same held to 80 SGPRs: 8 blocks of 256 threads per CU (MI355X_MICROARCH.md, residency: 82-96
+// SGPRs admit 7, 98+ 6; the compiler takes 106 when nothing bounds it)
+template <int NT, uint32_t LA, int FF = 0, bool KV = false>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(80))) void k_encode_la80(
+    EncArgs a, KeySched ks0, uint4 *heads, uint32_t *flags, const KeySched *kd) {
+    encode_la<NT, LA, FF, KV>(a, ks0, heads, flags, kd);
 }
 
 // A/B build only (round 4): few packets per wave.  Wave w frames packets [PPW w, PPW w + PPW) (linear
@@ -3379,8 +3427,8 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 // for the last packets, round 3) in the git history (profiles/r03_ab_encode_tail.json); 69 / 70 / 71 =
 // the block-cooperative copy k_encode_bc (16 waves per block, 1 / 2 / 4 packets per wave), 72 = 69 with
 // nontemporal stores; 73 / 74 = memory-pattern probes (wrong bytes: k_probe_gi, the shipped mapping and
-// batches; k_probe_one, one wave per packet); 75 / 76 = the two-pass form (k_enc_heads then
-// k_enc_copy1, normal / nontemporal stores); 77 / 78 / 79 / 80 / 81 = k_enc_few, 1 / 2 / 4 / 8 / 16 packets
+// batches; k_probe_one, one wave per packet); 75 / 76 = the two-pass form (k_encode_heads then
+// k_encode_copy, normal / nontemporal stores; 76 = the shipped two-pass path); 77 / 78 / 79 / 80 / 81 = k_enc_few, 1 / 2 / 4 / 8 / 16 packets
 // per wave, 82 = 78 with nontemporal stores; 83 / 84 = k_encode_occ (0 forced to 8 / 6 waves per
 // SIMD); 85 / 86 / 88 = k_probe_persist (2048 blocks / 2048 pipelined / 4096 blocks), 87 / 89 =
 // k_probe_chunk<8 / 2> (plain-copy probes, wrong bytes); 90 / 91 = k_encode_la (look-ahead header
@@ -3388,13 +3436,15 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 // with nontemporal stores, 96 / 97 = 93 / 92 with the tile flag loaded before the chunk loads, 98 = 93
 // without the flag (timing probe: the record is read unchecked) (round 4).  Rounds 1-2
 // measured ~45 more variants (profiles/r01_ab_*, r02_ab_*); their code is in the git history.
-// 99 = k_enc_copy1<2> alone on the records a previous 75 / 76 call left (timing probe), 100 = 76 with
+// 99 = k_encode_copy<2> alone on the records a previous 75 / 76 call left (timing probe), 100 = 76 with
 // the two kernels on two streams, concurrently (timing probe: the copy does not wait for the records);
-// 101 / 102 / 103 = 93 / 98 / 92 with the producer's key schedule in VGPRs (ks_vgpr).
+// 101 / 102 / 103 = 93 / 98 / 92 with the producer's key schedule in VGPRs (ks_vgpr); 104 = 93, 105 / 106 /
+// 107 = 101 / 102 / 103 held to 80 SGPRs (k_encode_la80); 108 = 0 with the flat sets' MD5 on the
+// payload-word-specialised schedule (MODE 12).
 // v + 1000 * cap (cap 1..8): the same kernel held to `cap` blocks per CU by unused LDS.
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
     const int k = v % 1000;
-    if (!c || v < 0 || v / 1000 > 8 || !(k == 0 || k == 12 || k == 13 || k == 37 || k == 47 || (k >= 50 && k <= 103)))
+    if (!c || v < 0 || v / 1000 > 8 || !(k == 0 || k == 12 || k == 13 || k == 37 || k == 47 || (k >= 50 && k <= 108)))
         return RSK_EINVAL;
     c->enc_variant = v;
     return RSK_OK;
@@ -3433,6 +3483,12 @@ rsk_ctx *rsk_create(const uint8_t *key, uint32_t key_len, int device) {
     e = g.ok ? hipMalloc(&c->tag_dev, 256 * sizeof(uint2)) : hipErrorInvalidDevice;
     if (e == hipSuccess) e = hipMalloc(&c->err_dev, sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemset(c->err_dev, 0, sizeof(uint32_t));
+    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&c->enc_stat_host), sizeof(uint32_t),
+                                           hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess) {
+        *c->enc_stat_host = 0u;
+        e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->enc_stat_dev), c->enc_stat_host, 0);
+    }
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
     if (e == hipSuccess) {
         hipLaunchKernelGGL(k_tag_table, dim3(1), dim3(256), 0, s, c->ks, c->tag_dev);
@@ -3444,6 +3500,7 @@ rsk_ctx *rsk_create(const uint8_t *key, uint32_t key_len, int device) {
         set_error("rsk_create: tag table", e);
         if (c->tag_dev) (void)hipFree(c->tag_dev);
         if (c->err_dev) (void)hipFree(c->err_dev);
+        if (c->enc_stat_host) (void)hipHostFree(c->enc_stat_host);
         delete c;
         return nullptr;
     }
@@ -3467,6 +3524,7 @@ void rsk_destroy(rsk_ctx *c) {
     if (c->shim_dev) (void)hipFree(c->shim_dev);
     if (c->tag_dev) (void)hipFree(c->tag_dev);
     if (c->err_dev) (void)hipFree(c->err_dev);
+    if (c->enc_stat_host) (void)hipHostFree(c->enc_stat_host);
     if (c->shim_host) (void)hipHostFree(c->shim_host);
     if (c->shim_stream) (void)hipStreamDestroy(c->shim_stream);
     delete c;
@@ -3480,6 +3538,17 @@ int rsk_release_stream(rsk_ctx *c, void *stream) {
     if (!g.ok) return RSK_EDEVICE;
     return rsk::release_ws(c, (hipStream_t)stream);
 }
+
+// Internal (tests, tools): encode path of this context's calls: 0 = chosen per call (enc_path), 1 = the
+// per-set kernel k_encode, 2 = the two-pass form (k_encode_heads + k_encode_copy).
+int rsk__set_encode_path(rsk_ctx *c, int path) {
+    if (!c || path < 0 || path > 2) return RSK_EINVAL;
+    c->enc_path = path;
+    return RSK_OK;
+}
+
+// Internal (tests, bench): the path the context's last rsk_encode_batch took (1 or 2; 0 before any).
+int rsk__last_encode_path(const rsk_ctx *c) { return c ? c->enc_last_path.load(std::memory_order_relaxed) : RSK_EINVAL; }
 
 // Internal (tests): the next compaction launch of this context runs with tile `tile` publishing
 // nothing (a stalled tile), to exercise the look-back timeout, the sticky flag and the recovery.
@@ -3523,7 +3592,21 @@ int rsk_reserve_stream(rsk_ctx *c, uint32_t n_max, void *stream) {
     DeviceGuard g(c->device);
     if (!g.ok) return RSK_EDEVICE;
     Compact ck;
-    return ensure_compact(c, n_max, (hipStream_t)stream, ck);
+    const int r = ensure_compact(c, n_max, (hipStream_t)stream, ck);
+    if (r || n_max < kTwoPassMinPackets) return r;
+    void *p = nullptr;  // the two-pass encode's header records (32 B per packet)
+    return rsk::stream_ws(c, (hipStream_t)stream, rsk::WS_ENC, 32ull * n_max, &p);
+}
+
+// Encode path per call: the context's forced path (rsk__set_encode_path), else the two-pass form for
+// batches of at least kTwoPassMinPackets when the context's last sampled batch (enc_sample: every
+// two-pass call, and k_enc_sample behind the first and every kSampleEvery-th per-set call) had a mean
+// payload of at least kTwoPassMinPayload bytes, else the per-set kernel.  The first call on a context
+// has no statistic yet and takes the per-set kernel; either path gives identical bytes.
+static int enc_path(rsk_ctx *c, uint32_t n) {
+    if (c->enc_path) return c->enc_path;
+    const uint32_t s = c->enc_stat_host ? __atomic_load_n(c->enc_stat_host, __ATOMIC_RELAXED) : 0u;
+    return n >= kTwoPassMinPackets && (s & kStatValid) && (s & ~kStatValid) >= kTwoPassMinPayload ? 2 : 1;
 }
 
 int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_encode_out *out,
@@ -3619,24 +3702,24 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
                     return launch_check("A/B fork stream");
                 (void)hipEventRecord(e0, st);
                 (void)hipStreamWaitEvent(s2, e0, 0);
-                hipLaunchKernelGGL(k_enc_heads, dim3(grid_for(n)), bd, 0, s2, a, c->ks, heads);
-                hipLaunchKernelGGL(k_enc_copy1<2>, dim3((unsigned)((n + 3ull) / 4ull)), bd, lds, st, a,
+                hipLaunchKernelGGL(k_encode_heads, dim3(grid_for(n)), bd, 0, s2, a, c->ks, heads, c->enc_stat_dev);
+                hipLaunchKernelGGL(k_encode_copy<2>, dim3((unsigned)((n + 3ull) / 4ull)), bd, lds, st, a,
                                    reinterpret_cast<const uint32_t *>(heads));
                 (void)hipEventRecord(e1, s2);
                 (void)hipStreamWaitEvent(st, e1, 0);
                 break;
             }
-            if (k != 99) hipLaunchKernelGGL(k_enc_heads, dim3(grid_for(n)), bd, 0, st, a, c->ks, heads);
+            if (k != 99) hipLaunchKernelGGL(k_encode_heads, dim3(grid_for(n)), bd, 0, st, a, c->ks, heads, c->enc_stat_dev);
             if (k == 75)
-                hipLaunchKernelGGL(k_enc_copy1<0>, dim3((unsigned)((n + 3ull) / 4ull)), bd, lds, st, a,
+                hipLaunchKernelGGL(k_encode_copy<0>, dim3((unsigned)((n + 3ull) / 4ull)), bd, lds, st, a,
                                    reinterpret_cast<const uint32_t *>(heads));
             else
-                hipLaunchKernelGGL(k_enc_copy1<2>, dim3((unsigned)((n + 3ull) / 4ull)), bd, lds, st, a,
+                hipLaunchKernelGGL(k_encode_copy<2>, dim3((unsigned)((n + 3ull) / 4ull)), bd, lds, st, a,
                                    reinterpret_cast<const uint32_t *>(heads));
             break;
         }
         case 90: case 91: case 92: case 93: case 94: case 95: case 96: case 97: case 98: case 101: case 102:
-        case 103: {
+        case 103: case 104: case 105: case 106: case 107: {
             // A/B only: the look-ahead form's flags (zeroed per call) and header records, never freed
             static uint8_t *la_ws = nullptr;
             static uint64_t la_n = 0;
@@ -3667,18 +3750,44 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
                 case 98: hipLaunchKernelGGL((k_encode_la<2, 1024, 2>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
                 case 101: hipLaunchKernelGGL((k_encode_la<2, 1024, 0, true>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
                 case 102: hipLaunchKernelGGL((k_encode_la<2, 1024, 2, true>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
-                default: hipLaunchKernelGGL((k_encode_la<2, 256, 0, true>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
+                case 103: hipLaunchKernelGGL((k_encode_la<2, 256, 0, true>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
+                case 104: hipLaunchKernelGGL((k_encode_la80<2, 1024, 0, false>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
+                case 105: hipLaunchKernelGGL((k_encode_la80<2, 1024, 0, true>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
+                case 106: hipLaunchKernelGGL((k_encode_la80<2, 1024, 2, true>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
+                default: hipLaunchKernelGGL((k_encode_la80<2, 256, 0, true>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
             }
             break;
         }
+        case 108: hipLaunchKernelGGL((k_encode<12, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
         default: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
     }
 #else
-    // the shipped kernel: per-wave hybrid (flat chunk list for short frames, with the tag behind the
+    (void)gd;
+    if (enc_path(c, n) == 2) {
+        // the two-pass form (batches of long frames): header records, then one wave per packet
+        void *hp = nullptr;
+        if (rsk::stream_ws_if(c, st, rsk::WS_ENC, 32ull * n, &hp) == RSK_OK) {
+            hipLaunchKernelGGL(k_encode_heads, dim3(grid_for(n)), bd, 0, st, a, c->ks, static_cast<uint4 *>(hp),
+                               c->enc_stat_dev);
+            hipLaunchKernelGGL(k_encode_copy<2>, dim3((unsigned)((n + 3ull) / 4ull)), bd, 0, st, a,
+                               static_cast<const uint32_t *>(hp));
+            c->enc_last_path.store(2, std::memory_order_relaxed);
+            return launch_check("k_encode_heads / k_encode_copy");
+        }
+        g_last_error[0] = 0;  // no records (a capture that would grow them, or no memory): one pass
+    }
+    // the per-set kernel: per-wave hybrid (flat chunk list for short frames, with the tag behind the
     // first chunk loads; software-pipelined one-load DPP per-packet copy, 4 packets per batch, for
     // the rest), tag in the copy loop for long-frame sets, per-set store policy
-    (void)gd;
     hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, 0, st, a, c->ks);
+    c->enc_last_path.store(1, std::memory_order_relaxed);
+    // the statistic for later calls: with no valid value yet, and every kSampleEvery-th call, unless the
+    // call is being captured (a graph replays its path as captured)
+    if (c->enc_path == 0 && n >= kTwoPassMinPackets && !rsk::capturing(st)) {
+        const uint32_t k = c->enc_calls.fetch_add(1, std::memory_order_relaxed);
+        if (!(__atomic_load_n(c->enc_stat_host, __ATOMIC_RELAXED) & kStatValid) || k % kSampleEvery == 0u)
+            hipLaunchKernelGGL(k_enc_sample, dim3(1), dim3(64), 0, st, in->pay_len, n, c->enc_stat_dev);
+    }
 #endif
     return launch_check("k_encode");
 }

@@ -30,16 +30,46 @@ def _le_bytes(x, nbytes):
     return torch.stack([(x >> (8 * k)) & 0xFF for k in range(nbytes)], dim=1).to(torch.uint8)
 
 
+@pytest.fixture(params=[1, 2], ids=lambda p: f"path{p}")
+def pcodec(request, codec):
+    """The codec held to one encode path (rsk__set_encode_path): 1 = k_encode, 2 = the two-pass form."""
+    codec.set_encode_path(request.param)
+    yield codec
+    codec.set_encode_path(0)
+
+
 @pytest.mark.parametrize("cfg", ["c3", "c2", "c4"])
 @pytest.mark.parametrize("pad16", [True, False])
-def test_fullsize_roundtrip(codec, gpu, oracle, cfg, pad16):
-    _roundtrip(codec, gpu, oracle, workload.describe(cfg), pad16)
+def test_fullsize_roundtrip(pcodec, gpu, oracle, cfg, pad16):
+    _roundtrip(pcodec, gpu, oracle, workload.describe(cfg), pad16)
+
+
+def test_encode_path_choice(codec, gpu):
+    """Path 0 (the default) picks per call from the previous batch's sampled mean payload: both
+    paths give the same frames whichever the library picks, call after call (C3 long frames, then
+    C4's mixed lengths)."""
+    import torch
+
+    for cfg in ("c3", "c4", "c3"):
+        d = workload.describe(cfg, 0, 40_000, n=40_000)
+        w = workload.DeviceWorkload(d, gpu)
+        frames = []
+        for path in (1, 0, 0, 2):
+            codec.set_encode_path(path)
+            w.frame.zero_()
+            codec.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame,
+                               w.frame_off, w.status, id_uniform=workload.ID_UNIFORM, pad16=True)
+            torch.cuda.synchronize()
+            frames.append(w.frame.clone())
+        codec.set_encode_path(0)
+        assert all(torch.equal(frames[0], f) for f in frames[1:])
 
 
 @pytest.mark.parametrize("rank", [7, 0])
-def test_c5_shard_roundtrip(codec, gpu, oracle, rank):
+def test_c5_shard_roundtrip(pcodec, gpu, oracle, rank):
     """BASELINE config 5 (64M x 1400-B packets sharded 8 ways): the shard rank `rank` of 8 runs on
     one device (8M packets, ~23 GB of arenas) — what each GPU of the 8-GPU bench line computes."""
+    codec = pcodec
     lo, hi = workload.shard_range(64 << 20, rank, 8)
     d = workload.describe("c5", lo, hi, n=64 << 20)
     assert d.n == 8 << 20 and d.first == lo

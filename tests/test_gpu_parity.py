@@ -116,13 +116,25 @@ def _rand_fields(rng, n):
 ENC_VARIANTS = [int(v) for v in os.environ.get("RSK_ENC_VARIANTS", "0").split(",")]
 
 
-@pytest.fixture(params=ENC_VARIANTS, ids=lambda v: f"encv{v}")
+# the shipped library's two encode paths (rsk__set_encode_path): 1 = the per-set kernel k_encode, 2 = the
+# two-pass form for long frames (k_encode_heads + one wave per packet); in normal use the library picks
+# one per call from the previous batch's mean payload, so every encode test runs both explicitly
+ENC_PATHS = (1, 2)
+
+
+@pytest.fixture(params=[(v, p) for v in ENC_VARIANTS for p in (ENC_PATHS if v == 0 else (0,))],
+                ids=lambda vp: f"encv{vp[0]}" + (f"-path{vp[1]}" if vp[1] else ""))
 def vcodec(request, codec):
-    if request.param:
-        codec.set_encode_variant(request.param)
+    v, p = request.param
+    if v:
+        codec.set_encode_variant(v)
+    if p:
+        codec.set_encode_path(p)
     yield codec
-    if request.param:
+    if v:
         codec.set_encode_variant(0)
+    if p:
+        codec.set_encode_path(0)
 
 
 @pytest.mark.parametrize("layout,pad", [("slots16", 0), ("packed", 0), ("odd_frames", 0), ("odd_payloads", 0),
@@ -180,7 +192,8 @@ def test_encode_edge_lengths_and_layouts(vcodec, gpu, oracle, layout, pad):
     assert bad.size == 0, f"{layout}: {bad.size} bytes differ, first at {bad[:8]}"
 
 
-def test_encode_per_packet_ids(codec, gpu, oracle):
+def test_encode_per_packet_ids(vcodec, gpu, oracle):
+    codec = vcodec
     rng = np.random.default_rng(11)
     n = 777
     plen = rng.integers(1, 1470, n).astype(np.uint16)
@@ -556,10 +569,12 @@ def test_parse_decode_slots(codec, gpu, oracle, slot, flags):
 @pytest.mark.parametrize("layout,pad", [("packed_bytes", 0), ("rand_r", 0), ("rand_r", 16), ("every_r", 0),
                                         ("every_r", 16)])
 @pytest.mark.parametrize("odd_payloads", [False, True])
-def test_encode_any_frame_alignment(codec, gpu, oracle, mix, layout, pad, odd_payloads):
+def test_encode_any_frame_alignment(vcodec, gpu, oracle, mix, layout, pad, odd_payloads):
     """k_encode's vector paths at every destination offset r = frame_off mod 16:
     flat path (short sets), per-packet path (mixed), per-packet with the tag in the copy loop (long),
-    frames packed back to back at byte granularity; bytes outside the frames must survive."""
+    frames packed back to back at byte granularity; bytes outside the frames must survive.  The same
+    for the two-pass form (every frame one wave, header chunks from the records)."""
+    codec = vcodec
     rng = np.random.default_rng(zlib.crc32(repr((mix, layout, pad, odd_payloads)).encode()))
     nset = 24
     n = 64 * nset

@@ -57,7 +57,7 @@ def main():
         h = (w.frame.clone(), w.status.clone())
         if ref is None:
             ref = h
-        elif v[0] % 1000 in (12, 13, 73, 74, 85, 86, 87, 88, 89, 98, 99, 100):
+        elif v[0] % 1000 in (12, 13, 73, 74, 85, 86, 87, 88, 89, 98, 99, 100, 102, 106):
             pass  # k_copy_probe: the memory-side ceiling probe writes the traffic, not the encoding
         elif not (torch.equal(ref[0], h[0]) and torch.equal(ref[1], h[1])):
             raise SystemExit(f"variant {v} frame arena or status differs from variant {variants[0]}")

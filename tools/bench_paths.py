@@ -24,6 +24,8 @@ def main():
                          "mixed lengths, else 16)")
     ap.add_argument("--wire-variants", default="", help="also time these rsk__set_wire_variant values (A/B)")
     ap.add_argument("--only", default="", help="time only these paths (comma list), e.g. demux,demux_64conn")
+    ap.add_argument("--encode-path", type=int, default=0,
+                    help="rsk__set_encode_path for the encode paths: 0 chosen per call, 1 k_encode, 2 two-pass")
     args = ap.parse_args()
     import torch
 
@@ -35,6 +37,8 @@ def main():
     d = workload.describe(args.config, 0, n, n=n)
     w = workload.DeviceWorkload(d, dev)
     cx = rc.Codec(b"hello135", 0)
+    if args.encode_path:
+        cx.set_encode_path(args.encode_path)
     cx.reserve(n)
     s = torch.cuda.current_stream()
     g = torch.Generator(device=dev)

@@ -15,13 +15,15 @@ import statistics
 
 
 def per_launch(path, kernel, counter):
-    vals = []
+    """Median per launch of each kernel whose name starts with `kernel`, summed over those kernels: the
+    encode step is one kernel (k_encode) or two (k_encode_heads + k_encode_copy, the two-pass form)."""
+    vals = {}
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] == counter and r["Kernel_Name"].startswith(kernel):
-            vals.append(float(r["Counter_Value"]))
+            vals.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
     if not vals:
         raise SystemExit(f"no {counter} rows for {kernel} in {path}")
-    return statistics.median(vals), len(vals)
+    return sum(statistics.median(v) for v in vals.values()), {k: len(v) for k, v in vals.items()}
 
 
 def main():
