@@ -3779,7 +3779,7 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
     // the per-set kernel: per-wave hybrid (flat chunk list for short frames, with the tag behind the
     // first chunk loads; software-pipelined one-load DPP per-packet copy, 4 packets per batch, for
     // the rest), tag in the copy loop for long-frame sets, per-set store policy
-    hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, 0, st, a, c->ks);
+    hipLaunchKernelGGL((k_encode<12, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, 0, st, a, c->ks);
     c->enc_last_path.store(1, std::memory_order_relaxed);
     // the statistic for later calls: with no valid value yet, and every kSampleEvery-th call, unless the
     // call is being captured (a graph replays its path as captured)

@@ -14,12 +14,18 @@ import os
 import statistics
 
 
+def base_name(k):
+    return k.split("(")[0].split("<")[0].strip()
+
+
 def per_launch(path, kernel, counter):
-    """Median per launch of each kernel whose name starts with `kernel`, summed over those kernels: the
-    encode step is one kernel (k_encode) or two (k_encode_heads + k_encode_copy, the two-pass form)."""
+    """Median per launch of each kernel named in `kernel` (comma list of names, template and argument
+    lists ignored), summed over them: the encode step is one kernel (k_encode) or two
+    (k_encode_heads,k_encode_copy: the two-pass form)."""
+    names = set(kernel.split(","))
     vals = {}
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] == counter and r["Kernel_Name"].startswith(kernel):
+        if r["Counter_Name"] == counter and base_name(r["Kernel_Name"]) in names:
             vals.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
     if not vals:
         raise SystemExit(f"no {counter} rows for {kernel} in {path}")
@@ -29,7 +35,7 @@ def per_launch(path, kernel, counter):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
-    ap.add_argument("--kernel", default="k_encode")
+    ap.add_argument("--kernel", default="k_encode", help="kernel name, or a comma list summed per launch")
     ap.add_argument("--config", default="c3")
     ap.add_argument("--packets", type=int, default=4194304)
     ap.add_argument("--algorithmic", type=float, default=0.0, help="algorithmic bytes per launch")
