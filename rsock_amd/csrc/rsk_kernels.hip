@@ -162,7 +162,7 @@ struct Lane1 {
     bool slow;
 };
 
-template <bool TAG = true>
+template <bool TAG = true, bool LANE = false>
 __device__ __forceinline__ Lane1 encode_phase1(const EncArgs &a, const KeySched &ks, uint64_t i) {
     Lane1 L;
     L.st = 0;
@@ -179,7 +179,7 @@ __device__ __forceinline__ Lane1 encode_phase1(const EncArgs &a, const KeySched 
                       : (P > RSK_MAX_PAYLOAD ? RSK_SEND_OVERSIZE : (int32_t)(RSK_HEAD_SIZE + P));
         if (L.st > 0) {
             const uint32_t b0 = TAG ? a.payload[L.po] : 0u;
-            if (TAG) tag_of(ks, b0, L.H[0], L.H[1]);
+            if (TAG) tag_of<LANE>(ks, b0, L.H[0], L.H[1]);
             uint32_t id0 = a.id_lo, id1 = a.id_hi;
             if (a.id) {
                 const uint2 v = *reinterpret_cast<const uint2 *>(a.id + 8 * i);
@@ -215,7 +215,7 @@ constexpr uint32_t kStatValid = 0x80000000u;
 // C2's 64 B keep the per-set kernel: one packet per wave idles their lanes, profiles/r04_c3_ceiling.json)
 constexpr uint32_t kTwoPassMinPackets = 16384;
 constexpr uint32_t kTwoPassMinPayload = 1024;
-constexpr uint32_t kSampleEvery = 256;  // per-set calls between two samples (k_enc_sample)
+[[maybe_unused]] constexpr uint32_t kSampleEvery = 256;  // per-set calls between two samples (k_enc_sample)
 __device__ __forceinline__ void enc_sample(const uint16_t *pay_len, uint32_t n, uint32_t *stat) {
     if (blockIdx.x != 0u || threadIdx.x >= 64u) return;
     uint32_t v = pay_len[((uint64_t)threadIdx.x * n) >> 6];
@@ -1080,30 +1080,47 @@ __global__ __launch_bounds__(1024) void k_encode_bc(EncArgs a, KeySched ks) {
 // Pass 1, k_encode_heads: phase 1 one lane per packet (status, the MD5 tag, EncHead, payload[0]; the
 // same code as k_encode's phase 1) into a 32-B record per packet in the stream's workspace.  Pass 2,
 // k_encode_copy: ONE WAVE PER PACKET -- descriptors and the record by scalar loads, the packet's chunk
-// loads, the DPP funnel, the header chunks from the record, nontemporal stores -- so waves are short-lived
+// loads, the DPP funnel, the header chunks from the record, nontemporal loads and stores -- so waves are short-lived
 // and independent.  That is the access shape of the fastest plain copy measured on this chip for C3's
 // arenas (one wave per packet: 6.0 TB/s, against 5.2 TB/s for k_encode's 64-packet sets; DESIGN.md §4.1,
 // profiles/r04_c3_ceiling.json), which k_encode cannot take: a one-packet wave would run a whole MD5
 // compression for one packet (~300 VALU whatever its active lanes; 4.5 ms for C3).  Pass 1 runs the
 // compressions 64 to a wave instead.  rsk_encode_batch takes this form for batches of long frames
 // (enc_path); for short frames one packet per wave idles most lanes and the per-set kernel stays.
-__global__ __launch_bounds__(kBlock) void k_encode_heads(EncArgs a, KeySched ks, uint4 *heads, uint32_t *stat) {
+template <int PPL = 1, bool LANE = false>
+__device__ __forceinline__ void encode_heads(const EncArgs &a, const KeySched &ks, uint4 *heads, uint32_t *stat) {
     stage_tags(ks);
     enc_sample(a.pay_len, a.n, stat);
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    const Lane1 L = encode_phase1<true>(a, ks, i < a.n ? i : a.n);
-    if (i < a.n && L.st > 0) {
-        heads[2 * i] = make_uint4(L.H[0], L.H[1], L.H[2], L.H[3]);
-        heads[2 * i + 1] = make_uint4(L.H[4], L.H[5], L.H[6], L.H[7]);
+#pragma unroll
+    for (int u = 0; u < PPL; ++u) {  // PPL > 1 (A/B): packets u * 256 apart in the block's PPL * 256
+        const uint64_t i = ((uint64_t)blockIdx.x * PPL + u) * kBlock + threadIdx.x;
+        const Lane1 L = encode_phase1<true, LANE>(a, ks, i < a.n ? i : a.n);
+        if (i < a.n && L.st > 0) {
+            heads[2 * i] = make_uint4(L.H[0], L.H[1], L.H[2], L.H[3]);
+            heads[2 * i + 1] = make_uint4(L.H[4], L.H[5], L.H[6], L.H[7]);
+        }
     }
 }
+__global__ __launch_bounds__(kBlock) void k_encode_heads(EncArgs a, KeySched ks, uint4 *heads, uint32_t *stat) {
+    encode_heads(a, ks, heads, stat);
+}
+#ifdef RSK_AB
+// A/B build only (round 4): the header pass held to 80 SGPRs (8 blocks per CU instead of 7), with 2
+// packets per lane, with the word-specialised MD5
+template <int PPL, bool LANE>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(80))) void k_encode_heads_ab(
+    EncArgs a, KeySched ks, uint4 *heads, uint32_t *stat) {
+    encode_heads<PPL, LANE>(a, ks, heads, stat);
+}
+#endif
 
-// NT: bit 0 nontemporal loads, bit 1 nontemporal stores (shipped: 2)
-template <int NT>
-__global__ __launch_bounds__(kBlock) void k_encode_copy(EncArgs a, const uint32_t *heads) {
+// NT: bit 0 nontemporal loads, bit 1 nontemporal stores (shipped: 3; C3 -1.4 % against 2, and 256-thread
+// blocks against 64 / 512 / 1024: profiles/r04r_two_pass_ab.json).  BS: threads per block (A/B).
+template <int NT, int BS = kBlock>
+__global__ __launch_bounds__(BS) void k_encode_copy(EncArgs a, const uint32_t *heads) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const uint64_t i = (uint64_t)blockIdx.x * kWavesPerBlock + w;
+    const uint64_t i = (uint64_t)blockIdx.x * (BS / 64) + w;
     if (i >= a.n) return;
     const uint32_t P = a.pay_len[i];  // uniform address, read-only in this launch: scalar loads
     if (P == 0u || P > (uint32_t)RSK_MAX_PAYLOAD) return;  // status written by pass 1
@@ -3440,11 +3457,13 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 // the two kernels on two streams, concurrently (timing probe: the copy does not wait for the records);
 // 101 / 102 / 103 = 93 / 98 / 92 with the producer's key schedule in VGPRs (ks_vgpr); 104 = 93, 105 / 106 /
 // 107 = 101 / 102 / 103 held to 80 SGPRs (k_encode_la80); 108 = 0 with the flat sets' MD5 on the
-// payload-word-specialised schedule (MODE 12).
+// payload-word-specialised schedule (MODE 12, shipped since); 109 / 110 / 111 / 112 = 76 with the header pass
+// held to 80 SGPRs: 1 / 2 packets per lane, generic / word-specialised MD5 (k_encode_heads_ab); 113 / 114 / 115 =
+// 76 with the copy pass in blocks of 512 / 1024 / 64 threads, 116 = 76 with nontemporal loads in the copy.
 // v + 1000 * cap (cap 1..8): the same kernel held to `cap` blocks per CU by unused LDS.
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
     const int k = v % 1000;
-    if (!c || v < 0 || v / 1000 > 8 || !(k == 0 || k == 12 || k == 13 || k == 37 || k == 47 || (k >= 50 && k <= 108)))
+    if (!c || v < 0 || v / 1000 > 8 || !(k == 0 || k == 12 || k == 13 || k == 37 || k == 47 || (k >= 50 && k <= 116)))
         return RSK_EINVAL;
     c->enc_variant = v;
     return RSK_OK;
@@ -3603,7 +3622,7 @@ int rsk_reserve_stream(rsk_ctx *c, uint32_t n_max, void *stream) {
 // two-pass call, and k_enc_sample behind the first and every kSampleEvery-th per-set call) had a mean
 // payload of at least kTwoPassMinPayload bytes, else the per-set kernel.  The first call on a context
 // has no statistic yet and takes the per-set kernel; either path gives identical bytes.
-static int enc_path(rsk_ctx *c, uint32_t n) {
+[[maybe_unused]] static int enc_path(rsk_ctx *c, uint32_t n) {
     if (c->enc_path) return c->enc_path;
     const uint32_t s = c->enc_stat_host ? __atomic_load_n(c->enc_stat_host, __ATOMIC_RELAXED) : 0u;
     return n >= kTwoPassMinPackets && (s & kStatValid) && (s & ~kStatValid) >= kTwoPassMinPayload ? 2 : 1;
@@ -3683,7 +3702,15 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         case 75:
         case 76:
         case 99:
-        case 100: {
+        case 100:
+        case 109:
+        case 110:
+        case 111:
+        case 112:
+        case 113:
+        case 114:
+        case 115:
+        case 116: {
             static uint4 *heads = nullptr;  // A/B only: the two-pass form's header workspace, never freed
             static uint64_t heads_n = 0;
             if (heads_n < n) {
@@ -3707,6 +3734,25 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
                                    reinterpret_cast<const uint32_t *>(heads));
                 (void)hipEventRecord(e1, s2);
                 (void)hipStreamWaitEvent(st, e1, 0);
+                break;
+            }
+            if (k == 109 || k == 110 || k == 111 || k == 112) {
+                void (*hk)(EncArgs, KeySched, uint4 *, uint32_t *) =
+                    k == 109 ? k_encode_heads_ab<1, false> : k == 110 ? k_encode_heads_ab<2, false>
+                    : k == 111 ? k_encode_heads_ab<1, true> : k_encode_heads_ab<2, true>;
+                hipLaunchKernelGGL(hk, dim3(k == 110 || k == 112 ? (grid_for(n) + 1u) / 2u : grid_for(n)), bd, 0, st,
+                                   a, c->ks, heads, c->enc_stat_dev);
+                hipLaunchKernelGGL(k_encode_copy<2>, dim3((unsigned)((n + 3ull) / 4ull)), bd, lds, st, a,
+                                   reinterpret_cast<const uint32_t *>(heads));
+                break;
+            }
+            if (k >= 113 && k <= 116) {  // the copy pass: 512 / 1024 / 64 threads per block, nontemporal loads
+                hipLaunchKernelGGL(k_encode_heads, dim3(grid_for(n)), bd, 0, st, a, c->ks, heads, c->enc_stat_dev);
+                const uint32_t* hr = reinterpret_cast<const uint32_t *>(heads);
+                if (k == 113) hipLaunchKernelGGL((k_encode_copy<2, 512>), dim3((unsigned)((n + 7ull) / 8ull)), dim3(512), 0, st, a, hr);
+                else if (k == 114) hipLaunchKernelGGL((k_encode_copy<2, 1024>), dim3((unsigned)((n + 15ull) / 16ull)), dim3(1024), 0, st, a, hr);
+                else if (k == 115) hipLaunchKernelGGL((k_encode_copy<2, 64>), dim3((unsigned)n), dim3(64), 0, st, a, hr);
+                else hipLaunchKernelGGL((k_encode_copy<3>), dim3((unsigned)((n + 3ull) / 4ull)), bd, 0, st, a, hr);
                 break;
             }
             if (k != 99) hipLaunchKernelGGL(k_encode_heads, dim3(grid_for(n)), bd, 0, st, a, c->ks, heads, c->enc_stat_dev);
@@ -3769,7 +3815,7 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         if (rsk::stream_ws_if(c, st, rsk::WS_ENC, 32ull * n, &hp) == RSK_OK) {
             hipLaunchKernelGGL(k_encode_heads, dim3(grid_for(n)), bd, 0, st, a, c->ks, static_cast<uint4 *>(hp),
                                c->enc_stat_dev);
-            hipLaunchKernelGGL(k_encode_copy<2>, dim3((unsigned)((n + 3ull) / 4ull)), bd, 0, st, a,
+            hipLaunchKernelGGL(k_encode_copy<3>, dim3((unsigned)((n + 3ull) / 4ull)), bd, 0, st, a,
                                static_cast<const uint32_t *>(hp));
             c->enc_last_path.store(2, std::memory_order_relaxed);
             return launch_check("k_encode_heads / k_encode_copy");
