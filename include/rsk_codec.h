@@ -137,8 +137,9 @@ int rsk_get_tag_mode(const rsk_ctx *ctx);
  * (from one host thread at a time, as with any hipStream_t).  The only per-context state the
  * kernels read is the immutable key schedule and tag table (and the tag mode, passed by value).
  *
- * Pre-size the compaction scratch of `stream` (rsk_reserve: the legacy default stream, NULL) for
- * batches of up to n packets.  Batch calls grow it on demand, which waits for that stream to
+ * Pre-size the scratch of `stream` (rsk_reserve: the legacy default stream, NULL) for batches of up
+ * to n packets: the compaction state and, for n >= 16384, the 32-B-per-packet header records of the
+ * two-pass encode (rsk_encode_batch).  Batch calls grow it on demand, which waits for that stream to
  * drain and allocates; reserve first if batch calls will be captured into a hipGraph. */
 int rsk_reserve(rsk_ctx *ctx, uint32_t n_max);
 int rsk_reserve_stream(rsk_ctx *ctx, uint32_t n_max, void *stream);
@@ -202,7 +203,13 @@ typedef struct rsk_encode_out {
 #define RSK_ENC_ZERO_PAD128 0x2u
 
 /* frame_i = tag(8) | EncHead(23) | payload(P), written to frame_arena + frame_off[i].
- * Frames must not overlap each other or the payload arena. */
+ * Frames must not overlap each other or the payload arena.
+ * Two device paths, identical bytes: batches of long frames (>= 16384 packets, the context's last
+ * sampled batch at a mean payload >= 1024 B) run a header pass (the MD5 tags 64 to a wave, 32-B
+ * records in the stream's scratch) and then one wave per packet; other batches run the per-set kernel.
+ * The choice reads a host-mapped statistic the previous calls' kernels left (no synchronisation); a
+ * call captured into a hipGraph keeps the path it was captured with, and one captured on a stream
+ * without reserved records takes the per-set kernel. */
 int rsk_encode_batch(rsk_ctx *ctx, uint32_t n, const rsk_encode_in *in, const rsk_encode_out *out,
                      void *stream);
 
