@@ -229,3 +229,79 @@ def test_capture_needs_reserved_stream_and_release(gpu):
         assert cx.check_device_errors() == 0
     finally:
         cx.close()
+
+
+def _c3_frames(codec, gpu, w, path, stream=None):
+    import torch
+
+    codec.set_encode_path(path)
+    w.frame.zero_()
+    codec.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
+                       w.status, id_uniform=workload.ID_UNIFORM, pad16=True, stream=stream)
+    torch.cuda.synchronize()
+    return w.frame.clone(), w.status.clone()
+
+
+def test_two_pass_encode_in_captured_graph(gpu):
+    """The two-pass encode (header records in the capture stream's scratch, then one wave per packet)
+    captured into a hipGraph and replayed gives the per-set kernel's bytes; a stream whose records were
+    not reserved captures the per-set kernel instead (same bytes), never an allocation."""
+    import torch
+
+    from rsock_amd.codec import Codec
+
+    n = 1 << 17
+    d = workload.describe("c3", 0, n, n=n)
+    w = workload.DeviceWorkload(d, gpu)
+    cx = Codec(b"hello135", 0)
+    try:
+        ref_f, ref_s = _c3_frames(cx, gpu, w, 1)
+        for reserved in (True, False):
+            s = torch.cuda.Stream(gpu)
+            if reserved:
+                cx.reserve(n, stream=s)
+            cx.set_encode_path(2)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                cx.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
+                                w.status, id_uniform=workload.ID_UNIFORM, pad16=True, stream=s)
+            assert cx.last_encode_path == (2 if reserved else 1)
+            for _ in range(2):
+                w.frame.zero_()
+                w.status.fill_(-9)
+                torch.cuda.synchronize()
+                g.replay()
+                torch.cuda.synchronize()
+                assert torch.equal(w.frame, ref_f) and torch.equal(w.status, ref_s)
+            del g
+            cx.set_encode_path(0)
+            cx.release_stream(s)
+    finally:
+        cx.close()
+
+
+def test_two_pass_encode_two_streams(codec, gpu):
+    """Two streams of one context encode different batches on the two-pass path at once: each stream
+    has its own header records (per-stream scratch), so neither batch sees the other's headers."""
+    import torch
+
+    n = 1 << 17
+    da = workload.describe("c3", 0, n, n=2 * n)
+    db = workload.describe("c3", n, 2 * n, n=2 * n)
+    wa, wb = workload.DeviceWorkload(da, gpu), workload.DeviceWorkload(db, gpu)
+    ref = [_c3_frames(codec, gpu, w, 1) for w in (wa, wb)]
+    sa, sb = torch.cuda.Stream(gpu), torch.cuda.Stream(gpu)
+    codec.set_encode_path(2)
+    try:
+        for w in (wa, wb):
+            w.frame.zero_()
+        torch.cuda.synchronize()
+        for _ in range(3):
+            for w, s in ((wa, sa), (wb, sb)):
+                codec.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame,
+                                   w.frame_off, w.status, id_uniform=workload.ID_UNIFORM, pad16=True, stream=s)
+        torch.cuda.synchronize()
+    finally:
+        codec.set_encode_path(0)
+    for w, (f, st) in zip((wa, wb), ref):
+        assert torch.equal(w.frame, f) and torch.equal(w.status, st)
