@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--pad16", action="store_true", help="RSK_ENC_ZERO_PAD16 (not for the byte-packed layout)")
+    ap.add_argument("--encode-path", type=int, default=0,
+                    help="rsk__set_encode_path: 0 chosen per call, 1 per-set kernel, 2 two-pass")
     args = ap.parse_args()
     import torch
 
@@ -37,6 +39,8 @@ def main():
     d = workload.describe(args.config, 0, n, n=n)
     w = workload.DeviceWorkload(d, dev)
     cx = rc.Codec(b"hello135", 0)
+    if args.encode_path:
+        cx.set_encode_path(args.encode_path)
     s = torch.cuda.current_stream()
     flen = d.frame_len.astype(np.int64)
     r16 = (flen + 15) // 16 * 16
