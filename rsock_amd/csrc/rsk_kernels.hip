@@ -217,7 +217,7 @@ constexpr uint32_t kTwoPassMinPackets = 16384;
 constexpr uint32_t kTwoPassMinPayload = 1024;
 [[maybe_unused]] constexpr uint32_t kSampleEvery = 256;  // per-set calls between two samples (k_enc_sample)
 __device__ __forceinline__ void enc_sample(const uint16_t *pay_len, uint32_t n, uint32_t *stat) {
-    if (blockIdx.x != 0u || threadIdx.x >= 64u) return;
+    if (stat == nullptr || blockIdx.x != 0u || threadIdx.x >= 64u) return;
     uint32_t v = pay_len[((uint64_t)threadIdx.x * n) >> 6];
 #pragma unroll
     for (int off = 32; off; off >>= 1) v += (uint32_t)__shfl_xor((int)v, off);
@@ -3502,12 +3502,18 @@ rsk_ctx *rsk_create(const uint8_t *key, uint32_t key_len, int device) {
     e = g.ok ? hipMalloc(&c->tag_dev, 256 * sizeof(uint2)) : hipErrorInvalidDevice;
     if (e == hipSuccess) e = hipMalloc(&c->err_dev, sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemset(c->err_dev, 0, sizeof(uint32_t));
-    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&c->enc_stat_host), sizeof(uint32_t),
-                                           hipHostMallocMapped | hipHostMallocCoherent);
-    if (e == hipSuccess) {
+    // the encode path statistic's host-mapped word (enc_path); without it every call takes the per-set
+    // kernel unless a path is forced -- not an error
+    if (e == hipSuccess && hipHostMalloc(reinterpret_cast<void **>(&c->enc_stat_host), sizeof(uint32_t),
+                                         hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
         *c->enc_stat_host = 0u;
-        e = hipHostGetDevicePointer(reinterpret_cast<void **>(&c->enc_stat_dev), c->enc_stat_host, 0);
+        if (hipHostGetDevicePointer(reinterpret_cast<void **>(&c->enc_stat_dev), c->enc_stat_host, 0) != hipSuccess) {
+            (void)hipHostFree(c->enc_stat_host);
+            c->enc_stat_host = nullptr;
+            c->enc_stat_dev = nullptr;
+        }
     }
+    (void)hipGetLastError();  // a failed optional allocation above must not surface as a later launch error
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
     if (e == hipSuccess) {
         hipLaunchKernelGGL(k_tag_table, dim3(1), dim3(256), 0, s, c->ks, c->tag_dev);
@@ -3829,7 +3835,7 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
     c->enc_last_path.store(1, std::memory_order_relaxed);
     // the statistic for later calls: with no valid value yet, and every kSampleEvery-th call, unless the
     // call is being captured (a graph replays its path as captured)
-    if (c->enc_path == 0 && n >= kTwoPassMinPackets && !rsk::capturing(st)) {
+    if (c->enc_path == 0 && c->enc_stat_dev && n >= kTwoPassMinPackets && !rsk::capturing(st)) {
         const uint32_t k = c->enc_calls.fetch_add(1, std::memory_order_relaxed);
         if (!(__atomic_load_n(c->enc_stat_host, __ATOMIC_RELAXED) & kStatValid) || k % kSampleEvery == 0u)
             hipLaunchKernelGGL(k_enc_sample, dim3(1), dim3(64), 0, st, in->pay_len, n, c->enc_stat_dev);
