@@ -851,13 +851,14 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
     const bool defer = MODE != 3 && MODE != 7 && !flat && (MODE == 10 || fl >= kDeferTagMeanBytes * cnt);
     // MODE 11 (shipped): as 9 with the flat sets' tag and header stores behind the first chunk loads;
     // MODE 12 (A/B): 11 with the flat sets' MD5 on the payload-word-specialised schedule (md5_tag_lane)
-    constexpr bool kFlatTagQ = MODE == 11 || MODE == 12;
+    // MODE 13 / 14 (A/B): 12 with the frames under 256 / 512 B of a per-packet set on the flat list
+    constexpr bool kFlatTagQ = MODE == 11 || MODE == 12 || MODE == 13 || MODE == 14;
     if constexpr (MODE != 3 && MODE != 7) {  // the tag now, except for the sets whose copy loop takes it
         if (!defer && !(kFlatTagQ && flat)) encode_tag(a, ks, L);
     }
     if (flat) {
         if (!kFlatTagQ && vec) store_head(L.H, a.frame + L.fo);
-        copy_flat<U, kFlatTagQ, MODE == 12>(a, ks, L, lane, vec, recs, cend);
+        copy_flat<U, kFlatTagQ, MODE >= 12>(a, ks, L, lane, vec, recs, cend);
         return;
     }
     bool nt = NT == 2;
@@ -878,7 +879,7 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
     // first slot store (lanes 0..2, words by readlane); the others by the slot lane (store_head).
     // Measured (A/B, profiles/r02_ab_head.json): C3 2.34 vs 2.55 ms with the first; C4 0.389 vs
     // 0.420 ms with the second.
-    if constexpr (MODE == 9 || MODE == 10 || MODE == 11 || MODE == 12) {  // software-pipelined per-packet copy
+    if constexpr (MODE == 9 || MODE == 10 || MODE >= 11) {  // software-pipelined per-packet copy
         // Byte-packed long frames (no pad; a frame ends mid-chunk and the next packet's frame
         // starts there): the TAG-form copy with the boundary-chunk merge (TailCarry), which writes
         // each shared chunk as one 16-B store.  Only sets that really have such a pair take it: the
@@ -900,8 +901,19 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
             else if (nt) copy_pkt_pipe<PU, 2, true, TG>(a, ks, L, lane, vm);
             else copy_pkt_pipe<PU, 0, true, TG>(a, ks, L, lane, vm);
         } else {
-            if (nt) copy_pkt_pipe<PU, 2, false>(a, ks, L, lane, vm);
-            else copy_pkt_pipe<PU, 0, false>(a, ks, L, lane, vm);
+            uint64_t pm = vm;
+            if constexpr (MODE == 13 || MODE == 14) {  // the set's short frames on the flat list first
+                constexpr int32_t kShort = MODE == 13 ? 256 : 512;
+                const bool shp = vec && L.st < kShort;
+                const uint64_t sm = __ballot(shp);
+                if (sm) {
+                    if (shp) store_head(L.H, a.frame + L.fo);
+                    copy_flat<U, false>(a, ks, L, lane, shp, recs, cend);
+                    pm &= ~sm;
+                }
+            }
+            if (nt) copy_pkt_pipe<PU, 2, false>(a, ks, L, lane, pm);
+            else copy_pkt_pipe<PU, 0, false>(a, ks, L, lane, pm);
         }
         return;
     }
@@ -3459,11 +3471,12 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 // 107 = 101 / 102 / 103 held to 80 SGPRs (k_encode_la80); 108 = 0 with the flat sets' MD5 on the
 // payload-word-specialised schedule (MODE 12, shipped since); 109 / 110 / 111 / 112 = 76 with the header pass
 // held to 80 SGPRs: 1 / 2 packets per lane, generic / word-specialised MD5 (k_encode_heads_ab); 113 / 114 / 115 =
-// 76 with the copy pass in blocks of 512 / 1024 / 64 threads, 116 = 76 with nontemporal loads in the copy.
+// 76 with the copy pass in blocks of 512 / 1024 / 64 threads, 116 = 76 with nontemporal loads in the copy;
+// 117 / 118 = the per-set kernel with a per-packet set's frames under 256 / 512 B on the flat list (MODE 13 / 14).
 // v + 1000 * cap (cap 1..8): the same kernel held to `cap` blocks per CU by unused LDS.
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
     const int k = v % 1000;
-    if (!c || v < 0 || v / 1000 > 8 || !(k == 0 || k == 12 || k == 13 || k == 37 || k == 47 || (k >= 50 && k <= 116)))
+    if (!c || v < 0 || v / 1000 > 8 || !(k == 0 || k == 12 || k == 13 || k == 37 || k == 47 || (k >= 50 && k <= 118)))
         return RSK_EINVAL;
     c->enc_variant = v;
     return RSK_OK;
@@ -3811,6 +3824,8 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
             break;
         }
         case 108: hipLaunchKernelGGL((k_encode<12, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
+        case 117: hipLaunchKernelGGL((k_encode<13, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
+        case 118: hipLaunchKernelGGL((k_encode<14, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
         default: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
     }
 #else
