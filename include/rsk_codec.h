@@ -138,9 +138,8 @@ int rsk_get_tag_mode(const rsk_ctx *ctx);
  * kernels read is the immutable key schedule and tag table (and the tag mode, passed by value).
  *
  * Pre-size the scratch of `stream` (rsk_reserve: the legacy default stream, NULL) for batches of up
- * to n packets: the compaction state and, for n >= 16384, the per-packet records of the two-pass
- * encode forms (rsk_encode_batch: 32 B, rsk_encode_wire_batch: up to 112 B; 112 B per packet are
- * reserved).  Batch calls grow it on demand, which waits for that stream to
+ * to n packets: the compaction state and, for n >= 16384, the 32-B-per-packet header records of the
+ * two-pass encode (rsk_encode_batch).  Batch calls grow it on demand, which waits for that stream to
  * drain and allocates; reserve first if batch calls will be captured into a hipGraph. */
 int rsk_reserve(rsk_ctx *ctx, uint32_t n_max);
 int rsk_reserve_stream(rsk_ctx *ctx, uint32_t n_max, void *stream);

@@ -1650,7 +1650,7 @@ __device__ __forceinline__ void wire_put_prefix(uint32_t (&PW)[WireGeom<E>::NPW]
 template <int E>
 __device__ __forceinline__ void wire_phase1(const EncArgs &a, const WireArgs &wa, const Lane1 &L, uint64_t i,
                                             uint32_t (&PW)[WireGeom<E>::NPW], uint32_t &sum_pre, int32_t &wst,
-                                            bool pre = true, bool put_status = true) {
+                                            bool pre = true) {
     using G = WireGeom<E>;
 #pragma unroll
     for (int q = 0; q < G::NPW; ++q) PW[q] = 0;
@@ -1660,7 +1660,7 @@ __device__ __forceinline__ void wire_phase1(const EncArgs &a, const WireArgs &wa
     const uint32_t flen = (uint32_t)L.st, P = flen - RSK_HEAD_SIZE;
     const uint32_t wlen = G::HL + flen;
     wst = (int32_t)wlen;
-    if (put_status) a.status[i] = wst;
+    a.status[i] = wst;
     const uint32_t src = wa.src[i], dst = wa.dst[i], sp = wa.sp[i], dp = wa.dp[i];
     const uint32_t seq = wa.seq[i], ack = wa.ack[i], fl = wa.flag[i], id = wa.ip_id[i];
     if constexpr (E > 0) {
@@ -2129,150 +2129,6 @@ __device__ __forceinline__ void copy_wire_pkt_pipe(const EncArgs &a, const KeySc
 // one flat chunk list (as copy_flat), each lane adding its chunk's halfword sum into the packet's
 // LDS slot; (2) the NPRE prefix chunks of every packet as a dense (packet, chunk) grid read from the
 // LDS stage, the TCP checksum patched into chunk CK/16 — both passes store coalesced runs.
-// ---- the two-pass form of the wire build for batches of long frames (round 4; as k_encode_heads /
-// k_encode_copy).  Pass 1 (k_wire_heads): one lane per packet -- phase 1 and the
-// packet's whole prefix image (link, IPv4 with its checksum, TCP, frame header, first payload bytes)
-// with its TCP checksum share (wire_phase1, as the per-set kernels' phase 1), RS words per packet into
-// the stream's workspace.  Pass 2 (k_wire_copy): one wave per packet -- the record by scalar loads,
-// lane m copies image chunk NPRE + m (aligned source chunk m, funnel partner from lane m + 1 by DPP)
-// and sums its halfwords; one wave sum gives the TCP checksum, patched into the prefix before any
-// prefix chunk is stored.  Packets at r = dst mod 16 != 0 are stored shifted: destination chunk j =
-// image chunks j - 1 and j at offset 16 - r, the partner from lane - 1 by DPP (wave_shr), lane 0 from
-// the last prefix chunk.  (A first form built the prefix in the copy wave from the descriptors: 2.5x
-// slower -- ~400 wave instructions of per-packet work, profiles/r04t_wire_two_pass.json.)
-template <int E>
-struct WireRec {
-    static constexpr int RS = WireGeom<E>::NPW + 4;  // prefix words, sum_pre, 3 words of padding
-    static constexpr int RQ = RS / 4;                // uint4 per record
-};
-
-template <int E>
-__global__ __launch_bounds__(kBlock) void k_wire_heads(EncArgs a, WireArgs wa, KeySched ks, uint4 *rec,
-                                                       uint32_t *stat) {
-    using G = WireGeom<E>;
-    stage_tags(ks);
-    enc_sample(a.pay_len, a.n, stat);
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    const Lane1 L = encode_phase1<true>(a, ks, i < a.n ? i : a.n);
-    if (i >= a.n || L.st <= 0) return;  // status written by phase 1
-    uint32_t PW[G::NPW], sum_pre;
-    int32_t wst;
-    wire_phase1<E>(a, wa, L, i, PW, sum_pre, wst);  // status = the wire length
-    uint4 *r = rec + (uint64_t)WireRec<E>::RQ * i;
-#pragma unroll
-    for (int q = 0; q < G::NPW / 4; ++q) r[q] = make_uint4(PW[4 * q], PW[4 * q + 1], PW[4 * q + 2], PW[4 * q + 3]);
-    r[G::NPW / 4] = make_uint4(sum_pre, 0u, 0u, 0u);
-}
-
-// uint4 of words 4k .. 4k + 3 of a uniform word array, k per lane (< N / 4), as AND/OR of masks (as
-// rsk::word_at): a select chain on a per-lane index becomes a dynamic extract lowered through scratch
-template <int N>
-__device__ __forceinline__ uint4 pick_chunk(const uint32_t (&W)[N], uint32_t k) {
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-    for (int q = 0; q < N / 4; ++q) {
-        const uint32_t m = (uint32_t)((int32_t)((k ^ (uint32_t)q) - 1u) >> 31);
-        v.x |= W[4 * q] & m;
-        v.y |= W[4 * q + 1] & m;
-        v.z |= W[4 * q + 2] & m;
-        v.w |= W[4 * q + 3] & m;
-    }
-    return v;
-}
-
-template <int E, int NT>
-__global__ __launch_bounds__(kBlock) void k_wire_copy(EncArgs a, const uint32_t *rec) {
-    using G = WireGeom<E>;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const uint64_t i = (uint64_t)blockIdx.x * kWavesPerBlock + w;
-    if (i >= a.n) return;
-    const uint32_t P = a.pay_len[i];  // uniform address, read-only in this launch: scalar loads
-    if (P == 0u || P > (uint32_t)RSK_MAX_PAYLOAD) return;  // status written by pass 1
-    const uint8_t *pay = a.payload + a.pay_off[i];
-    uint8_t *dst = a.frame + a.frame_off[i];
-    const uint32_t wlen = G::HL + RSK_HEAD_SIZE + P;
-    // payload chunks: lane m holds image chunk NPRE + m (slot q: m + 64 q)
-    const uint32_t shp = (uint32_t)((reinterpret_cast<uintptr_t>(pay) + G::D0) & 15u);
-    const uint8_t *src_al = pay + G::D0 - shp;
-    const int32_t last_rel = (int32_t)P - 1 - G::D0 + (int32_t)shp;
-    const uint32_t nch = (wlen + 15u) >> 4;  // image chunks holding packet bytes
-    const bool s1 = nch > (uint32_t)G::NPRE + 64u;  // slot 1 holds packet bytes (uniform)
-    uint4 A[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        A[q] = make_uint4(0u, 0u, 0u, 0u);
-        const uint32_t m = lane + 64u * q;
-        if (q == 1 && last_rel < 16 * 64) continue;  // uniform: no payload byte in source chunk 64 on
-        if ((int32_t)(16u * m) <= last_rel) A[q] = ld16<NT>(src_al + 16u * m);
-    }
-    uint32_t PW[G::NPW];
-    const uint32_t *rw = rec + (uint64_t)WireRec<E>::RS * i;  // uniform address: scalar loads
-#pragma unroll
-    for (int q = 0; q < G::NPW; ++q) PW[q] = rw[q];
-    const uint32_t sum_pre = rw[G::NPW];
-    // payload image chunks: funnel, mask past the packet's end, halfword sums
-    uint4 B[2], V[2];
-    B[0] = make_uint4(wave_shl1(A[0].x), wave_shl1(A[0].y), wave_shl1(A[0].z), wave_shl1(A[0].w));
-    B[1] = make_uint4(0u, 0u, 0u, 0u);
-    {
-        const uint4 l0 = rdl4(A[1], 0);
-        if (lane == 63u) B[0] = l0;
-    }
-    if (s1) B[1] = make_uint4(wave_shl1(A[1].x), wave_shl1(A[1].y), wave_shl1(A[1].z), wave_shl1(A[1].w));
-    uint32_t part = 0;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        V[q] = make_uint4(0u, 0u, 0u, 0u);
-        if (q == 1 && !s1) continue;  // uniform
-        const uint32_t k = G::NPRE + lane + 64u * q;
-        if (k < nch) {
-            V[q] = rsk::funnel16(A[q], B[q], shp);
-            const int lim = (int)wlen - 16 * (int)k;
-            if (lim < 16) V[q] = rsk::keep_bytes16(V[q], lim);
-            part = hsum4(V[q], part);
-        }
-    }
-    const uint32_t ck = ~fold16(wave_sum(part) + sum_pre) & 0xffffu;
-    PW[G::CK / 4] |= ck << (8 * (G::CK & 3));
-    const uint32_t r = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15u);  // uniform
-    const bool pad = a.pad != 0u;
-    if (r == 0u) {
-        const uint32_t nst = (padded_len(dst, wlen, a.pad) + 15u) >> 4;
-        if (lane < (uint32_t)G::NPRE && lane < nst)
-            store_last16<NT>(dst + 16u * lane, pick_chunk(PW, lane), (int)wlen - 16 * (int)lane, pad);
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            if (q == 1 && nst <= (uint32_t)G::NPRE + 64u) continue;  // uniform
-            const uint32_t k = G::NPRE + lane + 64u * q;
-            if (k < nst) store_last16<NT>(dst + 16u * k, V[q], (int)wlen - 16 * (int)k, pad);
-        }
-        return;
-    }
-    // shifted: destination chunk j = image chunks j - 1, j at offset 16 - r (bytes from d0 = dst - r)
-    uint8_t *d0 = dst - r;
-    const uint32_t nst = (r + padded_len(dst, wlen, a.pad) + 15u) >> 4;
-    const int wend = (int)(r + wlen);
-    const uint32_t sh = 16u - r;
-    const uint4 l63 = rdl4(V[0], 63);
-    const uint4 lastpre = make_uint4(PW[G::NPW - 4], PW[G::NPW - 3], PW[G::NPW - 2], PW[G::NPW - 1]);
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        uint4 prev = make_uint4(wave_shr1(V[q].x), wave_shr1(V[q].y), wave_shr1(V[q].z), wave_shr1(V[q].w));
-        if (lane == 0u) prev = q == 0 ? lastpre : l63;
-        const uint32_t j = G::NPRE + lane + 64u * q;
-        if (q == 1 && nst <= (uint32_t)G::NPRE + 64u) continue;  // uniform
-        if (j < nst) store_last16<NT>(d0 + 16u * j, rsk::funnel16(prev, V[q], sh), wend - 16 * (int)j, pad);
-    }
-    if (lane < (uint32_t)G::NPRE && lane < nst) {
-        const uint4 c1 = pick_chunk(PW, lane);
-        const uint4 c0 = lane ? pick_chunk(PW, lane - 1u) : make_uint4(0u, 0u, 0u, 0u);
-        const uint4 d = rsk::funnel16(c0, c1, sh);
-        if (lane == 0u) rsk::store_range16(d0, d, r, 16u);
-        else store_last16<NT>(d0 + 16u * lane, d, wend - 16 * (int)lane, pad);
-    }
-}
-
 template <int E, int U>
 __device__ __forceinline__ void copy_wire_flat(const EncArgs &a, const Lane1 &L, const uint32_t *stage,
                                                uint32_t sum_pre, int32_t wst, uint32_t lane, bool mine,
@@ -3776,8 +3632,8 @@ int rsk_reserve_stream(rsk_ctx *c, uint32_t n_max, void *stream) {
     Compact ck;
     const int r = ensure_compact(c, n_max, (hipStream_t)stream, ck);
     if (r || n_max < kTwoPassMinPackets) return r;
-    void *p = nullptr;  // the two-pass forms' records: 32 B per packet (frames), 112 B (Ethernet wire packets)
-    return rsk::stream_ws(c, (hipStream_t)stream, rsk::WS_ENC, 4ull * WireRec<14>::RS * n_max, &p);
+    void *p = nullptr;  // the two-pass encode's header records (32 B per packet)
+    return rsk::stream_ws(c, (hipStream_t)stream, rsk::WS_ENC, 32ull * n_max, &p);
 }
 
 // Encode path per call: the context's forced path (rsk__set_encode_path), else the two-pass form for
@@ -3785,15 +3641,6 @@ int rsk_reserve_stream(rsk_ctx *c, uint32_t n_max, void *stream) {
 // two-pass call, and k_enc_sample behind the first and every kSampleEvery-th per-set call) had a mean
 // payload of at least kTwoPassMinPayload bytes, else the per-set kernel.  The first call on a context
 // has no statistic yet and takes the per-set kernel; either path gives identical bytes.
-// After a per-set call: the statistic for later calls, when there is no valid value yet and every
-// kSampleEvery-th call, unless the stream is being captured (a graph replays its path as captured).
-[[maybe_unused]] static void enc_maybe_sample(rsk_ctx *c, hipStream_t st, const uint16_t *pay_len, uint32_t n) {
-    if (c->enc_path != 0 || !c->enc_stat_dev || n < kTwoPassMinPackets || rsk::capturing(st)) return;
-    const uint32_t k = c->enc_calls.fetch_add(1, std::memory_order_relaxed);
-    if (!(__atomic_load_n(c->enc_stat_host, __ATOMIC_RELAXED) & kStatValid) || k % kSampleEvery == 0u)
-        hipLaunchKernelGGL(k_enc_sample, dim3(1), dim3(64), 0, st, pay_len, n, c->enc_stat_dev);
-}
-
 [[maybe_unused]] static int enc_path(rsk_ctx *c, uint32_t n) {
     if (c->enc_path) return c->enc_path;
     const uint32_t s = c->enc_stat_host ? __atomic_load_n(c->enc_stat_host, __ATOMIC_RELAXED) : 0u;
@@ -4001,7 +3848,13 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
     // the rest), tag in the copy loop for long-frame sets, per-set store policy
     hipLaunchKernelGGL((k_encode<12, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, 0, st, a, c->ks);
     c->enc_last_path.store(1, std::memory_order_relaxed);
-    enc_maybe_sample(c, st, in->pay_len, n);
+    // the statistic for later calls: with no valid value yet, and every kSampleEvery-th call, unless the
+    // call is being captured (a graph replays its path as captured)
+    if (c->enc_path == 0 && c->enc_stat_dev && n >= kTwoPassMinPackets && !rsk::capturing(st)) {
+        const uint32_t k = c->enc_calls.fetch_add(1, std::memory_order_relaxed);
+        if (!(__atomic_load_n(c->enc_stat_host, __ATOMIC_RELAXED) & kStatValid) || k % kSampleEvery == 0u)
+            hipLaunchKernelGGL(k_enc_sample, dim3(1), dim3(64), 0, st, in->pay_len, n, c->enc_stat_dev);
+    }
 #endif
     return launch_check("k_encode");
 }
@@ -4054,32 +3907,10 @@ int rsk_encode_wire_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const
         else { RSK_WIRE4(0, 5, 108, 2); RSK_WIRE(0, 4, 2, 2); }
     }
 #else
-    if (enc_path(c, n) == 2) {
-        // the two-pass form (batches of long frames): prefix records, then one wave per packet
-        void *hp = nullptr;
-        const size_t rb = 4ull * WireRec<14>::RS * n;  // the larger record (Ethernet)
-        if (rsk::stream_ws_if(c, st, rsk::WS_ENC, rb, &hp) == RSK_OK) {
-            const dim3 g1((unsigned)((n + 3ull) / 4ull));
-            if (wire->with_eth) {
-                hipLaunchKernelGGL(k_wire_heads<14>, dim3(grid_for(n)), dim3(kBlock), 0, st, a, w, c->ks,
-                                   static_cast<uint4 *>(hp), c->enc_stat_dev);
-                hipLaunchKernelGGL((k_wire_copy<14, 3>), g1, dim3(kBlock), 0, st, a, static_cast<const uint32_t *>(hp));
-            } else {
-                hipLaunchKernelGGL(k_wire_heads<0>, dim3(grid_for(n)), dim3(kBlock), 0, st, a, w, c->ks,
-                                   static_cast<uint4 *>(hp), c->enc_stat_dev);
-                hipLaunchKernelGGL((k_wire_copy<0, 3>), g1, dim3(kBlock), 0, st, a, static_cast<const uint32_t *>(hp));
-            }
-            c->enc_last_path.store(2, std::memory_order_relaxed);
-            return launch_check("k_wire_heads / k_wire_copy");
-        }
-        g_last_error[0] = 0;  // no records (a capture that would grow them, or no memory): one pass
-    }
-    // the per-set kernels: per-packet half (DPP copy, 8 packets per iteration, tag + payload prefix in
+    // the shipped kernels: per-packet half (DPP copy, 8 packets per iteration, tag + payload prefix in
     // the copy loop for long-frame sets, 4 waves/SIMD) then the flat half
     if (wire->with_eth) { RSK_WIRE4(14, 5, 108, 2); RSK_WIRE(14, 4, 2, 2); }
     else { RSK_WIRE4(0, 5, 108, 2); RSK_WIRE(0, 4, 2, 2); }
-    c->enc_last_path.store(1, std::memory_order_relaxed);
-    enc_maybe_sample(c, st, in->pay_len, n);
 #endif
 #undef RSK_WIRE
 #undef RSK_WIRE4

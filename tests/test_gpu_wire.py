@@ -23,16 +23,10 @@ KEY = b"hello135"
 @pytest.mark.parametrize("layout", ["aligned", "odd_payload", "odd_wire", "any_wire", "packed_wire"])
 @pytest.mark.parametrize("pad", [0, 16, 128])
 @pytest.mark.parametrize("mix", ["mixed", "short", "bimodal", "long"])
-# shipped kernels: both encode paths (rsk__set_encode_path: 1 the per-set wire kernels, 2 the two-pass
-# form, prefix records then one wave per packet); RSK_LIB=librsk_ab.so RSK_WIRE_VARIANTS=0,1,...,9 covers
-# the A/B build
+# shipped kernel only; RSK_LIB=librsk_ab.so RSK_WIRE_VARIANTS=0,1,...,9 covers the A/B build
 @pytest.mark.parametrize("variant", [int(v) for v in os.environ.get("RSK_WIRE_VARIANTS", "0").split(",")])
-@pytest.mark.parametrize("path", [1, 2])
-def test_wire_batch(codec, gpu, oracle, eth, layout, pad, mix, variant, path):
+def test_wire_batch(codec, gpu, oracle, eth, layout, pad, mix, variant):
     import torch
-
-    if variant and path == 2:
-        pytest.skip("A/B wire variants run on the per-set path")
 
     if layout == "packed_wire" and pad:
         pytest.skip("back-to-back packets leave no room for the zero pad")
@@ -71,7 +65,6 @@ def test_wire_batch(codec, gpu, oracle, eth, layout, pad, mix, variant, path):
     status = torch.empty(n, dtype=torch.int32, device=gpu)
     if variant:
         codec.set_wire_variant(variant)
-    codec.set_encode_path(path)
     codec.output_wire_batch(dev(payload, gpu), dev(pay_off, gpu, np.int64), dev(plen, gpu, np.int16), dev(cmd, gpu),
                             dev(conv, gpu, np.int32), dev(ckey, gpu, np.int64), dev(src, gpu, np.int32),
                             dev(dst, gpu, np.int32), dev(sp, gpu, np.int16), dev(dp, gpu, np.int16),
@@ -80,8 +73,6 @@ def test_wire_batch(codec, gpu, oracle, eth, layout, pad, mix, variant, path):
                             pad16=pad == 16, pad128=pad == 128)
     if variant:
         codec.set_wire_variant(0)
-    codec.set_encode_path(0)
-    assert codec.last_encode_path == path
     torch.cuda.synchronize()
     got, st = wire.cpu().numpy(), status.cpu().numpy()
     exp = fill.copy()
