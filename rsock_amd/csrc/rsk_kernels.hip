@@ -1128,7 +1128,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(80))) void k
 
 // NT: bit 0 nontemporal loads, bit 1 nontemporal stores (shipped: 3; C3 -1.4 % against 2, and 256-thread
 // blocks against 64 / 512 / 1024: profiles/r04r_two_pass_ab.json).  BS: threads per block (A/B).
-template <int NT, int BS = kBlock>
+// EDGE (A/B): the frame's first and last chunks with normal stores (their lines are shared with the
+// neighbouring frames, written by another wave; L2 can merge the two halves), the rest as NT says.
+template <int NT, int BS = kBlock, bool EDGE = false>
 __global__ __launch_bounds__(BS) void k_encode_copy(EncArgs a, const uint32_t *heads) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -1167,7 +1169,10 @@ __global__ __launch_bounds__(BS) void k_encode_copy(EncArgs a, const uint32_t *h
         const uint4 V = rsk::funnel16(A[q], B[q], g.sh);
         const uint4 v = k < (g.r >= 2u ? 3u : 2u) ? head_chunk(Hj, k, g.r, V) : V;
         if (k >= nst) continue;
-        store_piece<NT>(g.d0 + 16u * k, v, k == 0u ? g.r : 0u, (int)flen - 16 * (int)k, a.pad != 0u);
+        if (EDGE && (k < 8u || k + 8u >= nst))  // the frame's first / last 128 B
+            store_piece<NT & 1>(g.d0 + 16u * k, v, k == 0u ? g.r : 0u, (int)flen - 16 * (int)k, a.pad != 0u);
+        else
+            store_piece<NT>(g.d0 + 16u * k, v, k == 0u ? g.r : 0u, (int)flen - 16 * (int)k, a.pad != 0u);
     }
 }
 
@@ -3472,11 +3477,12 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 // payload-word-specialised schedule (MODE 12, shipped since); 109 / 110 / 111 / 112 = 76 with the header pass
 // held to 80 SGPRs: 1 / 2 packets per lane, generic / word-specialised MD5 (k_encode_heads_ab); 113 / 114 / 115 =
 // 76 with the copy pass in blocks of 512 / 1024 / 64 threads, 116 = 76 with nontemporal loads in the copy;
-// 117 / 118 = the per-set kernel with a per-packet set's frames under 256 / 512 B on the flat list (MODE 13 / 14).
+// 117 / 118 = the per-set kernel with a per-packet set's frames under 256 / 512 B on the flat list (MODE 13 / 14);
+// 119 = 116 with normal stores for each frame's first and last 128 B (k_encode_copy EDGE).
 // v + 1000 * cap (cap 1..8): the same kernel held to `cap` blocks per CU by unused LDS.
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
     const int k = v % 1000;
-    if (!c || v < 0 || v / 1000 > 8 || !(k == 0 || k == 12 || k == 13 || k == 37 || k == 47 || (k >= 50 && k <= 118)))
+    if (!c || v < 0 || v / 1000 > 8 || !(k == 0 || k == 12 || k == 13 || k == 37 || k == 47 || (k >= 50 && k <= 119)))
         return RSK_EINVAL;
     c->enc_variant = v;
     return RSK_OK;
@@ -3729,7 +3735,8 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         case 113:
         case 114:
         case 115:
-        case 116: {
+        case 116:
+        case 119: {
             static uint4 *heads = nullptr;  // A/B only: the two-pass form's header workspace, never freed
             static uint64_t heads_n = 0;
             if (heads_n < n) {
@@ -3762,6 +3769,12 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
                 hipLaunchKernelGGL(hk, dim3(k == 110 || k == 112 ? (grid_for(n) + 1u) / 2u : grid_for(n)), bd, 0, st,
                                    a, c->ks, heads, c->enc_stat_dev);
                 hipLaunchKernelGGL(k_encode_copy<2>, dim3((unsigned)((n + 3ull) / 4ull)), bd, lds, st, a,
+                                   reinterpret_cast<const uint32_t *>(heads));
+                break;
+            }
+            if (k == 119) {  // the copy pass with normal stores for each frame's first and last 128 B
+                hipLaunchKernelGGL(k_encode_heads, dim3(grid_for(n)), bd, 0, st, a, c->ks, heads, c->enc_stat_dev);
+                hipLaunchKernelGGL((k_encode_copy<3, kBlock, true>), dim3((unsigned)((n + 3ull) / 4ull)), bd, 0, st, a,
                                    reinterpret_cast<const uint32_t *>(heads));
                 break;
             }
