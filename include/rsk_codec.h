@@ -205,7 +205,7 @@ typedef struct rsk_encode_out {
 /* frame_i = tag(8) | EncHead(23) | payload(P), written to frame_arena + frame_off[i].
  * Frames must not overlap each other or the payload arena.
  * Two device paths, identical bytes: batches of long frames (>= 16384 packets, the context's last
- * sampled batch at a mean payload >= 1024 B) run a header pass (the MD5 tags 64 to a wave, 32-B
+ * sampled batch at a mean payload >= 960 B) run a header pass (the MD5 tags 64 to a wave, 32-B
  * records in the stream's scratch) and then one wave per packet; other batches run the per-set kernel.
  * The choice reads a host-mapped statistic the previous calls' kernels left (no synchronisation); a
  * call captured into a hipGraph keeps the path it was captured with, and one captured on a stream

@@ -212,9 +212,10 @@ __device__ __forceinline__ void encode_tag(const EncArgs &a, const KeySched &ks,
 constexpr uint32_t kStatValid = 0x80000000u;
 // the two-pass form's batches (enc_path): at least this many packets whose previous batch's sampled
 // mean payload was at least this long (C3's 1400 B take it; C4's mixed lengths, mean ~700 B, and
-// C2's 64 B keep the per-set kernel: one packet per wave idles their lanes, profiles/r04_c3_ceiling.json)
+// C2's 64 B keep the per-set kernel: one packet per wave idles their lanes).  Measured crossover
+// (profiles/r04aa_path_threshold.json): two-pass +6 % at a uniform 900 B, -6.5 % at 1000 B.
 constexpr uint32_t kTwoPassMinPackets = 16384;
-constexpr uint32_t kTwoPassMinPayload = 1024;
+constexpr uint32_t kTwoPassMinPayload = 960;
 [[maybe_unused]] constexpr uint32_t kSampleEvery = 256;  // per-set calls between two samples (k_enc_sample)
 __device__ __forceinline__ void enc_sample(const uint16_t *pay_len, uint32_t n, uint32_t *stat) {
     if (stat == nullptr || blockIdx.x != 0u || threadIdx.x >= 64u) return;
