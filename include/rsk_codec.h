@@ -131,6 +131,19 @@ void rsk_destroy(rsk_ctx *ctx);
 int rsk_set_tag_mode(rsk_ctx *ctx, int mode);
 int rsk_get_tag_mode(const rsk_ctx *ctx);
 
+/* Encode path of this context's rsk_encode_batch calls (outputs are identical):
+ *   RSK_ENC_PATH_AUTO     (default) chosen per call: the two-pass form for batches of >= 16384 packets
+ *                         when the context's last sampled batch had a mean payload >= 960 B, else the
+ *                         per-set kernel (see rsk_encode_batch);
+ *   RSK_ENC_PATH_PER_SET  one kernel, 64 packets per wave (every batch shape);
+ *   RSK_ENC_PATH_TWO_PASS a header pass (MD5 tags 64 to a wave, 32-B records in the stream's scratch),
+ *                         then one wave per packet (batches of long frames).
+ * Read when a call is issued, as the tag mode; RSK_EINVAL for an unknown path. */
+#define RSK_ENC_PATH_AUTO 0
+#define RSK_ENC_PATH_PER_SET 1
+#define RSK_ENC_PATH_TWO_PASS 2
+int rsk_set_encode_path(rsk_ctx *ctx, int path);
+
 /* Streams: a context may be used from several streams at once.  Its device scratch (compaction
  * ballots and look-back state, demux and send-seq tables) is kept per stream, so calls on different streams
  * never share it; calls on ONE stream must be issued in the order the caller wants them to run
@@ -209,7 +222,8 @@ typedef struct rsk_encode_out {
  * records in the stream's scratch) and then one wave per packet; other batches run the per-set kernel.
  * The choice reads a host-mapped statistic the previous calls' kernels left (no synchronisation); a
  * call captured into a hipGraph keeps the path it was captured with, and one captured on a stream
- * without reserved records takes the per-set kernel. */
+ * without reserved records takes the per-set kernel.  rsk_set_encode_path fixes the
+ * path for a context (e.g. one fed alternating long- and short-frame batches). */
 int rsk_encode_batch(rsk_ctx *ctx, uint32_t n, const rsk_encode_in *in, const rsk_encode_out *out,
                      void *stream);
 

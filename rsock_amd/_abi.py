@@ -129,6 +129,7 @@ SIGNATURES = [
     ("rsk_destroy", None, [_vp]),
     ("rsk_set_tag_mode", ctypes.c_int, [_vp, ctypes.c_int]),
     ("rsk_get_tag_mode", ctypes.c_int, [_vp]),
+    ("rsk_set_encode_path", ctypes.c_int, [_vp, ctypes.c_int]),
     ("rsk_reserve", ctypes.c_int, [_vp, ctypes.c_uint32]),
     ("rsk_reserve_stream", ctypes.c_int, [_vp, ctypes.c_uint32, _vp]),
     ("rsk_release_stream", ctypes.c_int, [_vp, _vp]),

@@ -271,12 +271,10 @@ class Codec:
             pass
 
     def set_encode_path(self, path: int) -> None:
-        """Internal knob (tests, tools) for output_batch: 0 = chosen per call from the previous batch's
-        sampled mean payload (default), 1 = the per-set kernel k_encode, 2 = the two-pass form for long
-        frames (k_encode_heads + one wave per packet, k_encode_copy).  Both give identical bytes."""
-        fn = lib().rsk__set_encode_path
-        fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
-        _check(fn(self._ctx, path), "rsk__set_encode_path")
+        """rsk_set_encode_path for output_batch: 0 = chosen per call from the last sampled batch's mean
+        payload (default), 1 = the per-set kernel k_encode, 2 = the two-pass form for long frames
+        (k_encode_heads + one wave per packet, k_encode_copy).  Both give identical bytes."""
+        _check(lib().rsk_set_encode_path(self._ctx, path), "rsk_set_encode_path")
 
     @property
     def last_encode_path(self) -> int:

@@ -32,7 +32,7 @@ struct rsk_ctx {
     int enc_variant = 0;   // see rsk__set_encode_variant (A/B build)
     int wire_variant = 0;  // see rsk__set_wire_variant (A/B build)
     // encode path (rsk_encode_batch): 0 = chosen per call from the previous batch's statistic, 1 = the
-    // per-set kernel, 2 = the two-pass form (rsk__set_encode_path, tests and tools)
+    // per-set kernel, 2 = the two-pass form (rsk_set_encode_path)
     int enc_path = 0;
     std::atomic<int> enc_last_path{0};  // the path the last rsk_encode_batch took (rsk__last_encode_path)
     std::atomic<uint32_t> enc_calls{0};  // per-set encode calls (k_enc_sample cadence)

@@ -3584,10 +3584,10 @@ int rsk_release_stream(rsk_ctx *c, void *stream) {
     return rsk::release_ws(c, (hipStream_t)stream);
 }
 
-// Internal (tests, tools): encode path of this context's calls: 0 = chosen per call (enc_path), 1 = the
-// per-set kernel k_encode, 2 = the two-pass form (k_encode_heads + k_encode_copy).
-int rsk__set_encode_path(rsk_ctx *c, int path) {
-    if (!c || path < 0 || path > 2) return RSK_EINVAL;
+// Encode path of this context's calls (rsk_codec.h): RSK_ENC_PATH_AUTO (chosen per call, enc_path),
+// RSK_ENC_PATH_PER_SET (k_encode), RSK_ENC_PATH_TWO_PASS (k_encode_heads + k_encode_copy).
+int rsk_set_encode_path(rsk_ctx *c, int path) {
+    if (!c || path < RSK_ENC_PATH_AUTO || path > RSK_ENC_PATH_TWO_PASS) return RSK_EINVAL;
     c->enc_path = path;
     return RSK_OK;
 }
@@ -3643,7 +3643,7 @@ int rsk_reserve_stream(rsk_ctx *c, uint32_t n_max, void *stream) {
     return rsk::stream_ws(c, (hipStream_t)stream, rsk::WS_ENC, 32ull * n_max, &p);
 }
 
-// Encode path per call: the context's forced path (rsk__set_encode_path), else the two-pass form for
+// Encode path per call: the context's forced path (rsk_set_encode_path), else the two-pass form for
 // batches of at least kTwoPassMinPackets when the context's last sampled batch (enc_sample: every
 // two-pass call, and k_enc_sample behind the first and every kSampleEvery-th per-set call) had a mean
 // payload of at least kTwoPassMinPayload bytes, else the per-set kernel.  The first call on a context

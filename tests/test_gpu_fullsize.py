@@ -32,7 +32,7 @@ def _le_bytes(x, nbytes):
 
 @pytest.fixture(params=[1, 2], ids=lambda p: f"path{p}")
 def pcodec(request, codec):
-    """The codec held to one encode path (rsk__set_encode_path): 1 = k_encode, 2 = the two-pass form."""
+    """The codec held to one encode path (rsk_set_encode_path): 1 = k_encode, 2 = the two-pass form."""
     codec.set_encode_path(request.param)
     yield codec
     codec.set_encode_path(0)

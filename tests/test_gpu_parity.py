@@ -116,7 +116,7 @@ def _rand_fields(rng, n):
 ENC_VARIANTS = [int(v) for v in os.environ.get("RSK_ENC_VARIANTS", "0").split(",")]
 
 
-# the shipped library's two encode paths (rsk__set_encode_path): 1 = the per-set kernel k_encode, 2 = the
+# the shipped library's two encode paths (rsk_set_encode_path): 1 = the per-set kernel k_encode, 2 = the
 # two-pass form for long frames (k_encode_heads + one wave per packet); in normal use the library picks
 # one per call from the previous batch's mean payload, so every encode test runs both explicitly
 ENC_PATHS = (1, 2)

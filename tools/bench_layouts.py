@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--pad16", action="store_true", help="RSK_ENC_ZERO_PAD16 (not for the byte-packed layout)")
     ap.add_argument("--encode-path", type=int, default=0,
-                    help="rsk__set_encode_path: 0 chosen per call, 1 per-set kernel, 2 two-pass")
+                    help="rsk_set_encode_path: 0 chosen per call, 1 per-set kernel, 2 two-pass")
     args = ap.parse_args()
     import torch
 

@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--wire-variants", default="", help="also time these rsk__set_wire_variant values (A/B)")
     ap.add_argument("--only", default="", help="time only these paths (comma list), e.g. demux,demux_64conn")
     ap.add_argument("--encode-path", type=int, default=0,
-                    help="rsk__set_encode_path for the encode paths: 0 chosen per call, 1 k_encode, 2 two-pass")
+                    help="rsk_set_encode_path for the encode paths: 0 chosen per call, 1 k_encode, 2 two-pass")
     args = ap.parse_args()
     import torch
 

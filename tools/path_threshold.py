@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Where the two-pass encode starts to pay (rsk_encode_batch's kTwoPassMinPayload): encode time of
-both paths (rsk__set_encode_path 1 = per-set kernel, 2 = two-pass) on synthetic batches of uniform
+both paths (rsk_set_encode_path 1 = per-set kernel, 2 = two-pass) on synthetic batches of uniform
 and mixed payload lengths, device-resident, HIP events, interleaved rounds in one process.  Frames
 of both paths are compared byte for byte before timing.
     python tools/path_threshold.py [--packets 2097152] [--rounds 4] [--reps 5]"""
