@@ -132,16 +132,19 @@ int rsk_set_tag_mode(rsk_ctx *ctx, int mode);
 int rsk_get_tag_mode(const rsk_ctx *ctx);
 
 /* Encode path of this context's rsk_encode_batch calls (outputs are identical):
- *   RSK_ENC_PATH_AUTO     (default) chosen per call: the two-pass form for batches of >= 16384 packets
- *                         when the context's last sampled batch had a mean payload >= 960 B, else the
- *                         per-set kernel (see rsk_encode_batch);
+ *   RSK_ENC_PATH_AUTO     (default) chosen per call from the context's last sampled batch (>= 16384
+ *                         packets): mean payload >= 960 B the two-pass form, <= 160 B the short-frame
+ *                         kernel, else the per-set kernel (see rsk_encode_batch);
  *   RSK_ENC_PATH_PER_SET  one kernel, 64 packets per wave (every batch shape);
  *   RSK_ENC_PATH_TWO_PASS a header pass (MD5 tags 64 to a wave, 32-B records in the stream's scratch),
- *                         then one wave per packet (batches of long frames).
+ *                         then one wave per packet (batches of long frames);
+ *   RSK_ENC_PATH_SHORT    the per-set kernel with every set on the flat chunk list (batches of short
+ *                         frames; AUTO takes it when the last sampled mean payload is <= 160 B).
  * Read when a call is issued, as the tag mode; RSK_EINVAL for an unknown path. */
 #define RSK_ENC_PATH_AUTO 0
 #define RSK_ENC_PATH_PER_SET 1
 #define RSK_ENC_PATH_TWO_PASS 2
+#define RSK_ENC_PATH_SHORT 3
 int rsk_set_encode_path(rsk_ctx *ctx, int path);
 
 /* Streams: a context may be used from several streams at once.  Its device scratch (compaction

@@ -217,6 +217,9 @@ constexpr uint32_t kStatValid = 0x80000000u;
 constexpr uint32_t kTwoPassMinPackets = 16384;
 constexpr uint32_t kTwoPassMinPayload = 960;
 [[maybe_unused]] constexpr uint32_t kSampleEvery = 256;  // per-set calls between two samples (k_enc_sample)
+// batches whose sampled mean payload is at most this take the flat-only per-set kernel (RSK_ENC_PATH_SHORT):
+// every set of such a batch has a mean frame under the flat path's 256 B (kFlatBelowMeanBytes) anyway
+[[maybe_unused]] constexpr uint32_t kFlatMaxPayload = 160;
 __device__ __forceinline__ void enc_sample(const uint16_t *pay_len, uint32_t n, uint32_t *stat) {
     if (stat == nullptr || blockIdx.x != 0u || threadIdx.x >= 64u) return;
     uint32_t v = pay_len[((uint64_t)threadIdx.x * n) >> 6];
@@ -847,13 +850,15 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
 #pragma unroll
     for (int off = 32; off; off >>= 1) fl += __shfl_xor(fl, off);
     const uint32_t cnt = (uint32_t)__popcll(vm);
-    const bool flat = MODE == 7 ? true : MODE == 8 ? false : fl < kFlatBelowMeanBytes * cnt;
+    // MODE 16 (A/B): 12 with every set on the flat list (a launch for batches of short frames only: the
+    // per-packet path's registers out of the kernel)
+    const bool flat = MODE == 7 || MODE == 16 ? true : MODE == 8 ? false : fl < kFlatBelowMeanBytes * cnt;
     // MODE 10 (A/B): as 9 with the tag in the copy loop for every per-packet set
     const bool defer = MODE != 3 && MODE != 7 && !flat && (MODE == 10 || fl >= kDeferTagMeanBytes * cnt);
     // MODE 11 (shipped): as 9 with the flat sets' tag and header stores behind the first chunk loads;
     // MODE 12 (A/B): 11 with the flat sets' MD5 on the payload-word-specialised schedule (md5_tag_lane)
     // MODE 13 / 14 (A/B): 12 with the frames under 256 / 512 B of a per-packet set on the flat list
-    constexpr bool kFlatTagQ = MODE == 11 || MODE == 12 || MODE == 13 || MODE == 14;
+    constexpr bool kFlatTagQ = MODE == 11 || MODE == 12 || MODE == 13 || MODE == 14 || MODE == 16;
     if constexpr (MODE != 3 && MODE != 7) {  // the tag now, except for the sets whose copy loop takes it
         if (!defer && !(kFlatTagQ && flat)) encode_tag(a, ks, L);
     }
@@ -862,6 +867,7 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
         copy_flat<U, kFlatTagQ, MODE >= 12>(a, ks, L, lane, vec, recs, cend);
         return;
     }
+    if constexpr (MODE == 16) return;  // flat only
     bool nt = NT == 2;
     if constexpr (NT < 0) {
         // Store policy per set: frames packed back to back (each frame's padded end is the next
@@ -3479,11 +3485,13 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 // held to 80 SGPRs: 1 / 2 packets per lane, generic / word-specialised MD5 (k_encode_heads_ab); 113 / 114 / 115 =
 // 76 with the copy pass in blocks of 512 / 1024 / 64 threads, 116 = 76 with nontemporal loads in the copy;
 // 117 / 118 = the per-set kernel with a per-packet set's frames under 256 / 512 B on the flat list (MODE 13 / 14);
-// 119 = 116 with normal stores for each frame's first and last 128 B (k_encode_copy EDGE).
+// 119 = 116 with normal stores for each frame's first and last 128 B (k_encode_copy EDGE); 120 / 121 / 122 =
+// the per-set kernel with every set on the flat list (MODE 16, flat copy unroll U 4 / 2 / 8; 121 shipped as
+// RSK_ENC_PATH_SHORT).
 // v + 1000 * cap (cap 1..8): the same kernel held to `cap` blocks per CU by unused LDS.
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
     const int k = v % 1000;
-    if (!c || v < 0 || v / 1000 > 8 || !(k == 0 || k == 12 || k == 13 || k == 37 || k == 47 || (k >= 50 && k <= 119)))
+    if (!c || v < 0 || v / 1000 > 8 || !(k == 0 || k == 12 || k == 13 || k == 37 || k == 47 || (k >= 50 && k <= 122)))
         return RSK_EINVAL;
     c->enc_variant = v;
     return RSK_OK;
@@ -3587,7 +3595,7 @@ int rsk_release_stream(rsk_ctx *c, void *stream) {
 // Encode path of this context's calls (rsk_codec.h): RSK_ENC_PATH_AUTO (chosen per call, enc_path),
 // RSK_ENC_PATH_PER_SET (k_encode), RSK_ENC_PATH_TWO_PASS (k_encode_heads + k_encode_copy).
 int rsk_set_encode_path(rsk_ctx *c, int path) {
-    if (!c || path < RSK_ENC_PATH_AUTO || path > RSK_ENC_PATH_TWO_PASS) return RSK_EINVAL;
+    if (!c || path < RSK_ENC_PATH_AUTO || path > RSK_ENC_PATH_SHORT) return RSK_EINVAL;
     c->enc_path = path;
     return RSK_OK;
 }
@@ -3651,7 +3659,11 @@ int rsk_reserve_stream(rsk_ctx *c, uint32_t n_max, void *stream) {
 [[maybe_unused]] static int enc_path(rsk_ctx *c, uint32_t n) {
     if (c->enc_path) return c->enc_path;
     const uint32_t s = c->enc_stat_host ? __atomic_load_n(c->enc_stat_host, __ATOMIC_RELAXED) : 0u;
-    return n >= kTwoPassMinPackets && (s & kStatValid) && (s & ~kStatValid) >= kTwoPassMinPayload ? 2 : 1;
+    if (n < kTwoPassMinPackets || !(s & kStatValid)) return RSK_ENC_PATH_PER_SET;
+    const uint32_t mean = s & ~kStatValid;
+    return mean >= kTwoPassMinPayload ? RSK_ENC_PATH_TWO_PASS
+           : mean <= kFlatMaxPayload  ? RSK_ENC_PATH_SHORT
+                                      : RSK_ENC_PATH_PER_SET;
 }
 
 int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_encode_out *out,
@@ -3839,12 +3851,16 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         }
         case 108: hipLaunchKernelGGL((k_encode<12, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
         case 117: hipLaunchKernelGGL((k_encode<13, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
+        case 120: hipLaunchKernelGGL((k_encode<16, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
+        case 121: hipLaunchKernelGGL((k_encode<16, 4, 2, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
+        case 122: hipLaunchKernelGGL((k_encode<16, 4, 8, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
         case 118: hipLaunchKernelGGL((k_encode<14, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
         default: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
     }
 #else
     (void)gd;
-    if (enc_path(c, n) == 2) {
+    const int path = enc_path(c, n);
+    if (path == RSK_ENC_PATH_TWO_PASS) {
         // the two-pass form (batches of long frames): header records, then one wave per packet
         void *hp = nullptr;
         if (rsk::stream_ws_if(c, st, rsk::WS_ENC, 32ull * n, &hp) == RSK_OK) {
@@ -3857,11 +3873,18 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         }
         g_last_error[0] = 0;  // no records (a capture that would grow them, or no memory): one pass
     }
-    // the per-set kernel: per-wave hybrid (flat chunk list for short frames, with the tag behind the
-    // first chunk loads; software-pipelined one-load DPP per-packet copy, 4 packets per batch, for
-    // the rest), tag in the copy loop for long-frame sets, per-set store policy
-    hipLaunchKernelGGL((k_encode<12, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, 0, st, a, c->ks);
-    c->enc_last_path.store(1, std::memory_order_relaxed);
+    if (path == RSK_ENC_PATH_SHORT) {
+        // batches of short frames: the per-set kernel with every set on the flat chunk list, compiled
+        // without the per-packet copy (83 VGPRs, 6 waves per SIMD instead of 4; C2 -3 %)
+        hipLaunchKernelGGL((k_encode<16, 4, 2, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, 0, st, a, c->ks);
+        c->enc_last_path.store(RSK_ENC_PATH_SHORT, std::memory_order_relaxed);
+    } else {
+        // the per-set kernel: per-wave hybrid (flat chunk list for short frames, with the tag behind the
+        // first chunk loads; software-pipelined one-load DPP per-packet copy, 4 packets per batch, for
+        // the rest), tag in the copy loop for long-frame sets, per-set store policy
+        hipLaunchKernelGGL((k_encode<12, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, 0, st, a, c->ks);
+        c->enc_last_path.store(RSK_ENC_PATH_PER_SET, std::memory_order_relaxed);
+    }
     // the statistic for later calls: with no valid value yet, and every kSampleEvery-th call, unless the
     // call is being captured (a graph replays its path as captured)
     if (c->enc_path == 0 && c->enc_stat_dev && n >= kTwoPassMinPackets && !rsk::capturing(st)) {

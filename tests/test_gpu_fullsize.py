@@ -30,9 +30,10 @@ def _le_bytes(x, nbytes):
     return torch.stack([(x >> (8 * k)) & 0xFF for k in range(nbytes)], dim=1).to(torch.uint8)
 
 
-@pytest.fixture(params=[1, 2], ids=lambda p: f"path{p}")
+@pytest.fixture(params=[1, 2, 3], ids=lambda p: f"path{p}")
 def pcodec(request, codec):
-    """The codec held to one encode path (rsk_set_encode_path): 1 = k_encode, 2 = the two-pass form."""
+    """The codec held to one encode path (rsk_set_encode_path): 1 = k_encode, 2 = the two-pass form,
+    3 = every set on the flat chunk list."""
     codec.set_encode_path(request.param)
     yield codec
     codec.set_encode_path(0)
@@ -54,7 +55,7 @@ def test_encode_path_choice(codec, gpu):
         d = workload.describe(cfg, 0, 40_000, n=40_000)
         w = workload.DeviceWorkload(d, gpu)
         frames = []
-        for path in (1, 0, 0, 2):
+        for path in (1, 0, 0, 2, 3):
             codec.set_encode_path(path)
             w.frame.zero_()
             codec.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame,

@@ -116,10 +116,11 @@ def _rand_fields(rng, n):
 ENC_VARIANTS = [int(v) for v in os.environ.get("RSK_ENC_VARIANTS", "0").split(",")]
 
 
-# the shipped library's two encode paths (rsk_set_encode_path): 1 = the per-set kernel k_encode, 2 = the
-# two-pass form for long frames (k_encode_heads + one wave per packet); in normal use the library picks
-# one per call from the previous batch's mean payload, so every encode test runs both explicitly
-ENC_PATHS = (1, 2)
+# the shipped library's encode paths (rsk_set_encode_path): 1 = the per-set kernel k_encode, 2 = the
+# two-pass form for long frames (k_encode_heads + one wave per packet), 3 = the per-set kernel with every
+# set on the flat chunk list (short frames); in normal use the library picks one per call from the last
+# sampled batch's mean payload, so every encode test runs each explicitly
+ENC_PATHS = (1, 2, 3)
 
 
 @pytest.fixture(params=[(v, p) for v in ENC_VARIANTS for p in (ENC_PATHS if v == 0 else (0,))],
