@@ -854,11 +854,13 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
     // per-packet path's registers out of the kernel)
     const bool flat = MODE == 7 || MODE == 16 ? true : MODE == 8 ? false : fl < kFlatBelowMeanBytes * cnt;
     // MODE 10 (A/B): as 9 with the tag in the copy loop for every per-packet set
-    const bool defer = MODE != 3 && MODE != 7 && !flat && (MODE == 10 || fl >= kDeferTagMeanBytes * cnt);
+    // MODE 18 (A/B): 12 without the TAG form (the tag in phase 1 for every set: a build for mid-length
+    // batches, without the long-frame copy's registers)
+    const bool defer = MODE != 3 && MODE != 7 && MODE != 18 && !flat && (MODE == 10 || fl >= kDeferTagMeanBytes * cnt);
     // MODE 11 (shipped): as 9 with the flat sets' tag and header stores behind the first chunk loads;
     // MODE 12 (A/B): 11 with the flat sets' MD5 on the payload-word-specialised schedule (md5_tag_lane)
     // MODE 13 / 14 (A/B): 12 with the frames under 256 / 512 B of a per-packet set on the flat list
-    constexpr bool kFlatTagQ = MODE == 11 || MODE == 12 || MODE == 13 || MODE == 14 || MODE == 16;
+    constexpr bool kFlatTagQ = MODE == 11 || MODE == 12 || MODE == 13 || MODE == 14 || MODE == 16 || MODE == 18;
     if constexpr (MODE != 3 && MODE != 7) {  // the tag now, except for the sets whose copy loop takes it
         if (!defer && !(kFlatTagQ && flat)) encode_tag(a, ks, L);
     }
@@ -903,10 +905,12 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
             mrg = __ballot(vec && nvec && lane % GRP != GRP - 1u && (fe & 15u) != 0u &&
                            reinterpret_cast<uintptr_t>(a.frame + nfo) == fe) != 0ull;
         }
-        if (defer) {
-            if (mrg) copy_pkt_pipe<PU, 0, true, TG, true>(a, ks, L, lane, vm);
-            else if (nt) copy_pkt_pipe<PU, 2, true, TG>(a, ks, L, lane, vm);
-            else copy_pkt_pipe<PU, 0, true, TG>(a, ks, L, lane, vm);
+        if (MODE != 18 && defer) {
+            if constexpr (MODE != 18) {
+                if (mrg) copy_pkt_pipe<PU, 0, true, TG, true>(a, ks, L, lane, vm);
+                else if (nt) copy_pkt_pipe<PU, 2, true, TG>(a, ks, L, lane, vm);
+                else copy_pkt_pipe<PU, 0, true, TG>(a, ks, L, lane, vm);
+            }
         } else {
             uint64_t pm = vm;
             if constexpr (MODE == 13 || MODE == 14) {  // the set's short frames on the flat list first
@@ -3487,11 +3491,11 @@ const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 // 117 / 118 = the per-set kernel with a per-packet set's frames under 256 / 512 B on the flat list (MODE 13 / 14);
 // 119 = 116 with normal stores for each frame's first and last 128 B (k_encode_copy EDGE); 120 / 121 / 122 =
 // the per-set kernel with every set on the flat list (MODE 16, flat copy unroll U 4 / 2 / 8; 121 shipped as
-// RSK_ENC_PATH_SHORT).
+// RSK_ENC_PATH_SHORT); 123 = MODE 18 (12 without the TAG form).
 // v + 1000 * cap (cap 1..8): the same kernel held to `cap` blocks per CU by unused LDS.
 int rsk__set_encode_variant(rsk_ctx *c, int v) {
     const int k = v % 1000;
-    if (!c || v < 0 || v / 1000 > 8 || !(k == 0 || k == 12 || k == 13 || k == 37 || k == 47 || (k >= 50 && k <= 122)))
+    if (!c || v < 0 || v / 1000 > 8 || !(k == 0 || k == 12 || k == 13 || k == 37 || k == 47 || (k >= 50 && k <= 123)))
         return RSK_EINVAL;
     c->enc_variant = v;
     return RSK_OK;
@@ -3852,6 +3856,7 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         case 108: hipLaunchKernelGGL((k_encode<12, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
         case 117: hipLaunchKernelGGL((k_encode<13, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
         case 120: hipLaunchKernelGGL((k_encode<16, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
+        case 123: hipLaunchKernelGGL((k_encode<18, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
         case 121: hipLaunchKernelGGL((k_encode<16, 4, 2, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
         case 122: hipLaunchKernelGGL((k_encode<16, 4, 8, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
         case 118: hipLaunchKernelGGL((k_encode<14, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
