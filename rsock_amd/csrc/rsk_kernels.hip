@@ -852,7 +852,7 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
     const uint32_t cnt = (uint32_t)__popcll(vm);
     // MODE 16 (A/B): 12 with every set on the flat list (a launch for batches of short frames only: the
     // per-packet path's registers out of the kernel)
-    const bool flat = MODE == 7 || MODE == 16 ? true : MODE == 8 ? false : fl < kFlatBelowMeanBytes * cnt;
+    const bool flat = MODE == 7 || MODE == 16 || MODE == 19 ? true : MODE == 8 ? false : fl < kFlatBelowMeanBytes * cnt;
     // MODE 10 (A/B): as 9 with the tag in the copy loop for every per-packet set
     // MODE 18 (A/B): 12 without the TAG form (the tag in phase 1 for every set: a build for mid-length
     // batches, without the long-frame copy's registers)
@@ -860,16 +860,17 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
     // MODE 11 (shipped): as 9 with the flat sets' tag and header stores behind the first chunk loads;
     // MODE 12 (A/B): 11 with the flat sets' MD5 on the payload-word-specialised schedule (md5_tag_lane)
     // MODE 13 / 14 (A/B): 12 with the frames under 256 / 512 B of a per-packet set on the flat list
-    constexpr bool kFlatTagQ = MODE == 11 || MODE == 12 || MODE == 13 || MODE == 14 || MODE == 16 || MODE == 18;
+    constexpr bool kFlatTagQ = MODE == 11 || MODE == 12 || MODE == 13 || MODE == 14 || MODE == 16 || MODE == 18 ||
+                               MODE == 19;
     if constexpr (MODE != 3 && MODE != 7) {  // the tag now, except for the sets whose copy loop takes it
         if (!defer && !(kFlatTagQ && flat)) encode_tag(a, ks, L);
     }
     if (flat) {
         if (!kFlatTagQ && vec) store_head(L.H, a.frame + L.fo);
-        copy_flat<U, kFlatTagQ, MODE >= 12>(a, ks, L, lane, vec, recs, cend);
+        copy_flat<U, kFlatTagQ, MODE >= 12 && MODE != 19>(a, ks, L, lane, vec, recs, cend);
         return;
     }
-    if constexpr (MODE == 16) return;  // flat only
+    if constexpr (MODE == 16 || MODE == 19) return;  // flat only (19: with the generic MD5 schedule)
     bool nt = NT == 2;
     if constexpr (NT < 0) {
         // Store policy per set: frames packed back to back (each frame's padded end is the next
@@ -3880,8 +3881,8 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
     }
     if (path == RSK_ENC_PATH_SHORT) {
         // batches of short frames: the per-set kernel with every set on the flat chunk list, compiled
-        // without the per-packet copy (83 VGPRs, 6 waves per SIMD instead of 4; C2 -3 %)
-        hipLaunchKernelGGL((k_encode<16, 4, 2, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, 0, st, a, c->ks);
+        // without the per-packet copy (fewer VGPRs, more waves per SIMD; profiles/r04ac_short_path.json)
+        hipLaunchKernelGGL((k_encode<19, 4, 2, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, 0, st, a, c->ks);
         c->enc_last_path.store(RSK_ENC_PATH_SHORT, std::memory_order_relaxed);
     } else {
         // the per-set kernel: per-wave hybrid (flat chunk list for short frames, with the tag behind the
