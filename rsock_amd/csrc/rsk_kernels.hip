@@ -215,6 +215,7 @@ constexpr uint32_t kStatValid = 0x80000000u;
 // C2's 64 B keep the per-set kernel: one packet per wave idles their lanes).  Measured crossover
 // (profiles/r04aa_path_threshold.json): two-pass +6 % at a uniform 900 B, -6.5 % at 1000 B.
 constexpr uint32_t kTwoPassMinPackets = 16384;
+constexpr uint64_t kCopyMaxPackets = 1ull << 25;  // per k_encode_copy launch (2^31 work-items)
 constexpr uint32_t kTwoPassMinPayload = 960;
 [[maybe_unused]] constexpr uint32_t kSampleEvery = 256;  // per-set calls between two samples (k_enc_sample)
 // batches whose sampled mean payload is at most this take the flat-only per-set kernel (RSK_ENC_PATH_SHORT):
@@ -1142,11 +1143,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(80))) void k
 // blocks against 64 / 512 / 1024: profiles/r04r_two_pass_ab.json).  BS: threads per block (A/B).
 // EDGE (A/B): the frame's first and last chunks with normal stores (their lines are shared with the
 // neighbouring frames, written by another wave; L2 can merge the two halves), the rest as NT says.
+// base: the launch's first packet (a grid is limited to 2^32 - 1 work-items, i.e. 2^26 packets at 64
+// per packet: larger batches take several launches, kCopyMaxPackets each).
 template <int NT, int BS = kBlock, bool EDGE = false>
-__global__ __launch_bounds__(BS) void k_encode_copy(EncArgs a, const uint32_t *heads) {
+__global__ __launch_bounds__(BS) void k_encode_copy(EncArgs a, const uint32_t *heads, uint64_t base = 0) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const uint64_t i = (uint64_t)blockIdx.x * (BS / 64) + w;
+    const uint64_t i = base + (uint64_t)blockIdx.x * (BS / 64) + w;
     if (i >= a.n) return;
     const uint32_t P = a.pay_len[i];  // uniform address, read-only in this launch: scalar loads
     if (P == 0u || P > (uint32_t)RSK_MAX_PAYLOAD) return;  // status written by pass 1
@@ -3872,8 +3875,11 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         if (rsk::stream_ws_if(c, st, rsk::WS_ENC, 32ull * n, &hp) == RSK_OK) {
             hipLaunchKernelGGL(k_encode_heads, dim3(grid_for(n)), bd, 0, st, a, c->ks, static_cast<uint4 *>(hp),
                                c->enc_stat_dev);
-            hipLaunchKernelGGL(k_encode_copy<3>, dim3((unsigned)((n + 3ull) / 4ull)), bd, 0, st, a,
-                               static_cast<const uint32_t *>(hp));
+            for (uint64_t b0 = 0; b0 < n; b0 += kCopyMaxPackets) {  // one launch up to 2^25 packets
+                const uint64_t m = n - b0 < kCopyMaxPackets ? n - b0 : kCopyMaxPackets;
+                hipLaunchKernelGGL(k_encode_copy<3>, dim3((unsigned)((m + 3ull) / 4ull)), bd, 0, st, a,
+                                   static_cast<const uint32_t *>(hp), b0);
+            }
             c->enc_last_path.store(2, std::memory_order_relaxed);
             return launch_check("k_encode_heads / k_encode_copy");
         }

@@ -163,3 +163,24 @@ def test_compaction_large_random(codec, gpu, oracle):
     assert nv == exp.numel()
     assert torch.equal(out.valid_idx[:nv], exp)
     assert torch.equal(out.status == 1, valid)
+
+
+def test_two_pass_beyond_one_launch(codec, gpu):
+    """A batch past one copy launch (2^25 packets per k_encode_copy launch: a grid holds at most 2^32 - 1
+    work-items, 64 per packet) takes several launches; its frames equal the per-set kernel's."""
+    import torch
+
+    n = (1 << 25) + 4097
+    d = workload.describe("c2", 0, n, n=n)
+    w = workload.DeviceWorkload(d, gpu)
+    frames = []
+    for path in (1, 2):
+        codec.set_encode_path(path)
+        w.frame.zero_()
+        codec.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
+                           w.status, id_uniform=workload.ID_UNIFORM, pad16=True)
+        torch.cuda.synchronize()
+        assert codec.last_encode_path == path
+        frames.append(w.frame.clone())
+    codec.set_encode_path(0)
+    assert torch.equal(frames[0], frames[1])
