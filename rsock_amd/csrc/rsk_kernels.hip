@@ -215,7 +215,7 @@ constexpr uint32_t kStatValid = 0x80000000u;
 // C2's 64 B keep the per-set kernel: one packet per wave idles their lanes).  Measured crossover
 // (profiles/r04aa_path_threshold.json): two-pass +6 % at a uniform 900 B, -6.5 % at 1000 B.
 constexpr uint32_t kTwoPassMinPackets = 16384;
-constexpr uint64_t kCopyMaxPackets = 1ull << 25;  // per k_encode_copy launch (2^31 work-items)
+[[maybe_unused]] constexpr uint64_t kCopyMaxPackets = 1ull << 25;  // per k_encode_copy launch (2^31 work-items)
 constexpr uint32_t kTwoPassMinPayload = 960;
 [[maybe_unused]] constexpr uint32_t kSampleEvery = 256;  // per-set calls between two samples (k_enc_sample)
 // batches whose sampled mean payload is at most this take the flat-only per-set kernel (RSK_ENC_PATH_SHORT):
