@@ -10,7 +10,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# RSK_LIB selects another in-tree build of the same library (tools: librsk_ab.so, the A/B build)
+# RSK_LIB selects another in-tree build of the same library (tools: a saved copy of an earlier build,
+# for an A/B between builds in separate processes)
 LIB_PATH = os.path.join(_HERE, os.environ.get("RSK_LIB", "librsk.so"))
 
 # ---- constants (include/rsk_codec.h) ------------------------------------------------------------
@@ -28,6 +29,7 @@ DLT_NULL, DLT_EN10MB = 0, 1
 
 OK, EINVAL, ENOMEM, EDEVICE = 0, -22, -12, -5
 SEND_OVERSIZE, SEND_RESET = -1, 0
+MAX_BATCH = 0xFFFF0000
 RECV_VALID, RECV_CLOSE, RECV_DROP = 1, 0, -1
 PARSE_DROP, PARSE_DELIVER, PARSE_SYN, PARSE_MALFORMED, PARSE_SLOT_SHORT = 0, 1, 2, 3, 4
 CAP_SLOT_MIN = 64
@@ -60,6 +62,7 @@ class EncodeOut(ctypes.Structure):
 
 ENC_ZERO_PAD16 = 0x1
 ENC_ZERO_PAD128 = 0x2
+ENC_PATH_AUTO, ENC_PATH_PER_SET, ENC_PATH_TWO_PASS, ENC_PATH_SHORT, ENC_PATH_FUSED = 0, 1, 2, 3, 4
 
 
 class WireIn(ctypes.Structure):

@@ -48,15 +48,6 @@ class RskError(RuntimeError):
     pass
 
 
-def _ab_fn(name: str):
-    try:
-        fn = getattr(lib(), name)
-    except AttributeError:
-        raise RskError(f"{name}: A/B knob of the tools build only (make -C rsock_amd ab; RSK_LIB=librsk_ab.so)")
-    fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    return fn
-
-
 def _check(rc: int, what: str) -> None:
     if rc != 0:
         err = lib().rsk_last_error()
@@ -249,8 +240,7 @@ class Codec:
         self.set_tag_mode(tag_mode)
 
     def set_tag_mode(self, mode) -> None:
-        """rsk_set_tag_mode: "md5" / "table" (or the RSK_TAG_* value; the A/B build also takes 2, the
-        MD5 with its round constants staged in LDS)."""
+        """rsk_set_tag_mode: "md5" / "table" (or the RSK_TAG_* value)."""
         m = TAG_MODES[mode] if isinstance(mode, str) else int(mode)
         _check(lib().rsk_set_tag_mode(self._ctx, m), "rsk_set_tag_mode")
 
@@ -273,27 +263,25 @@ class Codec:
     def set_encode_path(self, path: int) -> None:
         """rsk_set_encode_path for output_batch: 0 = chosen per call from the last sampled batch's mean
         payload (default), 1 = the per-set kernel k_encode, 2 = the two-pass form for long frames
-        (k_encode_heads + one wave per packet, k_encode_copy).  Both give identical bytes."""
+        (k_encode_heads + one wave per packet, k_encode_copy), 3 = the short-frame kernel (k_encode
+        with every set on the flat chunk list), 4 = the fused form (k_encode_fused: header waves beside
+        copy waves of 1 / 2 / 4 packets, one launch).  Every path gives identical bytes."""
         _check(lib().rsk_set_encode_path(self._ctx, path), "rsk_set_encode_path")
 
     @property
     def last_encode_path(self) -> int:
-        """The path the last output_batch took: 1 = k_encode, 2 = the two-pass form (0 before any)."""
+        """The path the last output_batch took (1 .. 4 as set_encode_path; 0 before any)."""
         fn = lib().rsk__last_encode_path
         fn.argtypes = [ctypes.c_void_p]
         return int(fn(self._ctx))
 
-    def set_encode_variant(self, v: int) -> None:
-        """A/B build only (RSK_LIB=librsk_ab.so, `make -C rsock_amd ab`): selects a k_encode variant
-        for in-process A/B runs (tools/ab_encode.py; the list is in rsk_kernels.hip).  The shipped
-        librsk.so has two encode paths (set_encode_path) and no such knob."""
-        fn = _ab_fn("rsk__set_encode_variant")
-        _check(fn(self._ctx, v), "rsk__set_encode_variant")
-
-    def set_wire_variant(self, v: int) -> None:
-        """A/B build only, as set_encode_variant, for k_encode_wire (tools/bench_paths.py)."""
-        fn = _ab_fn("rsk__set_wire_variant")
-        _check(fn(self._ctx, v), "rsk__set_wire_variant")
+    def set_fused(self, k: int = 0, nt: int = 3) -> None:
+        """Internal knob of the fused encode path (rsk__set_fused): k packets per copy wave (1, 2, 4; 0 =
+        chosen from the last sampled mean payload) and the copy waves' store policy nt (bit 0
+        nontemporal loads, bit 1 nontemporal stores; 0, 2 or 3)."""
+        fn = lib().rsk__set_fused
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        _check(fn(self._ctx, k, nt), "rsk__set_fused")
 
     def set_send_seq_groupby(self, v: int) -> None:
         """Internal knob for rsk_tcp_send_seq_batch: 0 the per-tile table path when n_conn < 2048

@@ -29,13 +29,14 @@ struct WsBuf {
 
 struct rsk_ctx {
     int device = 0;
-    int enc_variant = 0;   // see rsk__set_encode_variant (A/B build)
-    int wire_variant = 0;  // see rsk__set_wire_variant (A/B build)
-    // encode path (rsk_encode_batch): 0 = chosen per call from the previous batch's statistic, 1 = the
-    // per-set kernel, 2 = the two-pass form (rsk_set_encode_path)
+    // encode path (rsk_encode_batch): 0 = chosen per call from the previous batch's statistic, else
+    // RSK_ENC_PATH_* (rsk_set_encode_path)
     int enc_path = 0;
+    int fused_k = 0, fused_nt = 3;  // the fused form's packets per copy wave / store policy (rsk__set_fused)
     std::atomic<int> enc_last_path{0};  // the path the last rsk_encode_batch took (rsk__last_encode_path)
-    std::atomic<uint32_t> enc_calls{0};  // per-set encode calls (k_enc_sample cadence)
+    // set once any call of this context was captured into a graph: its replays may run on streams the
+    // context never saw, so rsk_check_device_errors waits for the device instead of its streams
+    std::atomic<bool> captured{false};
     // host-mapped word the batch statistic is stored to (enc_sample: k_encode_heads, k_enc_sample) and
     // its device address; read without synchronisation by later calls (a stale value only picks the
     // slower path, never different bytes)
@@ -108,6 +109,7 @@ inline bool capturing(hipStream_t s) {
 // being captured (RSK_EINVAL: reserve before the capture, rsk_codec.h).
 inline int stream_ws(rsk_ctx *c, hipStream_t s, int kind, size_t need, void **out) {
     std::lock_guard<std::mutex> lk(c->ws_mu);
+    if (capturing(s)) c->captured.store(true, std::memory_order_relaxed);
     WsBuf &b = c->ws[s][kind];
     if (!b.p || b.bytes < need) {
         if (capturing(s)) {
@@ -135,6 +137,7 @@ inline int stream_ws(rsk_ctx *c, hipStream_t s, int kind, size_t need, void **ou
 // (RSK_EINVAL, no error text): for scratch whose caller has a path that needs none.
 inline int stream_ws_if(rsk_ctx *c, hipStream_t s, int kind, size_t need, void **out) {
     if (capturing(s)) {
+        c->captured.store(true, std::memory_order_relaxed);
         std::lock_guard<std::mutex> lk(c->ws_mu);
         auto it = c->ws.find(s);
         if (it == c->ws.end() || !it->second[kind].p || it->second[kind].bytes < need) return RSK_EINVAL;
@@ -175,20 +178,42 @@ inline void invalidate_compact(rsk_ctx *c) {
     for (auto &kv : c->ws) kv.second[WS_COMPACT].zeroed = false;
 }
 
-// Sync every stream this context has scratch on (the streams its look-back kernels ran on) and its
-// shim stream: rsk_check_device_errors waits for the context's own work only, not the device.
+// Wait for the work whose device error flags rsk_check_device_errors reads.  Normally the streams
+// this context has scratch on (its look-back kernels ran there) and its shim stream -- the context's
+// own work, not the device.  Two cases fall back to the whole device: a
+// context that ever had a call captured (its graphs may be replayed on streams ordered with the
+// capture stream, which the context never saw), and a scratch stream whose handle is no longer valid
+// (destroyed without rsk_release_stream: its scratch is freed and its entry dropped, so later calls
+// do not fail on it again).
 inline hipError_t sync_ctx_streams(rsk_ctx *c) {
+    if (c->captured.load(std::memory_order_relaxed)) return hipDeviceSynchronize();
     std::vector<hipStream_t> ss;
     {
         std::lock_guard<std::mutex> lk(c->ws_mu);
         for (auto &kv : c->ws) ss.push_back(kv.first);
     }
-    if (c->shim_stream) ss.push_back(c->shim_stream);
+    bool stale = false;
     for (hipStream_t s : ss) {
         hipError_t e = hipStreamSynchronize(s);
+        if (e == hipErrorInvalidHandle || e == hipErrorContextIsDestroyed || e == hipErrorInvalidResourceHandle) {
+            (void)hipGetLastError();
+            stale = true;
+            std::lock_guard<std::mutex> lk(c->ws_mu);
+            auto it = c->ws.find(s);
+            if (it != c->ws.end()) {
+                for (WsBuf &b : it->second)
+                    if (b.p) (void)hipFree(b.p);
+                c->ws.erase(it);
+            }
+        } else if (e != hipSuccess) {
+            return e;
+        }
+    }
+    if (c->shim_stream) {
+        hipError_t e = hipStreamSynchronize(c->shim_stream);
         if (e != hipSuccess) return e;
     }
-    return hipSuccess;
+    return stale ? hipDeviceSynchronize() : hipSuccess;
 }
 
 // Sync s, then free its scratch (rsk_release_stream).  Graphs captured on s point at that scratch:

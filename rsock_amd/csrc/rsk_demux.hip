@@ -899,19 +899,8 @@ extern "C" int rsk_demux_batch(rsk_ctx *c, uint32_t n, const rsk_demux_in *in, u
     const uint32_t nb = w.nb;
     hipLaunchKernelGGL(k_dm_flags_prep, dim3(w.nt), dim3(kBlock), 0, s, a, w.st_v, w.st_c, w.cidx, w.cep, w.nv,
                        c->err_dev);
-#ifdef RSK_AB
-    static const int dmv = getenv("RSK_DM_VARIANT") ? atoi(getenv("RSK_DM_VARIANT")) : 0;
-#define RSK_DM_INS(V) hipLaunchKernelGGL(k_dm_insert<V>, dim3((n + kInsTile - 1) / kInsTile), dim3(kBlock), 0, s, a, \
-                                         w.nv, w.cidx, w.cep, w.slots, w.tsize - 1u, w.hslot)
-    if (dmv == 1) RSK_DM_INS(1);
-    else if (dmv == 2) RSK_DM_INS(2);
-    else if (dmv == 3) RSK_DM_INS(3);
-    else RSK_DM_INS(0);
-#undef RSK_DM_INS
-#else
     hipLaunchKernelGGL(k_dm_insert<0>, dim3((n + kInsTile - 1) / kInsTile), dim3(kBlock), 0, s, a, w.nv, w.cidx,
                        w.cep, w.slots, w.tsize - 1u, w.hslot);
-#endif
     hipLaunchKernelGGL(k_dm_leader_rank, dim3(w.nt), dim3(kBlock), 0, s, w.nv, w.hslot, w.slots, w.cidx, w.st_l,
                        w.kA, w.vA, w.rank_at, out->seg_first, w.nseg, w.ghist, c->err_dev);
     hipLaunchKernelGGL(k_dm_segof_hist, dim3(w.nt), dim3(kBlock), 0, s, w.nv, w.nseg, w.rank_at, w.kA, w.vA,
@@ -1313,6 +1302,7 @@ extern "C" int rsk_tcp_send_seq_batch(rsk_ctx *c, uint32_t n, const uint32_t *co
                                       uint16_t *ip_id, void *stream) {
     if (!c) return RSK_EINVAL;
     if (n == 0) return RSK_OK;
+    if (n > RSK_MAX_BATCH) return RSK_EINVAL;  // grids of one lane per packet
     if (!conn || !status || !ip_id_next || !seq || !ip_id || (n_conn && !conn_seq)) return RSK_EINVAL;
     if (n > (1u << 30)) return RSK_EINVAL;
     rsk::DeviceGuard g(c->device);
@@ -1390,6 +1380,7 @@ extern "C" int rsk_tcp_recv_ack_batch(rsk_ctx *c, uint32_t n, const uint32_t *co
                                       const uint32_t *seq, uint32_t n_conn, uint32_t *conn_ack, void *stream) {
     if (!c) return RSK_EINVAL;
     if (n == 0) return RSK_OK;
+    if (n > RSK_MAX_BATCH) return RSK_EINVAL;  // grids of one lane per packet
     if (!conn || !delivered || !seq || (n_conn && !conn_ack)) return RSK_EINVAL;
     if (n > (1u << 30)) return RSK_EINVAL;  // as rsk_tcp_send_seq_batch: 32-bit grid arithmetic stays exact
     rsk::DeviceGuard g(c->device);

@@ -87,22 +87,10 @@ __device__ __forceinline__ uint64_t rdl64(uint64_t v, uint32_t j) {
 //                          computes them once per context and every kernel that frames or verifies
 //                          stages the 2-KB table in LDS (one entry per thread of the 256-thread block,
 //                          before any early exit) and looks the tag up with one ds_read_b64.
-// A/B build only (RSK_MD5_K_LDS, librsk_md5lds.so): RSK_TAG_MD5 reads the 64 round constants from an LDS copy staged per
-// block (the north star's "MD5 round constants ... staged in LDS") instead of instruction
-// immediates; compared against the shipped build by tools/ab_tag.py (profiles/r03_ab_md5_lds.json).
+// Round 3 measured the MD5 round constants staged in LDS per block (the north star's "MD5 round
+// constants ... staged in LDS") against instruction immediates and kept immediates
+// (profiles/r03_ab_md5_lds.json; that build is in the git history).
 __shared__ uint2 s_tags[256];
-#ifdef RSK_MD5_K_LDS
-__shared__ uint32_t s_md5k[64];
-struct KLds {
-    template <int I>
-    __device__ __forceinline__ uint32_t get() const {
-        // one group of 4 constants per 4 steps, read where they are used: without the scheduling
-        // barrier the compiler issues all 64 reads up front and holds them in 64 VGPRs
-        if constexpr ((I & 3) == 0) __builtin_amdgcn_sched_barrier(0);
-        return s_md5k[I];
-    }
-};
-#endif
 
 __device__ __forceinline__ void stage_tags(const KeySched &ks) {
     static_assert(kBlock == 256, "one tag-table entry per thread");
@@ -110,19 +98,14 @@ __device__ __forceinline__ void stage_tags(const KeySched &ks) {
         s_tags[threadIdx.x] = ks.tab[threadIdx.x];
         __syncthreads();
     }
-#ifdef RSK_MD5_K_LDS
-    else {
-        if (threadIdx.x < 64u) s_md5k[threadIdx.x] = rsk::Md5Consts::K[threadIdx.x];
-        __syncthreads();
-    }
-#endif
 }
 
-// LANE (the decode kernels): the payload-word-specialised schedule (rsk_md5.h md5_tag_lane: 4 VALU per
-// step instead of 5, 16 instantiations behind one scalar branch).  The framing kernels keep the generic
-// schedule: in k_encode the specialised one raised the register budget past 128 VGPRs (3 waves per
-// SIMD instead of 4, 2x the SGPR spills) and cost C2 / C4 13-16 % in both tag modes
-// (profiles/r04_ab_md5_isa.json); the decode kernels have registers to spare and gain ~1 %.
+// LANE: the payload-word-specialised schedule (rsk_md5.h md5_tag_lane: 4 VALU per step instead of 5,
+// 16 instantiations behind one scalar branch).  Who uses it: the decode kernels (registers to spare,
+// ~1 %), and the per-set k_encode<12> for its FLAT sets' tag only (profiles/r04q_md5_flat.json).  The
+// per-packet sets and the short-frame build k_encode<19> keep the generic schedule: there the
+// specialised one raised the register budget past 128 VGPRs (3 waves per SIMD instead of 4) and cost
+// C2 / C4 13-16 % (profiles/r04_ab_md5_isa.json).
 template <bool LANE = false>
 __device__ __forceinline__ void tag_of(const KeySched &ks, uint32_t b, uint32_t &t0, uint32_t &t1) {
     if (ks.tag_mode == RSK_TAG_TABLE) {
@@ -131,12 +114,8 @@ __device__ __forceinline__ void tag_of(const KeySched &ks, uint32_t b, uint32_t 
         t1 = t.y;
         return;
     }
-#ifdef RSK_MD5_K_LDS
-    rsk::md5_tag(ks, b & 255u, t0, t1, KLds());
-#else
     if constexpr (LANE) rsk::md5_tag_lane(ks, b & 255u, t0, t1);
     else rsk::md5_tag(ks, b & 255u, t0, t1);
-#endif
 }
 
 // Frame bytes 8..31 as words H[2..7] (bean/EncHead.cpp:9-24 field order; byte 30 reserved = 0,
@@ -217,7 +196,7 @@ constexpr uint32_t kStatValid = 0x80000000u;
 constexpr uint32_t kTwoPassMinPackets = 16384;
 [[maybe_unused]] constexpr uint64_t kCopyMaxPackets = 1ull << 25;  // per k_encode_copy launch (2^31 work-items)
 constexpr uint32_t kTwoPassMinPayload = 960;
-[[maybe_unused]] constexpr uint32_t kSampleEvery = 256;  // per-set calls between two samples (k_enc_sample)
+constexpr uint64_t kFusedMaxGroups = 1ull << 19;  // per k_encode_fused launch (<= 2^25 waves, 2^31 work-items)
 // batches whose sampled mean payload is at most this take the flat-only per-set kernel (RSK_ENC_PATH_SHORT):
 // every set of such a batch has a mean frame under the flat path's 256 B (kFlatBelowMeanBytes) anyway
 [[maybe_unused]] constexpr uint32_t kFlatMaxPayload = 160;
@@ -939,167 +918,8 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
     }
 }
 
-#ifdef RSK_AB
-// A/B build only: memory-side ceiling of the encode access pattern.  Same arenas, same per-packet
-// chunk counts, same store policy as k_encode, but every frame chunk k is a plain copy of aligned
-// source chunk k (no funnel, no header, no partial stores; the frame bytes are NOT the encoding).
-template <int PU>
-__global__ __launch_bounds__(kBlock) void k_copy_probe(EncArgs a) {
-    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    const uint64_t base = ((uint64_t)blockIdx.x * kWavesPerBlock + w) * 64u;
-    if (base >= a.n) return;
-    const uint64_t i = base + lane;
-    uint64_t po = 0, fo = 0;
-    uint32_t P = 0;
-    if (i < a.n) {
-        po = a.pay_off[i];
-        fo = a.frame_off[i];
-        P = a.pay_len[i];
-        a.status[i] = (int32_t)(RSK_HEAD_SIZE + P);
-    }
-    uint64_t vm = __ballot(i < a.n && P > 0u && P <= (uint32_t)RSK_MAX_PAYLOAD);
-    while (vm) {
-        uint4 A[PU][2];
-        uint32_t js[PU], nch[PU], nsrc[PU];
-        bool on[PU];
-#pragma unroll
-        for (int p = 0; p < PU; ++p) {
-            on[p] = vm != 0ull;
-            js[p] = on[p] ? (uint32_t)__builtin_ctzll(vm) : 0u;
-            if (on[p]) vm &= vm - 1ull;
-            const uint32_t Pj = on[p] ? rdl(P, js[p]) : 0u;
-            const uintptr_t s0 = reinterpret_cast<uintptr_t>(a.payload + rdl64(po, js[p]));
-            const uintptr_t d0 = reinterpret_cast<uintptr_t>(a.frame + rdl64(fo, js[p]));
-            // aligned source chunks holding payload bytes; aligned frame chunks up to the padded end
-            nsrc[p] = on[p] ? (uint32_t)(((s0 & 15u) + Pj + 15u) >> 4) : 0u;
-            nch[p] = on[p] ? (uint32_t)(((d0 & 15u) + Pj + RSK_HEAD_SIZE + 15u) >> 4) : 0u;
-            const uint8_t *src = reinterpret_cast<const uint8_t *>(s0 & ~(uintptr_t)15);
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const uint32_t k = lane + 64u * q;
-                A[p][q] = make_uint4(0u, 0u, 0u, 0u);
-                if (k < nsrc[p]) A[p][q] = ld16<0>(src + 16u * k);
-            }
-        }
-#pragma unroll
-        for (int p = 0; p < PU; ++p) {
-            uint8_t *dst = reinterpret_cast<uint8_t *>(reinterpret_cast<uintptr_t>(a.frame + rdl64(fo, js[p])) &
-                                                       ~(uintptr_t)15);
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const uint32_t k = lane + 64u * q;
-                if (k < nch[p]) st16<2>(dst + 16u * k, A[p][q]);
-            }
-        }
-    }
-}
-#endif
 
-#ifdef RSK_AB
-// A/B build only: the tiled mapping (round 1 and 2's shipped form): wave t takes packets
-// [64t, 64t + 64) (coalesced descriptor loads; the co-resident waves each stream their own region of
-// the arenas, 64 packets apart).  SET < 64: wave t takes [SET t, SET t + SET), lanes SET.. idle in
-// phase 1, so each wave streams a smaller region.
-template <int MODE, int PU, int U, int NT, int SET = 64>
-__global__ __launch_bounds__(kBlock) void k_encode_tiled(EncArgs a, KeySched ks) {
-    __shared__ CopyRec recs[kWavesPerBlock][64];
-    __shared__ uint32_t cend[kWavesPerBlock][64];
-    stage_tags(ks);
-    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    const uint64_t base = ((uint64_t)blockIdx.x * kWavesPerBlock + w) * (uint64_t)SET;
-    if (base >= a.n) return;  // wave-uniform; no block barriers below
-    if constexpr (SET < 64) {
-        EncArgs b = a;
-        b.n = (uint32_t)(base + SET < a.n ? base + SET : a.n);
-        encode_set<MODE, PU, U, NT>(b, ks, lane < (uint32_t)SET ? base + lane : b.n, lane, recs[w], cend[w]);
-    } else {
-        encode_set<MODE, PU, U, NT>(a, ks, base + lane, lane, recs[w], cend[w]);
-    }
-}
 
-#endif  // RSK_AB
-
-#ifdef RSK_AB
-// A/B build only (round 4): block-cooperative copy.  A block of 16 waves owns 16 * PPW consecutive
-// packets; each wave copies PPW of them (packet base + w + 16 p), one frame per wave-slot pair, and
-// the block's waves are short-lived, so the chip streams a compact window of the arenas (the
-// one-shot 1-KB-per-wave copy is this chip's fastest copy shape, profiles/r01_hbm_probe.json) instead
-// of ~4 K long-lived waves each streaming its own 64-packet set.  The MD5 stays per lane: wave 0's
-// lanes run phase 1 (descriptors, payload[0], tag, header words) for the block's packets while the
-// other waves already have their chunk loads in flight, and hand the header words over in LDS (one
-// block barrier between the loads and the stores).
-template <int PPW, int NT>
-__global__ __launch_bounds__(1024) void k_encode_bc(EncArgs a, KeySched ks) {
-    constexpr int NP = 16 * PPW;
-    __shared__ uint32_t s_h[NP][9];  // header words of the block's packets (+1: no bank conflicts)
-    if (ks.tag_mode == RSK_TAG_TABLE) {
-        if (threadIdx.x < 256u) s_tags[threadIdx.x] = ks.tab[threadIdx.x];
-        __syncthreads();
-    }
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const uint64_t base = (uint64_t)blockIdx.x * NP;
-    // per wave: its packets' geometry and chunk loads (descriptor loads at a uniform index: scalar)
-    uint4 A[PPW][2];
-    FrameGeo G[PPW];
-    uint32_t fl[PPW];
-#pragma unroll
-    for (int p = 0; p < PPW; ++p) {
-        const uint64_t i = base + w + 16u * p;
-        fl[p] = 0;
-        A[p][0] = A[p][1] = make_uint4(0u, 0u, 0u, 0u);
-        if (i >= a.n) continue;
-        const uint32_t P = a.pay_len[i];
-        if (P == 0u || P > (uint32_t)RSK_MAX_PAYLOAD) continue;
-        fl[p] = RSK_HEAD_SIZE + P;
-        G[p] = frame_geo(a.payload + a.pay_off[i], a.frame + a.frame_off[i], fl[p], a.pad);
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            if (q == 1 && G[p].nst < 64u) continue;  // uniform
-            const int32_t m = (int32_t)(lane + 64u * q) - 2;
-            if (m >= 0 && src_chunk_live(m, G[p].first_rel, G[p].last_rel)) A[p][q] = ld16<NT>(G[p].srcp + 16 * m);
-        }
-    }
-    if (w == 0u) {  // phase 1 of the block's packets, one lane each (status written here)
-        const uint64_t i = lane < (uint32_t)NP && base + lane < a.n ? base + lane : a.n;
-        const Lane1 L = encode_phase1<true>(a, ks, i);
-        if (lane < (uint32_t)NP) {
-#pragma unroll
-            for (int t = 0; t < 8; ++t) s_h[lane][t] = L.H[t];
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int p = 0; p < PPW; ++p) {
-        if (fl[p] == 0u) continue;  // uniform
-        const uint32_t j = w + 16u * p;
-        uint32_t Hj[8];
-#pragma unroll
-        for (int t = 0; t < 8; ++t) Hj[t] = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_h[j][t]);
-        const FrameGeo &g = G[p];
-        const uint32_t flen = fl[p] + g.r, nst = g.nst;
-        uint4 B[2];
-        B[0] = make_uint4(wave_shl1(A[p][0].x), wave_shl1(A[p][0].y), wave_shl1(A[p][0].z), wave_shl1(A[p][0].w));
-        B[1] = make_uint4(0u, 0u, 0u, 0u);
-        if (nst >= 64u) {
-            const uint4 l0 = rdl4(A[p][1], 0);
-            if (lane == 63u) B[0] = l0;
-            if (nst > 64u)
-                B[1] = make_uint4(wave_shl1(A[p][1].x), wave_shl1(A[p][1].y), wave_shl1(A[p][1].z),
-                                  wave_shl1(A[p][1].w));
-        }
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const uint32_t k = lane + 64u * q;
-            if (q == 1 && nst <= 64u) continue;  // uniform
-            const uint4 V = rsk::funnel16(A[p][q], B[q], g.sh);
-            const uint4 v = k < (g.r >= 2u ? 3u : 2u) ? head_chunk(Hj, k, g.r, V) : V;
-            if (k >= nst) continue;
-            store_piece<NT>(g.d0 + 16u * k, v, k == 0u ? g.r : 0u, (int)flen - 16 * (int)k, a.pad != 0u);
-        }
-    }
-}
-#endif  // RSK_AB
 
 // ---- the two-pass form for batches of long frames (round 4) ---------------------------------------
 // Pass 1, k_encode_heads: phase 1 one lane per packet (status, the MD5 tag, EncHead, payload[0]; the
@@ -1129,15 +949,6 @@ __device__ __forceinline__ void encode_heads(const EncArgs &a, const KeySched &k
 __global__ __launch_bounds__(kBlock) void k_encode_heads(EncArgs a, KeySched ks, uint4 *heads, uint32_t *stat) {
     encode_heads(a, ks, heads, stat);
 }
-#ifdef RSK_AB
-// A/B build only (round 4): the header pass held to 80 SGPRs (8 blocks per CU instead of 7), with 2
-// packets per lane, with the word-specialised MD5
-template <int PPL, bool LANE>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(80))) void k_encode_heads_ab(
-    EncArgs a, KeySched ks, uint4 *heads, uint32_t *stat) {
-    encode_heads<PPL, LANE>(a, ks, heads, stat);
-}
-#endif
 
 // NT: bit 0 nontemporal loads, bit 1 nontemporal stores (shipped: 3; C3 -1.4 % against 2, and 256-thread
 // blocks against 64 / 512 / 1024: profiles/r04r_two_pass_ab.json).  BS: threads per block (A/B).
@@ -1191,358 +1002,95 @@ __global__ __launch_bounds__(BS) void k_encode_copy(EncArgs a, const uint32_t *h
     }
 }
 
-#ifdef RSK_AB
-// A/B build only (round 4): look-ahead headers -- the one-wave-per-packet copy of k_encode_copy in ONE
-// launch.  Tile t = 64 consecutive packets = 16 blocks.  Wave 0 of tile t's first
-// block runs phase 1 + MD5 lane-per-packet for tile t + LA (for t < LA first for tile t itself) and
-// publishes the 32-B header records write-through (sc1 buffer stores, drained by s_waitcnt vmcnt(0))
-// behind one sc1 flag per tile; a packet's wave issues its chunk loads, polls its tile's flag (relaxed,
-// agent scope) and reads its record with sc1 loads (MI355X_MICROARCH.md, inter-workgroup visibility,
-// Valid forms, row 1).  A bounded spin falls back to the packet's own phase 1 + MD5, so the result
-// never depends on dispatch order.  The flags are zeroed per call (memset node before the kernel).
-constexpr uint32_t kLaSpinMax = 1u << 14;
 
-// Scalar loads of read-only descriptors behind the producer's stores (the compiler keeps loads that
-// follow a store in the kernel on the vector path, each one a dependent round trip): the constant
-// address space says the bytes are not written during the launch.
-#define RSK_CONST __attribute__((address_space(4)))
-template <typename T>
-__device__ __forceinline__ T ld_const(const T *p) {
-    return *(const RSK_CONST T *)p;
-}
-__device__ __forceinline__ uint32_t ld_const_u16(const uint16_t *p) {  // the dword holding it
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    const uint32_t w = ld_const(reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3));
-    return (w >> (8u * (uint32_t)(a & 2u))) & 0xffffu;
-}
+// ---- the two-pass form in ONE launch (round 5): header waves interleaved with copy waves ----------
+// The two-pass form's cost beyond its copy is the header pass: 0.15 ms on C3, bound by the rate of
+// its scattered payload[0] sector reads while the chip does nothing else, plus the records written
+// and read back (0.27 GB) and the first payload line fetched by both passes.  Here the
+// grid is cut into groups of G packets; wave 0 of a group is its HEADER wave (one lane per packet:
+// status, payload[0], the MD5 tag -- 64 compressions per wave instruction stream, as in pass 1 --
+// EncHead, and the header chunks stored straight into the frames, store_head), the other G / K waves
+// are COPY waves, K packets each (descriptors by scalar loads, every chunk load of the K packets
+// issued before any store, the DPP funnel of k_encode_copy, payload chunks k >= 2 only).  No wave
+// waits for another: a frame's first 32 bytes and the rest are written by two waves, as neighbouring
+// frames already share their boundary lines.  The header wave runs beside its group's copy waves, so
+// its latency-bound byte loads overlap the copy's bandwidth and hit the lines the copy waves fetch
+// at the same moment, and no records exist.  K = 1 for long frames (C3); K = 2 / 4 give a copy wave
+// the bytes in flight of a long frame on mid-length batches (C4).
+template <int K>
+struct FusedGeo {
+    static constexpr uint32_t G = K == 1 ? 63u : K == 2 ? 62u : K == 3 ? 63u : 60u;  // packets per group
+    static constexpr uint32_t WPG = 1u + G / K;                                    // waves per group
+    static_assert(G % K == 0 && G <= 64u, "group geometry");
+};
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t la_rsrc(uint4 *heads, uint32_t t) {
-    return __builtin_amdgcn_make_buffer_rsrc(heads + 128ull * t, (short)0, 2048, 0x00020000);
-}
-
-// KV: the key schedule comes from a device copy, read by vector loads at an opaque (inline-asm) zero
-// offset, so its words live in VGPRs inside the producer / fallback only -- as kernel arguments they
-// are SGPRs for the whole kernel (106, which admits 6 blocks of 256 threads per CU instead of 8).
-__device__ __forceinline__ KeySched ks_vgpr(const KeySched *kd) {
-    uint32_t z;
-    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-    const uint32_t *w = reinterpret_cast<const uint32_t *>(kd) + z;
-    KeySched v;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        v.mid[q] = w[offsetof(KeySched, mid) / 4 + q];
-        v.pre[q] = w[offsetof(KeySched, pre) / 4 + q];
-    }
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        v.blk[q] = w[offsetof(KeySched, blk) / 4 + q];
-        v.pad[q] = w[offsetof(KeySched, pad) / 4 + q];
-    }
-    v.bword = kd->bword;  // uniform: scalar
-    v.bshift = kd->bshift;
-    v.two_blocks = kd->two_blocks;
-    v.tag_mode = kd->tag_mode;
-    v.tab = kd->tab;
-    return v;
-}
-
-__device__ __forceinline__ void la_produce(const EncArgs &a, const KeySched &ks, uint32_t t, uint4 *heads,
-                                           uint32_t *flags, uint32_t lane) {
-    const uint64_t i = 64ull * t + lane;
-    const Lane1 L = encode_phase1<true>(a, ks, i < a.n ? i : a.n);
-    if (L.st > 0) {  // 0 past n
-        const __amdgpu_buffer_rsrc_t r = la_rsrc(heads, t);
-        const u32x4 lo = {L.H[0], L.H[1], L.H[2], L.H[3]}, hi = {L.H[4], L.H[5], L.H[6], L.H[7]};
-        __builtin_amdgcn_raw_buffer_store_b128(lo, r, (int)(32u * lane), 0, 16);  // aux 16 = sc1
-        __builtin_amdgcn_raw_buffer_store_b128(hi, r, (int)(32u * lane + 16u), 0, 16);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0u) __hip_atomic_store(flags + t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// FF: the tile's flag is loaded once BEFORE the chunk loads (its round trip runs beside theirs; the spin,
-// if needed, after them).  FF = 2: timing probe, no flag at all (the record is read unchecked).
-template <int NT, uint32_t LA, int FF, bool KV>
-__device__ __forceinline__ void encode_la(const EncArgs &a, const KeySched &ks0, uint4 *heads, uint32_t *flags,
-                                          const KeySched *kd) {
-    if constexpr (KV) {
-        if (kd->tag_mode == RSK_TAG_TABLE) {
-            s_tags[threadIdx.x] = kd->tab[threadIdx.x];
-            __syncthreads();
-        }
-    } else {
-        stage_tags(ks0);
-    }
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const uint32_t T = (uint32_t)(((uint64_t)a.n + 63ull) >> 6);
-    if ((blockIdx.x & 15u) == 0u && w == 0u) {
-        const KeySched ks = KV ? ks_vgpr(kd) : ks0;
-        const uint32_t t = blockIdx.x >> 4;
-        if (t < LA) la_produce(a, ks, t, heads, flags, lane);
-        if (t + LA < T) la_produce(a, ks, t + LA, heads, flags, lane);
-    }
-    const uint64_t i = (uint64_t)blockIdx.x * kWavesPerBlock + w;
-    if (i >= a.n) return;
-    const uint32_t P = ld_const_u16(a.pay_len + i);
-    const uint64_t po = ld_const(a.pay_off + i), fo = ld_const(a.frame_off + i);
-    if (P == 0u || P > (uint32_t)RSK_MAX_PAYLOAD) return;
-    const uint32_t fl = RSK_HEAD_SIZE + P;
-    const FrameGeo g = frame_geo(a.payload + po, a.frame + fo, fl, a.pad);
-    const uint32_t t = (uint32_t)(i >> 6);
-    uint32_t f0 = 0u;
-    if constexpr (FF == 1) f0 = __hip_atomic_load(flags + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint4 A[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        A[q] = make_uint4(0u, 0u, 0u, 0u);
-        if (q == 1 && g.nst < 64u) continue;  // uniform
-        const int32_t m = (int32_t)(lane + 64u * q) - 2;
-        if (m >= 0 && src_chunk_live(m, g.first_rel, g.last_rel)) A[q] = ld16<NT>(g.srcp + 16 * m);
-    }
-    uint32_t f = FF == 2 ? 1u : (uint32_t)__builtin_amdgcn_readfirstlane((int)f0);
-    for (uint32_t spins = 0; FF != 2 && f == 0u && spins < kLaSpinMax; ++spins) {
-        if (FF == 1 || spins > 0) __builtin_amdgcn_s_sleep(1);
-        f = (uint32_t)__builtin_amdgcn_readfirstlane(
-            (int)__hip_atomic_load(flags + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    }
-    uint32_t Hj[8];
-    if (f != 0u) {
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(la_rsrc(heads, t),
-                                                              (int)(32u * (uint32_t)(i & 63u) + 16u * (lane & 1u)), 0, 16);
-        Hj[0] = rdl(v.x, 0); Hj[1] = rdl(v.y, 0); Hj[2] = rdl(v.z, 0); Hj[3] = rdl(v.w, 0);
-        Hj[4] = rdl(v.x, 1); Hj[5] = rdl(v.y, 1); Hj[6] = rdl(v.z, 1); Hj[7] = rdl(v.w, 1);
-    } else {  // the producer has not published: frame the packet's header here
-        const KeySched ks = KV ? ks_vgpr(kd) : ks0;
-        const Lane1 L = encode_phase1<true>(a, ks, i);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) Hj[q] = (uint32_t)__builtin_amdgcn_readfirstlane((int)L.H[q]);
-    }
-    const uint32_t flen = fl + g.r, nst = g.nst;
-    uint4 B[2];
-    B[0] = make_uint4(wave_shl1(A[0].x), wave_shl1(A[0].y), wave_shl1(A[0].z), wave_shl1(A[0].w));
-    B[1] = make_uint4(0u, 0u, 0u, 0u);
-    if (nst >= 64u) {
-        const uint4 l0 = rdl4(A[1], 0);
-        if (lane == 63u) B[0] = l0;
-        if (nst > 64u) B[1] = make_uint4(wave_shl1(A[1].x), wave_shl1(A[1].y), wave_shl1(A[1].z), wave_shl1(A[1].w));
-    }
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const uint32_t k = lane + 64u * q;
-        if (q == 1 && nst <= 64u) continue;  // uniform
-        const uint4 V = rsk::funnel16(A[q], B[q], g.sh);
-        const uint4 vv = k < (g.r >= 2u ? 3u : 2u) ? head_chunk(Hj, k, g.r, V) : V;
-        if (k >= nst) continue;
-        store_piece<NT>(g.d0 + 16u * k, vv, k == 0u ? g.r : 0u, (int)flen - 16 * (int)k, a.pad != 0u);
-    }
-}
-
-template <int NT, uint32_t LA, int FF = 0, bool KV = false>
-__global__ __launch_bounds__(kBlock) void k_encode_la(EncArgs a, KeySched ks0, uint4 *heads, uint32_t *flags,
-                                                      const KeySched *kd) {
-    encode_la<NT, LA, FF, KV>(a, ks0, heads, flags, kd);
-}
-// the same held to 80 SGPRs: 8 blocks of 256 threads per CU (MI355X_MICROARCH.md, residency: 82-96
-// SGPRs admit 7, 98+ 6; the compiler takes 106 when nothing bounds it)
-template <int NT, uint32_t LA, int FF = 0, bool KV = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(80))) void k_encode_la80(
-    EncArgs a, KeySched ks0, uint4 *heads, uint32_t *flags, const KeySched *kd) {
-    encode_la<NT, LA, FF, KV>(a, ks0, heads, flags, kd);
-}
-
-// A/B build only (round 4): few packets per wave.  Wave w frames packets [PPW w, PPW w + PPW) (linear
-// mapping, short-lived waves: the access shape of k_probe_one) with the shipped long-frame copy
-// (copy_pkt_pipe, TAG form: payload[0] and one MD5 pass per batch of PU packets, header chunks in the
-// packets' own slot stores).
-template <int PPW, int PU, int NT>
-__global__ __launch_bounds__(kBlock) void k_enc_few(EncArgs a, KeySched ks) {
-    stage_tags(ks);
-    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    const uint64_t first = ((uint64_t)blockIdx.x * kWavesPerBlock + w) * PPW;
-    if (first >= a.n) return;  // wave-uniform
-    const uint64_t i = lane < (uint32_t)PPW && first + lane < a.n ? first + lane : a.n;
-    Lane1 L = encode_phase1<false>(a, ks, i);
-    const uint64_t vm = __ballot(L.st > 0);
-    copy_pkt_pipe<PU, NT, true>(a, ks, L, lane, vm);
-}
-
-// A/B build only (round 4): memory-pattern probes for C3's ceiling (wrong bytes: aligned source
-// chunk k -> aligned frame chunk k, no funnel, header or tag).  GI: the shipped grouped-interleave
-// mapping and 4-packet pipelined batches; ONE: one wave per packet.
-__device__ __forceinline__ void probe_geo(const EncArgs &a, uint64_t po, uint64_t fo, uint32_t P, const uint8_t *&src,
-                                          uint8_t *&dst, uint32_t &nsrc, uint32_t &nch) {
-    const uintptr_t s0 = reinterpret_cast<uintptr_t>(a.payload + po), d0 = reinterpret_cast<uintptr_t>(a.frame + fo);
-    nsrc = (uint32_t)(((s0 & 15u) + P + 15u) >> 4);
-    nch = (uint32_t)(((d0 & 15u) + P + RSK_HEAD_SIZE + 15u) >> 4);
-    src = reinterpret_cast<const uint8_t *>(s0 & ~(uintptr_t)15);
-    dst = reinterpret_cast<uint8_t *>(d0 & ~(uintptr_t)15);
-}
-
-__global__ __launch_bounds__(kBlock) void k_probe_one(EncArgs a) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const uint64_t i = (uint64_t)blockIdx.x * kWavesPerBlock + w;
-    if (i >= a.n) return;
-    const uint32_t P = a.pay_len[i];
-    if (P == 0u || P > (uint32_t)RSK_MAX_PAYLOAD) return;
-    const uint8_t *src;
-    uint8_t *dst;
-    uint32_t nsrc, nch;
-    probe_geo(a, a.pay_off[i], a.frame_off[i], P, src, dst, nsrc, nch);
-    uint4 A[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const uint32_t k = lane + 64u * q;
-        A[q] = make_uint4(0u, 0u, 0u, 0u);
-        if (k < nsrc) A[q] = ld16<0>(src + 16u * k);
-    }
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const uint32_t k = lane + 64u * q;
-        if (k < nch) st16<0>(dst + 16u * k, A[q]);
-    }
-}
-
-// persistent: NW waves, wave w copies packets w, w + NW, ... one per iteration; PIPE: the next
-// packet's loads issued before the current packet's stores.  CH > 1: wave w copies CH consecutive
-// packets [CH w, CH w + CH), one at a time (one-shot waves, linear mapping).
-template <bool PIPE>
-__global__ __launch_bounds__(kBlock) void k_probe_persist(EncArgs a) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t w0 = (uint64_t)blockIdx.x * kWavesPerBlock + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
-    auto issue = [&](uint64_t i, uint4 (&A)[2], uint8_t *&dst, uint32_t &nch) {
-        const uint32_t P = i < a.n ? a.pay_len[i] : 0u;
-        const uint8_t *src;
-        uint32_t nsrc;
-        probe_geo(a, i < a.n ? a.pay_off[i] : 0u, i < a.n ? a.frame_off[i] : 0u, P, src, dst, nsrc, nch);
-        if (i >= a.n) nsrc = nch = 0u;
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const uint32_t k = lane + 64u * q;
-            A[q] = ld16<0>(k < nsrc ? src + 16u * k : src);
-        }
-    };
-    auto store = [&](const uint4 (&A)[2], uint8_t *dst, uint32_t nch) {
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const uint32_t k = lane + 64u * q;
-            if (k < nch) st16<0>(dst + 16u * k, A[q]);
-        }
-    };
-    if constexpr (!PIPE) {
-        for (uint64_t i = w0; i < a.n; i += nw) {
-            uint4 A[2];
-            uint8_t *dst;
-            uint32_t nch;
-            issue(i, A, dst, nch);
-            store(A, dst, nch);
-        }
-    } else {
-        uint4 A0[2], A1[2];
-        uint8_t *d0, *d1;
-        uint32_t c0, c1;
-        uint64_t i = w0;
-        if (i >= a.n) return;
-        issue(i, A0, d0, c0);
-        while (true) {
-            const uint64_t j = i + nw;
-            if (j < a.n) issue(j, A1, d1, c1);
-            store(A0, d0, c0);
-            if (j >= a.n) break;
-            i = j + nw;
-            if (i < a.n) issue(i, A0, d0, c0);
-            store(A1, d1, c1);
-            if (i >= a.n) break;
-        }
-    }
-}
-
-template <int CH>
-__global__ __launch_bounds__(kBlock) void k_probe_chunk(EncArgs a) {
+template <int K, int NT>
+__global__ __launch_bounds__(kBlock) void k_encode_fused(EncArgs a, KeySched ks, uint32_t *stat, uint64_t gbase) {
+    using FG = FusedGeo<K>;
+    stage_tags(ks);  // RSK_TAG_TABLE: every wave of the block takes the barrier before any exit
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t w = (uint64_t)blockIdx.x * kWavesPerBlock + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    for (uint64_t i = w * CH; i < a.n && i < w * CH + CH; ++i) {
-        const uint8_t *src;
-        uint8_t *dst;
-        uint32_t nsrc, nch;
-        probe_geo(a, a.pay_off[i], a.frame_off[i], a.pay_len[i], src, dst, nsrc, nch);
-        uint4 A[2];
+    const uint64_t grp = gbase + w / FG::WPG;
+    const uint32_t role = (uint32_t)(w % FG::WPG);
+    const uint64_t g0 = grp * FG::G;
+    if (g0 >= a.n) return;  // wave-uniform
+    if (role == 0u) {
+        // header wave: lane j frames packet g0 + j (j < G)
+        enc_sample(a.pay_len, a.n, stat);  // block 0, lanes 0..63 of wave 0 (this wave of group 0)
+        const uint64_t i = g0 + lane;
+        const Lane1 L = encode_phase1<true, true>(a, ks, lane < FG::G && i < a.n ? i : a.n);
+        if (L.st > 0) store_head(L.H, a.frame + L.fo);
+        return;
+    }
+    const uint64_t i0 = g0 + (uint64_t)(role - 1u) * K;
+    uint4 A[K][2];
+    FrameGeo gg[K];
+    uint32_t flen[K];
+    bool on[K];
+#pragma unroll
+    for (int p = 0; p < K; ++p) {
+        const uint64_t i = i0 + p;
+        const uint32_t P = i < a.n ? a.pay_len[i] : 0u;  // uniform address: scalar loads
+        on[p] = P != 0u && P <= (uint32_t)RSK_MAX_PAYLOAD;  // uniform; status written by the header wave
+        flen[p] = on[p] ? RSK_HEAD_SIZE + P : 0u;
+        gg[p] = frame_geo(a.payload + (on[p] ? a.pay_off[i] : 0u), a.frame + (on[p] ? a.frame_off[i] : 0u), flen[p],
+                          a.pad);
+        if (!on[p]) gg[p].nst = 0u;
+        // lane k loads aligned source chunk k - 2 of slot q (destination chunk k + 64 q); the funnel
+        // partner (chunk k - 1) comes from lane k + 1 by a DPP shift, lane 63 of slot 0 from lane 0 of slot 1
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            A[p][q] = make_uint4(0u, 0u, 0u, 0u);
+            if (q == 1 && gg[p].nst < 64u) continue;  // uniform
+            const int32_t m = (int32_t)(lane + 64u * q) - 2;
+            if (on[p] && m >= 0 && src_chunk_live(m, gg[p].first_rel, gg[p].last_rel))
+                A[p][q] = ld16<NT>(gg[p].srcp + 16 * m);
+        }
+    }
+#pragma unroll
+    for (int p = 0; p < K; ++p) {
+        if (!on[p]) continue;  // uniform
+        const FrameGeo &g = gg[p];
+        const uint32_t fl = flen[p] + g.r, nst = g.nst;
+        uint4 B[2];
+        B[0] = make_uint4(wave_shl1(A[p][0].x), wave_shl1(A[p][0].y), wave_shl1(A[p][0].z), wave_shl1(A[p][0].w));
+        B[1] = make_uint4(0u, 0u, 0u, 0u);
+        if (nst >= 64u) {
+            const uint4 l0 = rdl4(A[p][1], 0);
+            if (lane == 63u) B[0] = l0;
+            if (nst > 64u)
+                B[1] = make_uint4(wave_shl1(A[p][1].x), wave_shl1(A[p][1].y), wave_shl1(A[p][1].z), wave_shl1(A[p][1].w));
+        }
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
             const uint32_t k = lane + 64u * q;
-            A[q] = make_uint4(0u, 0u, 0u, 0u);
-            if (k < nsrc) A[q] = ld16<0>(src + 16u * k);
-        }
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const uint32_t k = lane + 64u * q;
-            if (k < nch) st16<0>(dst + 16u * k, A[q]);
+            if (q == 1 && nst <= 64u) continue;  // uniform
+            if (k >= nst || k < 2u) continue;    // chunks 0, 1 (and chunk 2's header bytes): the header wave
+            const uint4 V = rsk::funnel16(A[p][q], B[q], g.sh);
+            store_piece<NT>(g.d0 + 16u * k, V, k == 2u ? chunk2_lo(g.r) : 0u, (int)fl - 16 * (int)k, a.pad != 0u);
         }
     }
 }
-
-__global__ __launch_bounds__(kBlock) void k_probe_gi(EncArgs a) {
-    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    const uint64_t wg = (uint64_t)blockIdx.x * kWavesPerBlock + w;
-    const uint64_t sb = wg / 1024u, wl = wg % 1024u;
-    if (sb * 1024u * 64u + wl * 8u >= a.n) return;
-    const uint64_t i = sb * 1024u * 64u + ((uint64_t)(lane / 8u) * 1024u + wl) * 8u + lane % 8u;
-    uint64_t po = 0, fo = 0;
-    uint32_t P = 0;
-    if (i < a.n) {
-        po = a.pay_off[i];
-        fo = a.frame_off[i];
-        P = a.pay_len[i];
-        a.status[i] = (int32_t)(RSK_HEAD_SIZE + P);
-    }
-    uint64_t vm = __ballot(i < a.n && P > 0u && P <= (uint32_t)RSK_MAX_PAYLOAD);
-    constexpr int PU = 4;
-    uint4 A0[PU][2], A1[PU][2];
-    uint8_t *d0[PU], *d1[PU];
-    uint32_t n0[PU], n1[PU];
-    auto issue = [&](uint64_t bm, uint4 (&A)[PU][2], uint8_t *(&dd)[PU], uint32_t (&nn)[PU]) {
-#pragma unroll
-        for (int p = 0; p < PU; ++p) {
-            const bool on = bm != 0ull;
-            const uint32_t j = on ? (uint32_t)__builtin_ctzll(bm) : 0u;
-            if (on) bm &= bm - 1ull;
-            const uint8_t *src;
-            uint32_t nsrc;
-            probe_geo(a, rdl64(po, j), rdl64(fo, j), rdl(P, j), src, dd[p], nsrc, nn[p]);
-            if (!on) nn[p] = 0u, nsrc = 0u;
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const uint32_t k = lane + 64u * q;
-                A[p][q] = ld16<0>(k < nsrc ? src + 16u * k : src);
-            }
-        }
-    };
-    auto store = [&](const uint4 (&A)[PU][2], uint8_t *const (&dd)[PU], const uint32_t (&nn)[PU]) {
-#pragma unroll
-        for (int p = 0; p < PU; ++p)
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const uint32_t k = lane + 64u * q;
-                if (k < nn[p]) st16<0>(dd[p] + 16u * k, A[p][q]);
-            }
-    };
-    uint64_t cur = take_batch<PU>(vm);
-    if (!cur) return;
-    issue(cur, A0, d0, n0);
-    while (true) {
-        const uint64_t nxt = take_batch<PU>(vm);
-        if (nxt) issue(nxt, A1, d1, n1);
-        store(A0, d0, n0);
-        if (!nxt) break;
-        cur = take_batch<PU>(vm);
-        if (cur) issue(cur, A0, d0, n0);
-        store(A1, d1, n1);
-        if (!cur) break;
-    }
-}
-#endif  // RSK_AB
 
 // Grouped-interleave mapping (shipped: GRP 8, SBW 1024).  A super-block of SBW consecutive waves owns
 // SBW * 64 consecutive packets; wave wl of it takes groups of GRP consecutive packets strided by
@@ -1577,15 +1125,6 @@ __global__ __launch_bounds__(kBlock) void k_encode(EncArgs a, KeySched ks) {
     encode_grid<MODE, PU, U, NT, GRP, SBW, XCD, TG>(a, ks);
 }
 
-#ifdef RSK_AB
-// A/B build only (round 4): the same kernel forced to MINW waves per SIMD (its register budget cut to
-// 512 / MINW VGPRs): how much C2's flat sets, which need few registers, gain from occupancy (the
-// long-frame copy spills at this budget, so C3 / C4 are expected to lose).
-template <int MINW>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MINW, 8))) void k_encode_occ(EncArgs a, KeySched ks) {
-    encode_grid<11, 4, 4, -1, 8, 1024, false, 0>(a, ks);
-}
-#endif
 
 // the same kernel held to 128 VGPRs (4 waves per SIMD): W = 8 lets the compiler aim higher, W = 4 not
 template <int MODE, int PU, int U, int NT, int GRP, int SBW, int TG, int W>
@@ -3461,61 +3000,6 @@ const char *rsk_last_error(void) { return g_last_error; }
 
 const char *rsk_version(void) { return "rsk 0.1 gfx950"; }
 
-#ifdef RSK_AB
-// A/B build only: selects the encode kernel variant for in-process A/B runs (tools/ab_encode.py).
-// 0 = the shipped k_encode<11, 4, 4, -1, 8, 1024> (grouped interleave; software-pipelined per-packet
-// copy, 4 packets per batch; flat sets' tag behind the first chunk loads); 12 / 13 = k_copy_probe
-// (memory-side ceiling probe, wrong bytes) with 12 / 4 packets per batch; 37 = the tiled mapping
-// with the shipped copy; 47 = the unpipelined copy (MODE 6), 8 packets per iteration; 50 / 51 / 52 /
-// 55 = groups of <GRP, SBW> = <1, 1024> / <2, 1024> / <1, 256> / <1, 4096> (concurrent waves on
-// adjacent packets); 53 / 54 = <1, 1024> / <8, 1024> with XCD-contiguous block numbering; 56 = 0 with
-// the tag (payload[0] + MD5) in the copy loop for every per-packet set (MODE 10); 57 / 58 / 59 / 60 = 0
-// with the long-frame sets' tag prepass over 8 / 16 / 32 / 64 packets (tag_prepass); 61 / 62 = 56 (every
-// per-packet set in the copy-loop tag form) with the prepass over 16 / 32 packets; 63 / 64 = 0, 65 / 66 =
-// 58, 67 / 68 = 59 held to 4 waves per SIMD, amdgpu_waves_per_eu(4, 8) / (4, 4); tail shaping (small sets
-// for the last packets, round 3) in the git history (profiles/r03_ab_encode_tail.json); 69 / 70 / 71 =
-// the block-cooperative copy k_encode_bc (16 waves per block, 1 / 2 / 4 packets per wave), 72 = 69 with
-// nontemporal stores; 73 / 74 = memory-pattern probes (wrong bytes: k_probe_gi, the shipped mapping and
-// batches; k_probe_one, one wave per packet); 75 / 76 = the two-pass form (k_encode_heads then
-// k_encode_copy, normal / nontemporal stores; 76 = the shipped two-pass path); 77 / 78 / 79 / 80 / 81 = k_enc_few, 1 / 2 / 4 / 8 / 16 packets
-// per wave, 82 = 78 with nontemporal stores; 83 / 84 = k_encode_occ (0 forced to 8 / 6 waves per
-// SIMD); 85 / 86 / 88 = k_probe_persist (2048 blocks / 2048 pipelined / 4096 blocks), 87 / 89 =
-// k_probe_chunk<8 / 2> (plain-copy probes, wrong bytes); 90 / 91 = k_encode_la (look-ahead header
-// records, one wave per packet) with LA = 256 / 1024 tiles, 92 / 93 / 94 / 95 = LA 256 / 1024 / 64 / 4096
-// with nontemporal stores, 96 / 97 = 93 / 92 with the tile flag loaded before the chunk loads, 98 = 93
-// without the flag (timing probe: the record is read unchecked) (round 4).  Rounds 1-2
-// measured ~45 more variants (profiles/r01_ab_*, r02_ab_*); their code is in the git history.
-// 99 = k_encode_copy<2> alone on the records a previous 75 / 76 call left (timing probe), 100 = 76 with
-// the two kernels on two streams, concurrently (timing probe: the copy does not wait for the records);
-// 101 / 102 / 103 = 93 / 98 / 92 with the producer's key schedule in VGPRs (ks_vgpr); 104 = 93, 105 / 106 /
-// 107 = 101 / 102 / 103 held to 80 SGPRs (k_encode_la80); 108 = 0 with the flat sets' MD5 on the
-// payload-word-specialised schedule (MODE 12, shipped since); 109 / 110 / 111 / 112 = 76 with the header pass
-// held to 80 SGPRs: 1 / 2 packets per lane, generic / word-specialised MD5 (k_encode_heads_ab); 113 / 114 / 115 =
-// 76 with the copy pass in blocks of 512 / 1024 / 64 threads, 116 = 76 with nontemporal loads in the copy;
-// 117 / 118 = the per-set kernel with a per-packet set's frames under 256 / 512 B on the flat list (MODE 13 / 14);
-// 119 = 116 with normal stores for each frame's first and last 128 B (k_encode_copy EDGE); 120 / 121 / 122 =
-// the per-set kernel with every set on the flat list (MODE 16, flat copy unroll U 4 / 2 / 8; 121 shipped as
-// RSK_ENC_PATH_SHORT); 123 = MODE 18 (12 without the TAG form).
-// v + 1000 * cap (cap 1..8): the same kernel held to `cap` blocks per CU by unused LDS.
-int rsk__set_encode_variant(rsk_ctx *c, int v) {
-    const int k = v % 1000;
-    if (!c || v < 0 || v / 1000 > 8 || !(k == 0 || k == 12 || k == 13 || k == 37 || k == 47 || (k >= 50 && k <= 123)))
-        return RSK_EINVAL;
-    c->enc_variant = v;
-    return RSK_OK;
-}
-
-// Internal (A/B and tests): wire-build copy path.  0 = two-launch hybrid whose per-packet half uses the
-// one-load DPP copy, 8 packets per iteration, tag + payload prefix in the copy loop for sets of long
-// frames (default), 8 = 0 with the tag in phase 1, 10 = 0 on the tiled mapping (64 consecutive
-// packets per wave), 11 / 12 = the software-pipelined per-packet copy (copy_wire_pkt_pipe, 4 / 3
-// packets per batch; round 4: its loads no longer waited for at issue).  Rounds 1-2's other variants: profiles/r0*_ab_wire_*, code in the git history.
-int rsk__set_wire_variant(rsk_ctx *c, int v) {
-    if (!c || !(v == 0 || v == 8 || v == 10 || v == 11 || v == 12)) return RSK_EINVAL;
-    c->wire_variant = v;
-    return RSK_OK;
-}
-#endif  // RSK_AB
 
 rsk_ctx *rsk_create(const uint8_t *key, uint32_t key_len, int device) {
     if (!key && key_len) { snprintf(g_last_error, sizeof g_last_error, "rsk_create: null key"); return nullptr; }
@@ -3603,8 +3087,17 @@ int rsk_release_stream(rsk_ctx *c, void *stream) {
 // Encode path of this context's calls (rsk_codec.h): RSK_ENC_PATH_AUTO (chosen per call, enc_path),
 // RSK_ENC_PATH_PER_SET (k_encode), RSK_ENC_PATH_TWO_PASS (k_encode_heads + k_encode_copy).
 int rsk_set_encode_path(rsk_ctx *c, int path) {
-    if (!c || path < RSK_ENC_PATH_AUTO || path > RSK_ENC_PATH_SHORT) return RSK_EINVAL;
+    if (!c || path < RSK_ENC_PATH_AUTO || path > RSK_ENC_PATH_FUSED) return RSK_EINVAL;
     c->enc_path = path;
+    return RSK_OK;
+}
+
+// Internal (tests, tools): the fused form's packets per copy wave k (1, 2, 4; 0 = from the sampled mean
+// payload) and its copy waves' store policy nt (bit 0 nontemporal loads, bit 1 nontemporal stores).
+int rsk__set_fused(rsk_ctx *c, int k, int nt) {
+    if (!c || !(k == 0 || k == 1 || k == 2 || k == 4) || !(nt == 0 || nt == 2 || nt == 3)) return RSK_EINVAL;
+    c->fused_k = k;
+    c->fused_nt = nt;
     return RSK_OK;
 }
 
@@ -3654,9 +3147,16 @@ int rsk_reserve_stream(rsk_ctx *c, uint32_t n_max, void *stream) {
     if (!g.ok) return RSK_EDEVICE;
     Compact ck;
     const int r = ensure_compact(c, n_max, (hipStream_t)stream, ck);
-    if (r || n_max < kTwoPassMinPackets) return r;
-    void *p = nullptr;  // the two-pass encode's header records (32 B per packet)
-    return rsk::stream_ws(c, (hipStream_t)stream, rsk::WS_ENC, 32ull * n_max, &p);
+    if (r || n_max < kTwoPassMinPackets || c->enc_path != RSK_ENC_PATH_TWO_PASS) return r;
+    // the two-pass encode's header records (32 B per packet), for a context held to that path only; a
+    // failed allocation is not an error: rsk_encode_batch then allocates on demand, or a
+    // captured call takes the per-set kernel
+    void *p = nullptr;
+    if (rsk::stream_ws(c, (hipStream_t)stream, rsk::WS_ENC, 32ull * n_max, &p) != RSK_OK) {
+        (void)hipGetLastError();
+        g_last_error[0] = 0;
+    }
+    return RSK_OK;
 }
 
 // Encode path per call: the context's forced path (rsk_set_encode_path), else the two-pass form for
@@ -3664,6 +3164,14 @@ int rsk_reserve_stream(rsk_ctx *c, uint32_t n_max, void *stream) {
 // two-pass call, and k_enc_sample behind the first and every kSampleEvery-th per-set call) had a mean
 // payload of at least kTwoPassMinPayload bytes, else the per-set kernel.  The first call on a context
 // has no statistic yet and takes the per-set kernel; either path gives identical bytes.
+// packets per copy wave of the fused form: forced (rsk__set_fused), else from the sampled mean payload
+static int fused_k(rsk_ctx *c) {
+    if (c->fused_k) return c->fused_k;
+    const uint32_t s = c->enc_stat_host ? __atomic_load_n(c->enc_stat_host, __ATOMIC_RELAXED) : 0u;
+    const uint32_t mean = (s & kStatValid) ? s & ~kStatValid : 1400u;
+    return mean >= 960u ? 1 : mean >= 480u ? 2 : 4;
+}
+
 [[maybe_unused]] static int enc_path(rsk_ctx *c, uint32_t n) {
     if (c->enc_path) return c->enc_path;
     const uint32_t s = c->enc_stat_host ? __atomic_load_n(c->enc_stat_host, __ATOMIC_RELAXED) : 0u;
@@ -3678,6 +3186,7 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
                      void *stream) {
     if (!c || !in || !out) return RSK_EINVAL;
     if (n == 0) return RSK_OK;
+    if (n > RSK_MAX_BATCH) return RSK_EINVAL;  // grids of one lane per packet
     if (!in->payload_arena || !in->pay_off || !in->pay_len || !in->cmd || !in->conv || !in->conn_key ||
         !out->frame_arena || !out->frame_off || !out->status)
         return RSK_EINVAL;
@@ -3696,177 +3205,6 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
     const unsigned grid = (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
     hipStream_t st = (hipStream_t)stream;
     const dim3 gd(grid), bd(kBlock);
-#ifdef RSK_AB
-    // A/B build only (make -C rsock_amd ab -> librsk_ab.so, tools/): variant + 100 * cap limits
-    // residency to `cap` blocks per CU through unused dynamic LDS
-    const int cap = c->enc_variant / 1000;
-    // caps 5..8 (kernels with <= 2 KB of static LDS): just over 1 / (cap + 1) of the CU's LDS per block
-    const size_t lds = !cap ? 0 : cap <= 4 ? (size_t)(163840 / cap) - 16384 : (size_t)(163840 / (cap + 1)) + 64;
-    switch (c->enc_variant % 1000) {
-        case 12: hipLaunchKernelGGL((k_copy_probe<12>), gd, bd, lds, st, a); break;
-        case 13: hipLaunchKernelGGL((k_copy_probe<4>), gd, bd, lds, st, a); break;
-        case 37: hipLaunchKernelGGL((k_encode_tiled<11, 4, 4, -1>), gd, bd, lds, st, a, c->ks); break;
-        case 47: hipLaunchKernelGGL((k_encode<6, 8, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-        case 50: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 1, 1024>), dim3(enc_grid(n, 1, 1024)), bd, lds, st, a, c->ks); break;
-        case 51: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 2, 1024>), dim3(enc_grid(n, 2, 1024)), bd, lds, st, a, c->ks); break;
-        case 52: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 1, 256>), dim3(enc_grid(n, 1, 256)), bd, lds, st, a, c->ks); break;
-        case 53: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 1, 1024, true>), dim3(enc_grid(n, 1, 1024)), bd, lds, st, a, c->ks); break;
-        case 54: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024, true>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-        case 55: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 1, 4096>), dim3(enc_grid(n, 1, 4096)), bd, lds, st, a, c->ks); break;
-        case 56: hipLaunchKernelGGL((k_encode<10, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-        case 57: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024, false, 8>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-        case 58: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024, false, 16>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-        case 59: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024, false, 32>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-        case 60: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024, false, 64>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-        case 61: hipLaunchKernelGGL((k_encode<10, 4, 4, -1, 8, 1024, false, 16>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-        case 62: hipLaunchKernelGGL((k_encode<10, 4, 4, -1, 8, 1024, false, 32>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-        case 63: hipLaunchKernelGGL((k_encode_w4<11, 4, 4, -1, 8, 1024, 0, 8>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-        case 64: hipLaunchKernelGGL((k_encode_w4<11, 4, 4, -1, 8, 1024, 0, 4>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-        case 65: hipLaunchKernelGGL((k_encode_w4<11, 4, 4, -1, 8, 1024, 16, 8>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-        case 66: hipLaunchKernelGGL((k_encode_w4<11, 4, 4, -1, 8, 1024, 16, 4>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-        case 67: hipLaunchKernelGGL((k_encode_w4<11, 4, 4, -1, 8, 1024, 32, 8>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-        case 68: hipLaunchKernelGGL((k_encode_w4<11, 4, 4, -1, 8, 1024, 32, 4>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-        case 69: hipLaunchKernelGGL((k_encode_bc<1, 0>), dim3((unsigned)((n + 15ull) / 16ull)), dim3(1024), lds, st, a, c->ks); break;
-        case 70: hipLaunchKernelGGL((k_encode_bc<2, 0>), dim3((unsigned)((n + 31ull) / 32ull)), dim3(1024), lds, st, a, c->ks); break;
-        case 71: hipLaunchKernelGGL((k_encode_bc<4, 0>), dim3((unsigned)((n + 63ull) / 64ull)), dim3(1024), lds, st, a, c->ks); break;
-        case 72: hipLaunchKernelGGL((k_encode_bc<1, 2>), dim3((unsigned)((n + 15ull) / 16ull)), dim3(1024), lds, st, a, c->ks); break;
-        case 73: hipLaunchKernelGGL(k_probe_gi, dim3(enc_grid(n, 8, 1024)), bd, lds, st, a); break;
-        case 85: hipLaunchKernelGGL(k_probe_persist<false>, dim3(2048), bd, lds, st, a); break;
-        case 86: hipLaunchKernelGGL(k_probe_persist<true>, dim3(2048), bd, lds, st, a); break;
-        case 87: hipLaunchKernelGGL(k_probe_chunk<8>, dim3((unsigned)((n + 31ull) / 32ull)), bd, lds, st, a); break;
-        case 88: hipLaunchKernelGGL(k_probe_persist<false>, dim3(4096), bd, lds, st, a); break;
-        case 89: hipLaunchKernelGGL(k_probe_chunk<2>, dim3((unsigned)((n + 7ull) / 8ull)), bd, lds, st, a); break;
-        case 83: hipLaunchKernelGGL((k_encode_occ<8>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-        case 84: hipLaunchKernelGGL((k_encode_occ<6>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-        case 77: hipLaunchKernelGGL((k_enc_few<1, 1, 0>), dim3((unsigned)((n + 3ull) / 4ull)), bd, lds, st, a, c->ks); break;
-        case 78: hipLaunchKernelGGL((k_enc_few<2, 2, 0>), dim3((unsigned)((n + 7ull) / 8ull)), bd, lds, st, a, c->ks); break;
-        case 79: hipLaunchKernelGGL((k_enc_few<4, 4, 0>), dim3((unsigned)((n + 15ull) / 16ull)), bd, lds, st, a, c->ks); break;
-        case 80: hipLaunchKernelGGL((k_enc_few<8, 4, 0>), dim3((unsigned)((n + 31ull) / 32ull)), bd, lds, st, a, c->ks); break;
-        case 81: hipLaunchKernelGGL((k_enc_few<16, 4, 0>), dim3((unsigned)((n + 63ull) / 64ull)), bd, lds, st, a, c->ks); break;
-        case 82: hipLaunchKernelGGL((k_enc_few<2, 2, 2>), dim3((unsigned)((n + 7ull) / 8ull)), bd, lds, st, a, c->ks); break;
-        case 74: hipLaunchKernelGGL(k_probe_one, dim3((unsigned)((n + 3ull) / 4ull)), bd, lds, st, a); break;
-        case 75:
-        case 76:
-        case 99:
-        case 100:
-        case 109:
-        case 110:
-        case 111:
-        case 112:
-        case 113:
-        case 114:
-        case 115:
-        case 116:
-        case 119: {
-            static uint4 *heads = nullptr;  // A/B only: the two-pass form's header workspace, never freed
-            static uint64_t heads_n = 0;
-            if (heads_n < n) {
-                if (heads) (void)hipFree(heads);
-                heads = nullptr;
-                if (hipMalloc(&heads, 32ull * n) != hipSuccess) return RSK_ENOMEM;
-                heads_n = n;
-            }
-            const int k = c->enc_variant % 1000;
-            if (k == 100) {  // fork: the header pass on a second stream beside the copy
-                static hipStream_t s2 = nullptr;
-                static hipEvent_t e0 = nullptr, e1 = nullptr;
-                if (!s2 && (hipStreamCreateWithFlags(&s2, hipStreamNonBlocking) != hipSuccess ||
-                            hipEventCreateWithFlags(&e0, hipEventDisableTiming) != hipSuccess ||
-                            hipEventCreateWithFlags(&e1, hipEventDisableTiming) != hipSuccess))
-                    return launch_check("A/B fork stream");
-                (void)hipEventRecord(e0, st);
-                (void)hipStreamWaitEvent(s2, e0, 0);
-                hipLaunchKernelGGL(k_encode_heads, dim3(grid_for(n)), bd, 0, s2, a, c->ks, heads, c->enc_stat_dev);
-                hipLaunchKernelGGL(k_encode_copy<2>, dim3((unsigned)((n + 3ull) / 4ull)), bd, lds, st, a,
-                                   reinterpret_cast<const uint32_t *>(heads));
-                (void)hipEventRecord(e1, s2);
-                (void)hipStreamWaitEvent(st, e1, 0);
-                break;
-            }
-            if (k == 109 || k == 110 || k == 111 || k == 112) {
-                void (*hk)(EncArgs, KeySched, uint4 *, uint32_t *) =
-                    k == 109 ? k_encode_heads_ab<1, false> : k == 110 ? k_encode_heads_ab<2, false>
-                    : k == 111 ? k_encode_heads_ab<1, true> : k_encode_heads_ab<2, true>;
-                hipLaunchKernelGGL(hk, dim3(k == 110 || k == 112 ? (grid_for(n) + 1u) / 2u : grid_for(n)), bd, 0, st,
-                                   a, c->ks, heads, c->enc_stat_dev);
-                hipLaunchKernelGGL(k_encode_copy<2>, dim3((unsigned)((n + 3ull) / 4ull)), bd, lds, st, a,
-                                   reinterpret_cast<const uint32_t *>(heads));
-                break;
-            }
-            if (k == 119) {  // the copy pass with normal stores for each frame's first and last 128 B
-                hipLaunchKernelGGL(k_encode_heads, dim3(grid_for(n)), bd, 0, st, a, c->ks, heads, c->enc_stat_dev);
-                hipLaunchKernelGGL((k_encode_copy<3, kBlock, true>), dim3((unsigned)((n + 3ull) / 4ull)), bd, 0, st, a,
-                                   reinterpret_cast<const uint32_t *>(heads));
-                break;
-            }
-            if (k >= 113 && k <= 116) {  // the copy pass: 512 / 1024 / 64 threads per block, nontemporal loads
-                hipLaunchKernelGGL(k_encode_heads, dim3(grid_for(n)), bd, 0, st, a, c->ks, heads, c->enc_stat_dev);
-                const uint32_t* hr = reinterpret_cast<const uint32_t *>(heads);
-                if (k == 113) hipLaunchKernelGGL((k_encode_copy<2, 512>), dim3((unsigned)((n + 7ull) / 8ull)), dim3(512), 0, st, a, hr);
-                else if (k == 114) hipLaunchKernelGGL((k_encode_copy<2, 1024>), dim3((unsigned)((n + 15ull) / 16ull)), dim3(1024), 0, st, a, hr);
-                else if (k == 115) hipLaunchKernelGGL((k_encode_copy<2, 64>), dim3((unsigned)n), dim3(64), 0, st, a, hr);
-                else hipLaunchKernelGGL((k_encode_copy<3>), dim3((unsigned)((n + 3ull) / 4ull)), bd, 0, st, a, hr);
-                break;
-            }
-            if (k != 99) hipLaunchKernelGGL(k_encode_heads, dim3(grid_for(n)), bd, 0, st, a, c->ks, heads, c->enc_stat_dev);
-            if (k == 75)
-                hipLaunchKernelGGL(k_encode_copy<0>, dim3((unsigned)((n + 3ull) / 4ull)), bd, lds, st, a,
-                                   reinterpret_cast<const uint32_t *>(heads));
-            else
-                hipLaunchKernelGGL(k_encode_copy<2>, dim3((unsigned)((n + 3ull) / 4ull)), bd, lds, st, a,
-                                   reinterpret_cast<const uint32_t *>(heads));
-            break;
-        }
-        case 90: case 91: case 92: case 93: case 94: case 95: case 96: case 97: case 98: case 101: case 102:
-        case 103: case 104: case 105: case 106: case 107: {
-            // A/B only: the look-ahead form's flags (zeroed per call) and header records, never freed
-            static uint8_t *la_ws = nullptr;
-            static uint64_t la_n = 0;
-            const uint64_t tiles = (n + 63ull) / 64ull, fbytes = (4ull * tiles + 255ull) & ~255ull;
-            if (la_n < n) {
-                if (la_ws) (void)hipFree(la_ws);
-                la_ws = nullptr;
-                if (hipMalloc(&la_ws, fbytes + 2048ull * tiles) != hipSuccess) return RSK_ENOMEM;
-                la_n = n;
-            }
-            static KeySched *kd = nullptr;  // the key schedule in device memory (KV variants)
-            if (!kd && hipMalloc(&kd, sizeof(KeySched)) != hipSuccess) return RSK_ENOMEM;
-            if (hipMemcpyAsync(kd, &c->ks, sizeof(KeySched), hipMemcpyHostToDevice, st) != hipSuccess)
-                return launch_check("hipMemcpyAsync(la key schedule)");
-            uint32_t *fl = reinterpret_cast<uint32_t *>(la_ws);
-            uint4 *hd = reinterpret_cast<uint4 *>(la_ws + ((4ull * ((la_n + 63ull) / 64ull) + 255ull) & ~255ull));
-            if (hipMemsetAsync(fl, 0, fbytes, st) != hipSuccess) return launch_check("hipMemsetAsync(la flags)");
-            const dim3 g1((unsigned)((n + 3ull) / 4ull));
-            switch (c->enc_variant % 1000) {
-                case 90: hipLaunchKernelGGL((k_encode_la<0, 256>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
-                case 91: hipLaunchKernelGGL((k_encode_la<0, 1024>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
-                case 92: hipLaunchKernelGGL((k_encode_la<2, 256>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
-                case 93: hipLaunchKernelGGL((k_encode_la<2, 1024>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
-                case 94: hipLaunchKernelGGL((k_encode_la<2, 64>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
-                case 95: hipLaunchKernelGGL((k_encode_la<2, 4096>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
-                case 96: hipLaunchKernelGGL((k_encode_la<2, 1024, 1>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
-                case 97: hipLaunchKernelGGL((k_encode_la<2, 256, 1>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
-                case 98: hipLaunchKernelGGL((k_encode_la<2, 1024, 2>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
-                case 101: hipLaunchKernelGGL((k_encode_la<2, 1024, 0, true>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
-                case 102: hipLaunchKernelGGL((k_encode_la<2, 1024, 2, true>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
-                case 103: hipLaunchKernelGGL((k_encode_la<2, 256, 0, true>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
-                case 104: hipLaunchKernelGGL((k_encode_la80<2, 1024, 0, false>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
-                case 105: hipLaunchKernelGGL((k_encode_la80<2, 1024, 0, true>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
-                case 106: hipLaunchKernelGGL((k_encode_la80<2, 1024, 2, true>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
-                default: hipLaunchKernelGGL((k_encode_la80<2, 256, 0, true>), g1, bd, lds, st, a, c->ks, hd, fl, kd); break;
-            }
-            break;
-        }
-        case 108: hipLaunchKernelGGL((k_encode<12, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-        case 117: hipLaunchKernelGGL((k_encode<13, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-        case 120: hipLaunchKernelGGL((k_encode<16, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-        case 123: hipLaunchKernelGGL((k_encode<18, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-        case 121: hipLaunchKernelGGL((k_encode<16, 4, 2, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-        case 122: hipLaunchKernelGGL((k_encode<16, 4, 8, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-        case 118: hipLaunchKernelGGL((k_encode<14, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-        default: hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, lds, st, a, c->ks); break;
-    }
-#else
     (void)gd;
     const int path = enc_path(c, n);
     if (path == RSK_ENC_PATH_TWO_PASS) {
@@ -3885,6 +3223,27 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         }
         g_last_error[0] = 0;  // no records (a capture that would grow them, or no memory): one pass
     }
+    if (path == RSK_ENC_PATH_FUSED) {
+        // header waves interleaved with copy waves, one launch per 2^19 groups (2^31 work-items)
+        const int fk = fused_k(c), fnt = c->fused_nt;
+        for (uint64_t gb = 0; ; ) {
+            const uint32_t G = fk == 1 ? FusedGeo<1>::G : fk == 2 ? FusedGeo<2>::G : FusedGeo<4>::G;
+            const uint32_t WPG = fk == 1 ? FusedGeo<1>::WPG : fk == 2 ? FusedGeo<2>::WPG : FusedGeo<4>::WPG;
+            const uint64_t ng = (n + G - 1ull) / G;
+            if (gb >= ng) break;
+            const uint64_t m = std::min<uint64_t>(ng - gb, kFusedMaxGroups);
+            const dim3 fg((unsigned)((m * WPG + kWavesPerBlock - 1) / kWavesPerBlock));
+            uint32_t *sp = gb == 0 ? c->enc_stat_dev : nullptr;
+#define RSK_FUSED(KK, NN) hipLaunchKernelGGL((k_encode_fused<KK, NN>), fg, bd, 0, st, a, c->ks, sp, gb)
+            if (fk == 1) { if (fnt == 3) RSK_FUSED(1, 3); else if (fnt == 2) RSK_FUSED(1, 2); else RSK_FUSED(1, 0); }
+            else if (fk == 2) { if (fnt == 3) RSK_FUSED(2, 3); else if (fnt == 2) RSK_FUSED(2, 2); else RSK_FUSED(2, 0); }
+            else { if (fnt == 3) RSK_FUSED(4, 3); else if (fnt == 2) RSK_FUSED(4, 2); else RSK_FUSED(4, 0); }
+#undef RSK_FUSED
+            gb += m;
+        }
+        c->enc_last_path.store(RSK_ENC_PATH_FUSED, std::memory_order_relaxed);
+        return launch_check("k_encode_fused");
+    }
     if (path == RSK_ENC_PATH_SHORT) {
         // batches of short frames: the per-set kernel with every set on the flat chunk list, compiled
         // without the per-packet copy (fewer VGPRs, more waves per SIMD; profiles/r04ac_short_path.json)
@@ -3897,14 +3256,13 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         hipLaunchKernelGGL((k_encode<12, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, 0, st, a, c->ks);
         c->enc_last_path.store(RSK_ENC_PATH_PER_SET, std::memory_order_relaxed);
     }
-    // the statistic for later calls: with no valid value yet, and every kSampleEvery-th call, unless the
-    // call is being captured (a graph replays its path as captured)
-    if (c->enc_path == 0 && c->enc_stat_dev && n >= kTwoPassMinPackets && !rsk::capturing(st)) {
-        const uint32_t k = c->enc_calls.fetch_add(1, std::memory_order_relaxed);
-        if (!(__atomic_load_n(c->enc_stat_host, __ATOMIC_RELAXED) & kStatValid) || k % kSampleEvery == 0u)
-            hipLaunchKernelGGL(k_enc_sample, dim3(1), dim3(64), 0, st, in->pay_len, n, c->enc_stat_dev);
-    }
-#endif
+    // the statistic for the next call, on every call this path takes (a sample every 256th
+    // call left a context that switched from short to long frames on the flat-only kernel for up to 255
+    // calls), unless the call is being captured (a graph replays the path it was captured with).  One
+    // 64-thread launch behind the encode: the per-set kernel itself carries no pointer for it (one more
+    // argument cost C4 12 % through SGPR spills, gpurun_out/r04o).
+    if (c->enc_path == 0 && c->enc_stat_dev && n >= kTwoPassMinPackets && !rsk::capturing(st))
+        hipLaunchKernelGGL(k_enc_sample, dim3(1), dim3(64), 0, st, in->pay_len, n, c->enc_stat_dev);
     return launch_check("k_encode");
 }
 
@@ -3912,6 +3270,7 @@ int rsk_encode_wire_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const
                           const rsk_encode_out *out, void *stream) {
     if (!c || !in || !wire || !out) return RSK_EINVAL;
     if (n == 0) return RSK_OK;
+    if (n > RSK_MAX_BATCH) return RSK_EINVAL;  // grids of one lane per packet
     if (!in->payload_arena || !in->pay_off || !in->pay_len || !in->cmd || !in->conv || !in->conn_key ||
         !out->frame_arena || !out->frame_off || !out->status || !wire->src || !wire->dst || !wire->sp ||
         !wire->dp || !wire->seq || !wire->ack || !wire->flag || !wire->ip_id)
@@ -3937,36 +3296,12 @@ int rsk_encode_wire_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const
     const hipStream_t st = (hipStream_t)stream;
 #define RSK_WIRE(E, M, PU, U) hipLaunchKernelGGL((k_encode_wire<E, M, PU, U>), dim3(grid), dim3(kBlock), 0, st, a, w, c->ks)
 #define RSK_WIRE4(E, M, PU, U) hipLaunchKernelGGL((k_encode_wire_w4<E, M, PU, U>), dim3(grid), dim3(kBlock), 0, st, a, w, c->ks)
-#ifdef RSK_AB
-    const unsigned tgrid = (unsigned)(((n + 63ull) / 64ull + kWavesPerBlock - 1) / kWavesPerBlock);
-#define RSK_WIRET(E, M, PU, U) hipLaunchKernelGGL((k_encode_wire<E, M, PU, U, false>), dim3(tgrid), dim3(kBlock), 0, st, a, w, c->ks)
-#define RSK_WIRE4T(E, M, PU, U) hipLaunchKernelGGL((k_encode_wire_w4<E, M, PU, U, false>), dim3(tgrid), dim3(kBlock), 0, st, a, w, c->ks)
-    const int v = c->wire_variant;
-    if (wire->with_eth) {
-        if (v == 8) { RSK_WIRE(14, 3, 108, 2); RSK_WIRE(14, 4, 2, 2); }
-        else if (v == 10) { RSK_WIRE4T(14, 5, 108, 2); RSK_WIRET(14, 4, 2, 2); }
-        else if (v == 11) { RSK_WIRE4(14, 5, 204, 2); RSK_WIRE(14, 4, 2, 2); }
-        else if (v == 12) { RSK_WIRE4(14, 5, 203, 2); RSK_WIRE(14, 4, 2, 2); }
-        else { RSK_WIRE4(14, 5, 108, 2); RSK_WIRE(14, 4, 2, 2); }
-    } else {
-        if (v == 8) { RSK_WIRE(0, 3, 108, 2); RSK_WIRE(0, 4, 2, 2); }
-        else if (v == 10) { RSK_WIRE4T(0, 5, 108, 2); RSK_WIRET(0, 4, 2, 2); }
-        else if (v == 11) { RSK_WIRE4(0, 5, 204, 2); RSK_WIRE(0, 4, 2, 2); }
-        else if (v == 12) { RSK_WIRE4(0, 5, 203, 2); RSK_WIRE(0, 4, 2, 2); }
-        else { RSK_WIRE4(0, 5, 108, 2); RSK_WIRE(0, 4, 2, 2); }
-    }
-#else
     // the shipped kernels: per-packet half (DPP copy, 8 packets per iteration, tag + payload prefix in
     // the copy loop for long-frame sets, 4 waves/SIMD) then the flat half
     if (wire->with_eth) { RSK_WIRE4(14, 5, 108, 2); RSK_WIRE(14, 4, 2, 2); }
     else { RSK_WIRE4(0, 5, 108, 2); RSK_WIRE(0, 4, 2, 2); }
-#endif
 #undef RSK_WIRE
 #undef RSK_WIRE4
-#ifdef RSK_AB
-#undef RSK_WIRET
-#undef RSK_WIRE4T
-#endif
     return launch_check("k_encode_wire");
 }
 
@@ -3975,6 +3310,7 @@ int rsk_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *frame_arena, const u
                      void *stream) {
     if (!c || !out) return RSK_EINVAL;
     if (n == 0) return empty_batch(c, out->n_valid, stream);
+    if (n > RSK_MAX_BATCH) return RSK_EINVAL;  // grids of one lane per packet
     if (!frame_arena || !frame_off || !frame_len || !dec_out_ok(out)) return RSK_EINVAL;
     DeviceGuard g(c->device);
     if (!g.ok) return RSK_EDEVICE;
@@ -3996,6 +3332,7 @@ int rsk_encode_headers_batch(rsk_ctx *c, uint32_t n, const rsk_encode_hdr_in *in
                              void *stream) {
     if (!c || !in) return RSK_EINVAL;
     if (n == 0) return RSK_OK;
+    if (n > RSK_MAX_BATCH) return RSK_EINVAL;  // grids of one lane per packet
     if (!in->first_byte || !in->pay_len || !in->cmd || !in->conv || !in->conn_key || !hdr || !status)
         return RSK_EINVAL;
     if ((reinterpret_cast<uintptr_t>(hdr) & 15u) || (in->id && (reinterpret_cast<uintptr_t>(in->id) & 7u)))
@@ -4015,6 +3352,7 @@ int rsk_decode_headers_batch(rsk_ctx *c, uint32_t n, const uint8_t *hdr, const u
                              const uint8_t *is_tcp_close, const rsk_decode_out *out, void *stream) {
     if (!c || !out) return RSK_EINVAL;
     if (n == 0) return empty_batch(c, out->n_valid, stream);
+    if (n > RSK_MAX_BATCH) return RSK_EINVAL;  // grids of one lane per packet
     if (!hdr || !frame_len || !dec_out_ok(out)) return RSK_EINVAL;
     if (reinterpret_cast<uintptr_t>(hdr) & 15u) return RSK_EINVAL;
     DeviceGuard g(c->device);
@@ -4052,6 +3390,7 @@ int parse_decode(rsk_ctx *c, uint32_t n, const uint8_t *cap_arena, const uint64_
     if (!c || !tcp || !dec) return RSK_EINVAL;
     if (datalink != RSK_DLT_EN10MB && datalink != RSK_DLT_NULL) return RSK_EINVAL;  // RawTcp.cpp:161-164
     if (n == 0) return empty_batch(c, dec->n_valid, stream);
+    if (n > RSK_MAX_BATCH) return RSK_EINVAL;  // grids of one lane per packet
     if (!cap_arena || (!slot && !cap_off) || !wire_len || !cap_len || !dec_out_ok(dec)) return RSK_EINVAL;
     if (!tcp->src || !tcp->dst || !tcp->sp || !tcp->dp || !tcp->seq || !tcp->ack || !tcp->flag ||
         !tcp->parse_status || !tcp->cap_pay_off || !tcp->cap_pay_len)
@@ -4105,6 +3444,7 @@ int rsk_syncinput_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *rec_arena,
                                void *stream) {
     if (!c || !tcp || !dec) return RSK_EINVAL;
     if (n == 0) return empty_batch(c, dec->n_valid, stream);
+    if (n > RSK_MAX_BATCH) return RSK_EINVAL;  // grids of one lane per packet
     if (!rec_arena || !rec_off || !nread || !dec_out_ok(dec)) return RSK_EINVAL;
     if (!tcp->src || !tcp->dst || !tcp->sp || !tcp->dp || !tcp->seq || !tcp->ack || !tcp->flag ||
         !tcp->parse_status || !tcp->cap_pay_off || !tcp->cap_pay_len)
@@ -4137,6 +3477,7 @@ int rsk_filter_parse_decode_batch(rsk_ctx *c, uint32_t n, const uint8_t *cap_are
     if (datalink != RSK_DLT_EN10MB && datalink != RSK_DLT_NULL) return RSK_EINVAL;
     if (filter_ports_bad(f)) return RSK_EINVAL;
     if (n == 0) return empty_batch(c, dec->n_valid, stream);
+    if (n > RSK_MAX_BATCH) return RSK_EINVAL;  // grids of one lane per packet
     if (!cap_arena || !cap_off || !wire_len || !cap_len || !match || !dec_out_ok(dec)) return RSK_EINVAL;
     if (!tcp->src || !tcp->dst || !tcp->sp || !tcp->dp || !tcp->seq || !tcp->ack || !tcp->flag ||
         !tcp->parse_status || !tcp->cap_pay_off || !tcp->cap_pay_len)
@@ -4172,6 +3513,7 @@ int rsk_capture_filter_batch(rsk_ctx *c, uint32_t n, const uint8_t *cap_arena, c
     if (datalink != RSK_DLT_EN10MB && datalink != RSK_DLT_NULL) return RSK_EINVAL;
     if (filter_ports_bad(f)) return RSK_EINVAL;
     if (n == 0) return empty_batch(c, n_match, stream);
+    if (n > RSK_MAX_BATCH) return RSK_EINVAL;  // grids of one lane per packet
     DeviceGuard g(c->device);
     if (!g.ok) return RSK_EDEVICE;
     const bool compact = match_idx || n_match;
@@ -4233,6 +3575,7 @@ int rsk_tcpinfo_encode_batch(rsk_ctx *c, uint32_t n, const uint32_t *src, const 
                              const uint32_t *ack, const uint8_t *flag, uint8_t *rec, void *stream) {
     if (!c) return RSK_EINVAL;
     if (n == 0) return RSK_OK;
+    if (n > RSK_MAX_BATCH) return RSK_EINVAL;  // grids of one lane per packet
     if (!src || !dst || !sp || !dp || !seq || !ack || !flag || !rec) return RSK_EINVAL;
     DeviceGuard g(c->device);
     if (!g.ok) return RSK_EDEVICE;

@@ -214,13 +214,6 @@ __host__ __device__ __forceinline__ void md5_tag_bw(const KeySched &ks, uint32_t
 
 // Dispatch on the key's payload word (uniform per launch: one scalar branch).
 __host__ __device__ __forceinline__ void md5_tag_lane(const KeySched &ks, uint32_t b, uint32_t &t0, uint32_t &t1) {
-#if defined(RSK_AB) && defined(__HIP_DEVICE_COMPILE__)
-    // A/B build (tools only): the tools' key "hello135" (word 2) specialised, every other key on the
-    // generic schedule, so the ~60 encode variants compile in minutes, not tens of minutes
-    if (ks.bword == 2) md5_tag_bw<2>(ks, b, t0, t1);
-    else md5_tag(ks, b, t0, t1);
-    return;
-#endif
     switch (ks.bword) {
 #define RSK_MD5_BW(W) \
     case W: md5_tag_bw<W>(ks, b, t0, t1); return;

@@ -1,0 +1,40 @@
+"""The encode paths of rsk_encode_batch every GPU encode test runs explicitly (rsk_set_encode_path),
+and a holder that asserts after EVERY encode that the library really took the path it was held to
+(rsk__last_encode_path): a silent fallback to another path must fail the test, not pass it on the
+other path's bytes."""
+from __future__ import annotations
+
+import contextlib
+
+# (path, packets per copy wave of the fused form; 0 = not the fused form)
+#   1 = the per-set kernel k_encode; 2 = the two-pass form (k_encode_heads + k_encode_copy);
+#   3 = the short-frame kernel (every set on the flat chunk list); 4 = the fused form
+#   (k_encode_fused: header waves beside copy waves of k packets)
+ENC_PATHS = [(1, 0), (2, 0), (3, 0), (4, 1), (4, 2), (4, 4)]
+
+
+def path_id(pk) -> str:
+    p, k = pk
+    return f"path{p}" + (f"k{k}" if p == 4 else "")
+
+
+@contextlib.contextmanager
+def held(codec, path: int, k: int = 0):
+    """codec held to encode path `path` (and fused k); every output_batch inside asserts the path."""
+    codec.set_encode_path(path)
+    if path == 4:
+        codec.set_fused(k)
+    cls_fn = type(codec).output_batch
+
+    def checked(*a, **kw):
+        cls_fn(codec, *a, **kw)
+        got = codec.last_encode_path
+        assert got == path, f"encode held to path {path} ran path {got}"
+
+    codec.output_batch = checked
+    try:
+        yield codec
+    finally:
+        del codec.output_batch
+        codec.set_encode_path(0)
+        codec.set_fused(0)

@@ -11,6 +11,7 @@ import numpy as np
 import pytest
 
 from rsock_amd import workload
+from tests.enc_paths import ENC_PATHS, held, path_id
 
 pytestmark = pytest.mark.gpu
 KEY = b"hello135"
@@ -30,13 +31,11 @@ def _le_bytes(x, nbytes):
     return torch.stack([(x >> (8 * k)) & 0xFF for k in range(nbytes)], dim=1).to(torch.uint8)
 
 
-@pytest.fixture(params=[1, 2, 3], ids=lambda p: f"path{p}")
+@pytest.fixture(params=ENC_PATHS, ids=path_id)
 def pcodec(request, codec):
-    """The codec held to one encode path (rsk_set_encode_path): 1 = k_encode, 2 = the two-pass form,
-    3 = every set on the flat chunk list."""
-    codec.set_encode_path(request.param)
-    yield codec
-    codec.set_encode_path(0)
+    """The codec held to one encode path (tests/enc_paths.py): each encode asserts the path it took."""
+    with held(codec, *request.param) as c:
+        yield c
 
 
 @pytest.mark.parametrize("cfg", ["c3", "c2", "c4"])
@@ -165,22 +164,29 @@ def test_compaction_large_random(codec, gpu, oracle):
     assert torch.equal(out.status == 1, valid)
 
 
-def test_two_pass_beyond_one_launch(codec, gpu):
-    """A batch past one copy launch (2^25 packets per k_encode_copy launch: a grid holds at most 2^32 - 1
-    work-items, 64 per packet) takes several launches; its frames equal the per-set kernel's."""
+def test_encode_paths_beyond_one_grid(codec, gpu, oracle):
+    """A batch of 2^26 + 4097 packets: one grid of the two-pass copy (64 work-items per packet) or of the
+    fused form (64 per packet + a header wave per group) would exceed the 2^32 - 1 work-items a grid may
+    hold (r04's C5-on-one-GPU run failed exactly there: "invalid configuration argument"), so both run
+    in several launches; every path's frames must equal the per-set kernel's, and the tags the oracle's
+    table at payload[0] (C2-shaped: ~11 GB of arenas)."""
     import torch
 
-    n = (1 << 25) + 4097
+    n = (1 << 26) + 4097
+    assert 64 * n > 2**32 - 1  # an unsplit copy grid would be illegal
     d = workload.describe("c2", 0, n, n=n)
     w = workload.DeviceWorkload(d, gpu)
-    frames = []
-    for path in (1, 2):
-        codec.set_encode_path(path)
-        w.frame.zero_()
-        codec.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
-                           w.status, id_uniform=workload.ID_UNIFORM, pad16=True)
-        torch.cuda.synchronize()
-        assert codec.last_encode_path == path
-        frames.append(w.frame.clone())
-    codec.set_encode_path(0)
-    assert torch.equal(frames[0], frames[1])
+    ref = None
+    for pk in [(1, 0), (2, 0), (4, 1), (4, 2), (4, 4)]:
+        with held(codec, *pk):
+            w.frame.zero_()
+            codec.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
+                               w.status, id_uniform=workload.ID_UNIFORM, pad16=True)
+            torch.cuda.synchronize()
+        if ref is None:
+            ref = w.frame.clone()
+            frames = ref.view(n, d.frame_pitch)
+            pays = w.payload.view(n, d.pay_pitch)
+            assert torch.equal(frames[:, :8], _tag_table(oracle, gpu)[pays[:, 0].long()])
+        else:
+            assert torch.equal(w.frame, ref), f"path {pk} differs from the per-set kernel"

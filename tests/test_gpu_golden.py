@@ -8,7 +8,8 @@ import os
 import numpy as np
 import pytest
 
-from tests.test_gpu_parity import DEC_VIEWS, dev, run_decode, run_encode
+from tests.enc_paths import ENC_PATHS, held, path_id
+from tests.test_gpu_parity import DEC_VIEWS, dev, run_decode, run_encode, vcodec  # noqa: F401
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -27,7 +28,10 @@ def _golden_encode(cx, gpu, g, pad16=False):
 
 
 @pytest.mark.parametrize("pad16", [False, True])
-def test_encode_matches_reference_frames(codec, gpu, pad16):
+def test_encode_matches_reference_frames(vcodec, gpu, pad16):
+    """The reference's own RConn::Output frames (frames.npz, oracle/_ref) through EVERY encode path
+    (vcodec: held to one path, the path asserted after the encode), both tag modes."""
+    codec = vcodec
     g = gold("frames.npz")
     n = len(g["status"])
     pitch = 1504
@@ -49,7 +53,10 @@ def test_decode_matches_reference_onrecv(codec, gpu):
     assert np.array_equal(got["valid_idx"][:nv].view(np.uint32), np.nonzero(g["status"] == 1)[0].astype(np.uint32))
 
 
-def test_tags_all_keys_match_reference(gpu, tag_mode):
+@pytest.mark.parametrize("pk", ENC_PATHS, ids=path_id)
+def test_tags_all_keys_match_reference(gpu, tag_mode, pk):
+    """tags.npz (the reference's compute_hash for all 256 first bytes x 10 key lengths: 1-block,
+    2-block and midstate schedules) through every encode path, both tag modes."""
     from rsock_amd.codec import Codec
 
     g = gold("tags.npz")
@@ -58,14 +65,37 @@ def test_tags_all_keys_match_reference(gpu, tag_mode):
         key = kb[int(ko[k]): int(ko[k]) + int(kl[k])].tobytes()
         cx = Codec(key, 0, tag_mode=tag_mode)
         try:
-            payload = np.repeat(np.arange(256, dtype=np.uint8), 16)
-            z = np.zeros(256, np.uint8)
-            fr, st = run_encode(cx, gpu, payload, (np.arange(256) * 16).astype(np.uint64), np.full(256, 16, np.uint16),
-                                z, z.astype(np.uint32), z.astype(np.uint64), (np.arange(256) * 48).astype(np.uint64),
-                                256 * 48)
+            with held(cx, *pk):
+                payload = np.repeat(np.arange(256, dtype=np.uint8), 16)
+                z = np.zeros(256, np.uint8)
+                fr, st = run_encode(cx, gpu, payload, (np.arange(256) * 16).astype(np.uint64),
+                                    np.full(256, 16, np.uint16), z, z.astype(np.uint32), z.astype(np.uint64),
+                                    (np.arange(256) * 48).astype(np.uint64), 256 * 48)
             assert np.array_equal(fr.reshape(256, 48)[:, :8], g["tags"][k]), len(key)
         finally:
             cx.close()
+
+
+def test_golden_roundtrip_every_path(vcodec, gpu, oracle):
+    """frames.npz's inputs encoded by the held path, then decoded: the frames equal the reference's, every
+    framed packet comes back VALID with the reference's fields, and the decode of the reference's own
+    frames (onrecv.npz's rule: the oracle pinned to it) agrees field for field."""
+    codec = vcodec
+    g = gold("frames.npz")
+    n = len(g["status"])
+    pitch = 1504
+    fr, st = _golden_encode(codec, gpu, g)
+    ok = st > 0
+    flen = np.where(ok, st, 0).astype(np.uint16)
+    off = (np.arange(n) * pitch).astype(np.uint64)
+    got = run_decode(codec, gpu, fr, off, flen)
+    exp = oracle.decode_batch(KEY, fr, off, flen)
+    for k, dt in DEC_VIEWS.items():
+        assert np.array_equal(got[k].view(dt), exp[k]), k
+    assert np.array_equal(got["status"].view(np.int8) == 1, ok)
+    assert np.array_equal(got["conv"].view(np.uint32)[ok], g["conv"][ok].astype(np.uint32))
+    assert np.array_equal(got["conn_key"].view(np.uint64)[ok], g["conn_key"][ok].astype(np.uint64))
+    assert np.array_equal(got["cmd"][ok], g["cmd"][ok].astype(np.uint8))
 
 
 def test_tcpinfo_records_match_reference(codec, gpu):

@@ -5,7 +5,6 @@ size-independent properties in test_gpu_fullsize.py.
 """
 from __future__ import annotations
 
-import os
 import zlib
 
 import numpy as np
@@ -13,6 +12,7 @@ import pytest
 
 from rsock_amd import workload
 from tests import pkt as P
+from tests.enc_paths import ENC_PATHS, held, path_id
 
 pytestmark = pytest.mark.gpu
 
@@ -111,31 +111,11 @@ def _rand_fields(rng, n):
             rng.integers(0, 2**63, n, dtype=np.uint64) * 2 + rng.integers(0, 2, n, dtype=np.uint64))
 
 
-# the shipped library has one encode kernel (the A/B variants live in the tools build, librsk_ab.so:
-# RSK_LIB=librsk_ab.so RSK_ENC_VARIANTS=0,13,22 runs these tests over them)
-ENC_VARIANTS = [int(v) for v in os.environ.get("RSK_ENC_VARIANTS", "0").split(",")]
-
-
-# the shipped library's encode paths (rsk_set_encode_path): 1 = the per-set kernel k_encode, 2 = the
-# two-pass form for long frames (k_encode_heads + one wave per packet), 3 = the per-set kernel with every
-# set on the flat chunk list (short frames); in normal use the library picks one per call from the last
-# sampled batch's mean payload, so every encode test runs each explicitly
-ENC_PATHS = (1, 2, 3)
-
-
-@pytest.fixture(params=[(v, p) for v in ENC_VARIANTS for p in (ENC_PATHS if v == 0 else (0,))],
-                ids=lambda vp: f"encv{vp[0]}" + (f"-path{vp[1]}" if vp[1] else ""))
+@pytest.fixture(params=ENC_PATHS, ids=path_id)
 def vcodec(request, codec):
-    v, p = request.param
-    if v:
-        codec.set_encode_variant(v)
-    if p:
-        codec.set_encode_path(p)
-    yield codec
-    if v:
-        codec.set_encode_variant(0)
-    if p:
-        codec.set_encode_path(0)
+    """The codec held to one encode path (tests/enc_paths.py): each encode asserts the path it took."""
+    with held(codec, *request.param) as c:
+        yield c
 
 
 @pytest.mark.parametrize("layout,pad", [("slots16", 0), ("packed", 0), ("odd_frames", 0), ("odd_payloads", 0),

@@ -258,9 +258,9 @@ def test_two_pass_encode_in_captured_graph(gpu):
         ref_f, ref_s = _c3_frames(cx, gpu, w, 1)
         for reserved in (True, False):
             s = torch.cuda.Stream(gpu)
-            if reserved:
-                cx.reserve(n, stream=s)
             cx.set_encode_path(2)
+            if reserved:  # reserves the records because the context is held to the two-pass path
+                cx.reserve(n, stream=s)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=s):
                 cx.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
@@ -305,3 +305,77 @@ def test_two_pass_encode_two_streams(codec, gpu):
         codec.set_encode_path(0)
     for w, (f, st) in zip((wa, wb), ref):
         assert torch.equal(w.frame, f) and torch.equal(w.status, st)
+
+
+def test_fused_encode_in_captured_graph(gpu):
+    """The fused encode (header waves beside copy waves, one launch, no scratch) captured into a hipGraph
+    on a stream that was never reserved, replayed: the per-set kernel's bytes, for every copy-wave size."""
+    import torch
+
+    from rsock_amd.codec import Codec
+
+    n = 1 << 17
+    d = workload.describe("c3", 0, n, n=n)
+    w = workload.DeviceWorkload(d, gpu)
+    cx = Codec(b"hello135", 0)
+    try:
+        ref_f, ref_s = _c3_frames(cx, gpu, w, 1)
+        for k in (1, 2, 4):
+            s = torch.cuda.Stream(gpu)
+            cx.set_encode_path(4)
+            cx.set_fused(k)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                cx.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
+                                w.status, id_uniform=workload.ID_UNIFORM, pad16=True, stream=s)
+            assert cx.last_encode_path == 4
+            for _ in range(2):
+                w.frame.zero_()
+                w.status.fill_(-9)
+                torch.cuda.synchronize()
+                g.replay()
+                torch.cuda.synchronize()
+                assert torch.equal(w.frame, ref_f) and torch.equal(w.status, ref_s)
+            del g
+        cx.set_encode_path(0)
+        cx.set_fused(0)
+        assert cx.check_device_errors() == 0  # a captured context waits for the device here
+    finally:
+        cx.close()
+
+
+def test_check_errors_after_stream_destroyed_unreleased(gpu):
+    """a stream that ran a compacting decode is destroyed without rsk_release_stream.
+    rsk_check_device_errors must still work (the stale handle's scratch is dropped, not synced forever
+    as an error), and the context keeps decoding on other streams."""
+    import ctypes
+
+    import torch
+
+    from rsock_amd.codec import Codec, DecodeBuffers
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    n = 50_000
+    d = workload.describe("c2", 0, n, n=n)
+    w = workload.DeviceWorkload(d, gpu)
+    cx = Codec(b"hello135", 0)
+    try:
+        cx.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
+                        w.status, id_uniform=workload.ID_UNIFORM)
+        torch.cuda.synchronize()
+        o = DecodeBuffers.alloc(n, gpu)
+        for _ in range(2):
+            raw = ctypes.c_void_p()
+            assert hip.hipStreamCreate(ctypes.byref(raw)) == 0
+            cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, o, stream=raw.value)
+            assert hip.hipStreamSynchronize(raw) == 0
+            assert int(o.n_valid.item()) == n
+            assert hip.hipStreamDestroy(raw) == 0  # no rsk_release_stream
+            assert cx.check_device_errors() == 0
+            assert cx.check_device_errors() == 0
+        o.n_valid.zero_()
+        cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, o)
+        torch.cuda.synchronize()
+        assert int(o.n_valid.item()) == n and cx.check_device_errors() == 0
+    finally:
+        cx.close()

@@ -22,10 +22,9 @@ def main():
     ap.add_argument("--wire-align", type=int, default=0,
                     help="wire packet pitch alignment (bytes); 0 = the frame slot rule (128 with PAD128 for "
                          "mixed lengths, else 16)")
-    ap.add_argument("--wire-variants", default="", help="also time these rsk__set_wire_variant values (A/B)")
     ap.add_argument("--only", default="", help="time only these paths (comma list), e.g. demux,demux_64conn")
     ap.add_argument("--encode-path", type=int, default=0,
-                    help="rsk_set_encode_path for the encode paths: 0 chosen per call, 1 k_encode, 2 two-pass")
+                    help="rsk_set_encode_path for the encode paths: 0 chosen per call, 1 k_encode, 2 two-pass, 3 short, 4 fused")
     args = ap.parse_args()
     import torch
 
@@ -72,14 +71,6 @@ def main():
         "decode": lambda: cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, w.dec, stream=s),
         "parse_decode": lambda: cx.rawinput_batch(wiree, offe, ste, ste, 1, 0, tcp, pdec, stream=s),
     }
-    # the A/B build (RSK_LIB=librsk_ab.so) exposes rsk__set_wire_variant (0, 8, 10): --wire-variants
-    for v in [int(x) for x in args.wire_variants.split(",") if x]:
-        ops[f"encode_wire_raw4_v{v}"] = (lambda v=v: (cx.set_wire_variant(v), cx.output_wire_batch(
-            *common, src, dst, sp, dp, seq, ack, flag, ipid, wire4, off4, st4, id_uniform=workload.ID_UNIFORM,
-            stream=s, **wpad), cx.set_wire_variant(0)))
-        ops[f"encode_wire_eth_v{v}"] = (lambda v=v: (cx.set_wire_variant(v), cx.output_wire_batch(
-            *common, src, dst, sp, dp, seq, ack, flag, ipid, wiree, offe, ste, eth=eth, id_uniform=workload.ID_UNIFORM,
-            stream=s, **wpad), cx.set_wire_variant(0)))
     # fake-TCP connection state: seq / IP id of a send batch over 64 connections, ack of a receive batch
     conn64 = (torch.arange(n, device=dev, dtype=torch.int64) % 64).to(torch.int32)
     cseq, cack = torch.zeros(64, dtype=torch.int32, device=dev), torch.zeros(64, dtype=torch.int32, device=dev)
