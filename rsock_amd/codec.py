@@ -283,6 +283,19 @@ class Codec:
         fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
         _check(fn(self._ctx, k, nt), "rsk__set_fused")
 
+    def set_two_pass_chunk(self, packets: int = 0) -> None:
+        """Internal knob of the two-pass encode (rsk__set_two_pass_chunk): header pass then copy per chunk
+        of `packets` (0 = the whole batch)."""
+        fn = lib().rsk__set_two_pass_chunk
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+        _check(fn(self._ctx, packets), "rsk__set_two_pass_chunk")
+
+    def set_copy_cap(self, cap: int = 0) -> None:
+        """Internal A/B knob (rsk__set_copy_cap): at most `cap` two-pass copy blocks per CU (0 = no limit)."""
+        fn = lib().rsk__set_copy_cap
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        _check(fn(self._ctx, cap), "rsk__set_copy_cap")
+
     def set_send_seq_groupby(self, v: int) -> None:
         """Internal knob for rsk_tcp_send_seq_batch: 0 the per-tile table path when n_conn < 2048
         (default), 1 the demux group-by path for every n_conn, 2 the table path with the one-kernel

@@ -201,7 +201,7 @@ constexpr uint64_t kFusedMaxGroups = 1ull << 19;  // per k_encode_fused launch (
 // every set of such a batch has a mean frame under the flat path's 256 B (kFlatBelowMeanBytes) anyway
 [[maybe_unused]] constexpr uint32_t kFlatMaxPayload = 160;
 __device__ __forceinline__ void enc_sample(const uint16_t *pay_len, uint32_t n, uint32_t *stat) {
-    if (stat == nullptr || blockIdx.x != 0u || threadIdx.x >= 64u) return;
+    if (stat == nullptr || blockIdx.x != 0u || threadIdx.x >= 64u) return;  // one wave of block 0
     uint32_t v = pay_len[((uint64_t)threadIdx.x * n) >> 6];
 #pragma unroll
     for (int off = 32; off; off >>= 1) v += (uint32_t)__shfl_xor((int)v, off);
@@ -932,76 +932,150 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
 // compression for one packet (~300 VALU whatever its active lanes; 4.5 ms for C3).  Pass 1 runs the
 // compressions 64 to a wave instead.  rsk_encode_batch takes this form for batches of long frames
 // (enc_path); for short frames one packet per wave idles most lanes and the per-set kernel stays.
-template <int PPL = 1, bool LANE = false>
-__device__ __forceinline__ void encode_heads(const EncArgs &a, const KeySched &ks, uint4 *heads, uint32_t *stat) {
+// base: the first packet of this launch (a chunked call runs heads / copy per chunk of packets)
+__global__ __launch_bounds__(kBlock) void k_encode_heads(EncArgs a, KeySched ks, uint4 *heads, uint32_t *stat,
+                                                         uint64_t base) {
     stage_tags(ks);
     enc_sample(a.pay_len, a.n, stat);
+    const uint64_t i = base + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const Lane1 L = encode_phase1<true>(a, ks, i < a.n ? i : a.n);
+    if (i < a.n && L.st > 0) {
+        heads[2 * i] = make_uint4(L.H[0], L.H[1], L.H[2], L.H[3]);
+        heads[2 * i + 1] = make_uint4(L.H[4], L.H[5], L.H[6], L.H[7]);
+    }
+}
+
+// ---- K packets per wave, one wave-instruction stream: the copy of the two-pass and fused forms -------
+// Issue: lanes 0..K-1 load the K packets' pay_len / pay_off / frame_off together (ONE dependent round
+// trip for all descriptors; pay_len has no scalar 16-bit load, and a vector load per packet made the
+// compiler wait for every earlier packet's chunk loads before the next packet's descriptors -- K
+// packets ran one after another), then every chunk load of the K packets with all lanes (no exec
+// mask: dead lanes re-read a chunk a live lane of the instruction reads), so the stores of packet p
+// wait for packet p's loads, not for the later packets'.  Dead lanes' data only ever reaches bytes no
+// store writes (past the frame's end, masked by store_piece; before payload[0], header bytes).
+template <int K>
+struct CopyK {
+    uint4 A[K][2];
+    FrameGeo g[K];
+    uint32_t flen[K];  // frame bytes counted from g.d0 (31 + P + r); 0: packet not framed
+};
+
+template <int K, int NT, bool CL = true>
+__device__ __forceinline__ void copyk_issue(const EncArgs &a, uint64_t i0, uint32_t lane, CopyK<K> &c) {
+    uint32_t dP = 0;
+    uint64_t dpo = 0, dfo = 0;
+    if constexpr (K > 1) {
+        const uint64_t il = i0 + lane;
+        if (lane < (uint32_t)K && il < a.n) {
+            dP = a.pay_len[il];
+            dpo = a.pay_off[il];
+            dfo = a.frame_off[il];
+        }
+    }
 #pragma unroll
-    for (int u = 0; u < PPL; ++u) {  // PPL > 1 (A/B): packets u * 256 apart in the block's PPL * 256
-        const uint64_t i = ((uint64_t)blockIdx.x * PPL + u) * kBlock + threadIdx.x;
-        const Lane1 L = encode_phase1<true, LANE>(a, ks, i < a.n ? i : a.n);
-        if (i < a.n && L.st > 0) {
-            heads[2 * i] = make_uint4(L.H[0], L.H[1], L.H[2], L.H[3]);
-            heads[2 * i + 1] = make_uint4(L.H[4], L.H[5], L.H[6], L.H[7]);
+    for (int p = 0; p < K; ++p) {
+        uint32_t P;
+        const uint8_t *src;
+        uint8_t *dst;
+        if constexpr (K > 1) {
+            P = rdl(dP, (uint32_t)p);
+            src = a.payload + rdl64(dpo, (uint32_t)p);
+            dst = a.frame + rdl64(dfo, (uint32_t)p);
+        } else {
+            // one packet: pay_len, then the offsets of a framed packet only (uniform addresses).  Loading
+            // all three at once shortens each wave by a round trip yet made C3's copy 6 % SLOWER
+            // (gpurun_out/r05k: 2.22 vs 2.08 ms) -- the copy is bound by the memory side, and waves
+            // that start their payload loads together contend for it
+            P = i0 < a.n ? a.pay_len[i0] : 0u;
+            const bool ok = P != 0u && P <= (uint32_t)RSK_MAX_PAYLOAD;
+            src = a.payload + (ok ? a.pay_off[i0] : 0u);
+            dst = a.frame + (ok ? a.frame_off[i0] : 0u);
+        }
+        const bool on = P != 0u && P <= (uint32_t)RSK_MAX_PAYLOAD;  // uniform; status written elsewhere
+        c.g[p] = frame_geo(src, dst, RSK_HEAD_SIZE + P, a.pad);
+        c.flen[p] = on ? RSK_HEAD_SIZE + P + c.g[p].r : 0u;
+        if (!on) c.g[p].nst = 0u;
+        // source chunks holding payload bytes: m_lo .. m_hi (relative to srcp; none when P = 1 and
+        // payload[0] sits in destination chunk 1: no load at all)
+        const int32_t m_lo = c.g[p].first_rel >= 16 ? 1 : 0, m_hi = c.g[p].last_rel >> 4;
+        // lane k loads aligned source chunk k - 2 of slot q (destination chunk k + 64 q); the funnel
+        // partner (chunk k - 1) comes from lane k + 1 by a DPP shift, lane 63 of slot 0 from lane 0 of slot 1.
+        // A lane outside m_lo .. m_hi loads the nearest chunk of that range, which a live lane of the same
+        // instruction requests too: the instruction costs no extra memory request.  Instructions with no
+        // live lane (packet not framed; slot 1 of a frame under 64 chunks) are skipped by a uniform branch.
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            c.A[p][q] = make_uint4(0u, 0u, 0u, 0u);
+            if (!on || m_hi < m_lo || (q == 1 && c.g[p].nst < 64u)) continue;  // uniform
+            const int32_t m = (int32_t)(lane + 64u * q) - 2;
+            if constexpr (CL) {
+                const int32_t mc = m < m_lo ? m_lo : m > m_hi ? m_hi : m;
+                c.A[p][q] = ld16<NT>(c.g[p].srcp + 16 * mc);  // uniform base + lane offset
+            } else {  // A/B: exec-masked loads of the live chunks only
+                if (m >= m_lo && m <= m_hi) c.A[p][q] = ld16<NT>(c.g[p].srcp + 16 * m);
+            }
         }
     }
 }
-__global__ __launch_bounds__(kBlock) void k_encode_heads(EncArgs a, KeySched ks, uint4 *heads, uint32_t *stat) {
-    encode_heads(a, ks, heads, stat);
-}
 
-// NT: bit 0 nontemporal loads, bit 1 nontemporal stores (shipped: 3; C3 -1.4 % against 2, and 256-thread
-// blocks against 64 / 512 / 1024: profiles/r04r_two_pass_ab.json).  BS: threads per block (A/B).
-// EDGE (A/B): the frame's first and last chunks with normal stores (their lines are shared with the
-// neighbouring frames, written by another wave; L2 can merge the two halves), the rest as NT says.
-// base: the launch's first packet (a grid is limited to 2^32 - 1 work-items, i.e. 2^26 packets at 64
-// per packet: larger batches take several launches, kCopyMaxPackets each).
-template <int NT, int BS = kBlock, bool EDGE = false>
-__global__ __launch_bounds__(BS) void k_encode_copy(EncArgs a, const uint32_t *heads, uint64_t base = 0) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const uint64_t i = base + (uint64_t)blockIdx.x * (BS / 64) + w;
-    if (i >= a.n) return;
-    const uint32_t P = a.pay_len[i];  // uniform address, read-only in this launch: scalar loads
-    if (P == 0u || P > (uint32_t)RSK_MAX_PAYLOAD) return;  // status written by pass 1
-    const uint32_t fl = RSK_HEAD_SIZE + P;
-    const FrameGeo g = frame_geo(a.payload + a.pay_off[i], a.frame + a.frame_off[i], fl, a.pad);
-    // lane k loads aligned source chunk k - 2 of slot q (destination chunk k + 64 q); the funnel partner
-    // (chunk k - 1) comes from lane k + 1 by a DPP shift, lane 63 of slot 0 from lane 0 of slot 1
-    uint4 A[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        A[q] = make_uint4(0u, 0u, 0u, 0u);
-        if (q == 1 && g.nst < 64u) continue;  // uniform
-        const int32_t m = (int32_t)(lane + 64u * q) - 2;
-        if (m >= 0 && src_chunk_live(m, g.first_rel, g.last_rel)) A[q] = ld16<NT>(g.srcp + 16 * m);
-    }
-    uint32_t Hj[8];
-#pragma unroll
-    for (int t = 0; t < 8; ++t) Hj[t] = heads[8 * i + t];  // uniform address: scalar loads
-    const uint32_t flen = fl + g.r, nst = g.nst;
+// Store packet p's chunks: TAG (two-pass) every chunk incl. the header chunks from the packet's 8
+// header words Hj; !TAG (fused) only chunks k >= 2 (chunk 2 from its first payload byte), the header
+// wave stores the rest.
+template <int K, int NT, bool TAG>
+__device__ __forceinline__ void copyk_store(const EncArgs &a, const CopyK<K> &c, int p, uint32_t lane,
+                                            const uint32_t (&Hj)[8]) {
+    const FrameGeo &g = c.g[p];
+    const uint32_t nst = g.nst, fl = c.flen[p];
     uint4 B[2];
-    B[0] = make_uint4(wave_shl1(A[0].x), wave_shl1(A[0].y), wave_shl1(A[0].z), wave_shl1(A[0].w));
+    B[0] = make_uint4(wave_shl1(c.A[p][0].x), wave_shl1(c.A[p][0].y), wave_shl1(c.A[p][0].z), wave_shl1(c.A[p][0].w));
     B[1] = make_uint4(0u, 0u, 0u, 0u);
     if (nst >= 64u) {
-        const uint4 l0 = rdl4(A[1], 0);
+        const uint4 l0 = rdl4(c.A[p][1], 0);
         if (lane == 63u) B[0] = l0;
-        if (nst > 64u) B[1] = make_uint4(wave_shl1(A[1].x), wave_shl1(A[1].y), wave_shl1(A[1].z), wave_shl1(A[1].w));
+        if (nst > 64u)
+            B[1] = make_uint4(wave_shl1(c.A[p][1].x), wave_shl1(c.A[p][1].y), wave_shl1(c.A[p][1].z),
+                              wave_shl1(c.A[p][1].w));
     }
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
         const uint32_t k = lane + 64u * q;
         if (q == 1 && nst <= 64u) continue;  // uniform
-        const uint4 V = rsk::funnel16(A[q], B[q], g.sh);
-        const uint4 v = k < (g.r >= 2u ? 3u : 2u) ? head_chunk(Hj, k, g.r, V) : V;
-        if (k >= nst) continue;
-        if (EDGE && (k < 8u || k + 8u >= nst))  // the frame's first / last 128 B
-            store_piece<NT & 1>(g.d0 + 16u * k, v, k == 0u ? g.r : 0u, (int)flen - 16 * (int)k, a.pad != 0u);
-        else
-            store_piece<NT>(g.d0 + 16u * k, v, k == 0u ? g.r : 0u, (int)flen - 16 * (int)k, a.pad != 0u);
+        const uint4 V = rsk::funnel16(c.A[p][q], B[q], g.sh);
+        if constexpr (TAG) {
+            const uint4 v = k < (g.r >= 2u ? 3u : 2u) ? head_chunk(Hj, k, g.r, V) : V;
+            if (k >= nst) continue;
+            store_piece<NT>(g.d0 + 16u * k, v, k == 0u ? g.r : 0u, (int)fl - 16 * (int)k, a.pad != 0u);
+        } else {
+            if (k >= nst || k < 2u) continue;
+            store_piece<NT>(g.d0 + 16u * k, V, k == 2u ? chunk2_lo(g.r) : 0u, (int)fl - 16 * (int)k, a.pad != 0u);
+        }
     }
 }
 
+// NT: bit 0 nontemporal loads, bit 1 nontemporal stores (shipped: 3; C3 -1.4 % against 2, and 256-thread
+// blocks against 64 / 512 / 1024: profiles/r04r_two_pass_ab.json).  K: packets per wave (round 5):
+// every chunk load of the K packets is issued before any store, so a wave carries K frames' bytes in
+// flight -- the chip retires a bounded number of waves per second (the one-packet waves of C3 run at
+// ~2 G waves/s), so short frames need several per wave to keep the memory system busy.
+// base: the launch's first packet (a grid is limited to 2^32 - 1 work-items, i.e. 2^26 packets at 64
+// per packet: larger batches take several launches, kCopyMaxPackets each).
+template <int NT, int K = 1, bool CL = true>
+__global__ __launch_bounds__(kBlock) void k_encode_copy(EncArgs a, const uint32_t *heads, uint64_t base = 0) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint64_t i0 = base + ((uint64_t)blockIdx.x * kWavesPerBlock + w) * K;
+    if (i0 >= a.n) return;
+    CopyK<K> c;
+    copyk_issue<K, NT, CL>(a, i0, lane, c);
+#pragma unroll
+    for (int p = 0; p < K; ++p) {
+        if (!c.flen[p]) continue;  // uniform
+        uint32_t Hj[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) Hj[t] = heads[8 * (i0 + p) + t];  // uniform address: scalar loads
+        copyk_store<K, NT, true>(a, c, p, lane, Hj);
+    }
+}
 
 // ---- the two-pass form in ONE launch (round 5): header waves interleaved with copy waves ----------
 // The two-pass form's cost beyond its copy is the header pass: 0.15 ms on C3, bound by the rate of
@@ -1024,72 +1098,79 @@ struct FusedGeo {
     static_assert(G % K == 0 && G <= 64u, "group geometry");
 };
 
-template <int K, int NT>
-__global__ __launch_bounds__(kBlock) void k_encode_fused(EncArgs a, KeySched ks, uint32_t *stat, uint64_t gbase) {
+// HV (header-store variants, measured): bit 0 -- aligned frames' 32 header bytes stored by lane pairs
+// (lane 2j chunk 0, lane 2j + 1 chunk 1 of packet j: one 32-B piece per packet per instruction instead
+// of two 16-B stores from one lane); bit 1 -- nontemporal header stores; bit 2 -- XCD grouping: a
+// group's blocks all have the same blockIdx % 8 (one XCD, one L2, under round-robin placement: speed
+// only), so the header bytes and the rest of a frame's first line meet in one L2.
+template <int HV>
+__device__ __forceinline__ void fused_store_heads(const EncArgs &a, const Lane1 &L, uint32_t lane, uint32_t G) {
+    const bool al = L.st <= 0 || (reinterpret_cast<uintptr_t>(a.frame + L.fo) & 15u) == 0u;
+    if (!(HV & 1) || __ballot(!al) != 0ull) {
+        if (L.st > 0) store_head(L.H, a.frame + L.fo);
+        return;
+    }
+    const uint32_t h = lane & 1u;
+#pragma unroll
+    for (int rd = 0; rd < 2; ++rd) {
+        const uint32_t j = (lane >> 1) + 32u * rd;
+        uint32_t v[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[t] = (uint32_t)__shfl((int)L.H[t], (int)j);
+        const int32_t st = __shfl(L.st, (int)j);
+        const uint64_t fo = shfl64(L.fo, j);
+        const uint4 w4 = h ? make_uint4(v[4], v[5], v[6], v[7]) : make_uint4(v[0], v[1], v[2], v[3]);
+        if (j < G && st > 0) st16<(HV & 2) ? 2 : 0>(a.frame + fo + 16u * h, w4);
+    }
+}
+
+template <int K, int NT, int HV>
+__device__ __forceinline__ void encode_fused(const EncArgs &a, const KeySched &ks, uint32_t *stat, uint64_t gbase) {
     using FG = FusedGeo<K>;
     stage_tags(ks);  // RSK_TAG_TABLE: every wave of the block takes the barrier before any exit
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t w = (uint64_t)blockIdx.x * kWavesPerBlock + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const uint64_t grp = gbase + w / FG::WPG;
-    const uint32_t role = (uint32_t)(w % FG::WPG);
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    uint64_t grp;
+    uint32_t role;
+    if constexpr (HV & 4) {
+        constexpr uint32_t BPG = FG::WPG / kWavesPerBlock;  // blocks per group
+        static_assert(FG::WPG % kWavesPerBlock == 0, "whole blocks per group");
+        const uint32_t x = blockIdx.x % 8u, j = blockIdx.x / 8u;
+        grp = gbase + (uint64_t)(j / BPG) * 8u + x;
+        role = (j % BPG) * kWavesPerBlock + wv;
+    } else {
+        const uint64_t w = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
+        grp = gbase + w / FG::WPG;
+        role = (uint32_t)(w % FG::WPG);
+    }
     const uint64_t g0 = grp * FG::G;
     if (g0 >= a.n) return;  // wave-uniform
     if (role == 0u) {
         // header wave: lane j frames packet g0 + j (j < G)
-        enc_sample(a.pay_len, a.n, stat);  // block 0, lanes 0..63 of wave 0 (this wave of group 0)
+        if (blockIdx.x == 0u) enc_sample(a.pay_len, a.n, stat);  // group 0's header wave (wave 0 of block 0)
         const uint64_t i = g0 + lane;
         const Lane1 L = encode_phase1<true, true>(a, ks, lane < FG::G && i < a.n ? i : a.n);
-        if (L.st > 0) store_head(L.H, a.frame + L.fo);
+        fused_store_heads<HV>(a, L, lane, FG::G);
         return;
     }
     const uint64_t i0 = g0 + (uint64_t)(role - 1u) * K;
-    uint4 A[K][2];
-    FrameGeo gg[K];
-    uint32_t flen[K];
-    bool on[K];
+    CopyK<K> c;
+    copyk_issue<K, NT>(a, i0, lane, c);
+    const uint32_t none[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
 #pragma unroll
-    for (int p = 0; p < K; ++p) {
-        const uint64_t i = i0 + p;
-        const uint32_t P = i < a.n ? a.pay_len[i] : 0u;  // uniform address: scalar loads
-        on[p] = P != 0u && P <= (uint32_t)RSK_MAX_PAYLOAD;  // uniform; status written by the header wave
-        flen[p] = on[p] ? RSK_HEAD_SIZE + P : 0u;
-        gg[p] = frame_geo(a.payload + (on[p] ? a.pay_off[i] : 0u), a.frame + (on[p] ? a.frame_off[i] : 0u), flen[p],
-                          a.pad);
-        if (!on[p]) gg[p].nst = 0u;
-        // lane k loads aligned source chunk k - 2 of slot q (destination chunk k + 64 q); the funnel
-        // partner (chunk k - 1) comes from lane k + 1 by a DPP shift, lane 63 of slot 0 from lane 0 of slot 1
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            A[p][q] = make_uint4(0u, 0u, 0u, 0u);
-            if (q == 1 && gg[p].nst < 64u) continue;  // uniform
-            const int32_t m = (int32_t)(lane + 64u * q) - 2;
-            if (on[p] && m >= 0 && src_chunk_live(m, gg[p].first_rel, gg[p].last_rel))
-                A[p][q] = ld16<NT>(gg[p].srcp + 16 * m);
-        }
-    }
-#pragma unroll
-    for (int p = 0; p < K; ++p) {
-        if (!on[p]) continue;  // uniform
-        const FrameGeo &g = gg[p];
-        const uint32_t fl = flen[p] + g.r, nst = g.nst;
-        uint4 B[2];
-        B[0] = make_uint4(wave_shl1(A[p][0].x), wave_shl1(A[p][0].y), wave_shl1(A[p][0].z), wave_shl1(A[p][0].w));
-        B[1] = make_uint4(0u, 0u, 0u, 0u);
-        if (nst >= 64u) {
-            const uint4 l0 = rdl4(A[p][1], 0);
-            if (lane == 63u) B[0] = l0;
-            if (nst > 64u)
-                B[1] = make_uint4(wave_shl1(A[p][1].x), wave_shl1(A[p][1].y), wave_shl1(A[p][1].z), wave_shl1(A[p][1].w));
-        }
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const uint32_t k = lane + 64u * q;
-            if (q == 1 && nst <= 64u) continue;  // uniform
-            if (k >= nst || k < 2u) continue;    // chunks 0, 1 (and chunk 2's header bytes): the header wave
-            const uint4 V = rsk::funnel16(A[p][q], B[q], g.sh);
-            store_piece<NT>(g.d0 + 16u * k, V, k == 2u ? chunk2_lo(g.r) : 0u, (int)fl - 16 * (int)k, a.pad != 0u);
-        }
-    }
+    for (int p = 0; p < K; ++p)
+        if (c.flen[p]) copyk_store<K, NT, false>(a, c, p, lane, none);  // uniform
+}
+
+// HV bit 3: held to 8 waves per SIMD (the key schedule's SGPRs otherwise allow 7)
+template <int K, int NT, int HV = 0>
+__global__ __launch_bounds__(kBlock) void k_encode_fused(EncArgs a, KeySched ks, uint32_t *stat, uint64_t gbase) {
+    encode_fused<K, NT, HV>(a, ks, stat, gbase);
+}
+template <int K, int NT, int HV = 0>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_encode_fused8(
+    EncArgs a, KeySched ks, uint32_t *stat, uint64_t gbase) {
+    encode_fused<K, NT, HV>(a, ks, stat, gbase);
 }
 
 // Grouped-interleave mapping (shipped: GRP 8, SBW 1024).  A super-block of SBW consecutive waves owns
@@ -3095,9 +3176,29 @@ int rsk_set_encode_path(rsk_ctx *c, int path) {
 // Internal (tests, tools): the fused form's packets per copy wave k (1, 2, 4; 0 = from the sampled mean
 // payload) and its copy waves' store policy nt (bit 0 nontemporal loads, bit 1 nontemporal stores).
 int rsk__set_fused(rsk_ctx *c, int k, int nt) {
-    if (!c || !(k == 0 || k == 1 || k == 2 || k == 4) || !(nt == 0 || nt == 2 || nt == 3)) return RSK_EINVAL;
+    const int hv = nt >> 4;  // header-store variant (k_encode_fused HV) in bits 4..7
+    nt &= 15;  // bit 3: the two-pass copy with exec-masked loads (A/B)
+    if (!c || !(k == 0 || k == 1 || k == 2 || k == 4) || !((nt & 7) == 0 || (nt & 7) == 2 || (nt & 7) == 3) ||
+        !(hv == 0 || hv == 1 || hv == 3 || hv == 4 || hv == 5 || hv == 7 || hv == 9))
+        return RSK_EINVAL;
     c->fused_k = k;
     c->fused_nt = nt;
+    c->fused_hv = hv;
+    c->copy_k = k;  // the two-pass copy's packets per wave too
+    return RSK_OK;
+}
+
+// Internal (tools): at most `cap` two-pass copy blocks per CU (0: no limit), by unused dynamic LDS (A/B).
+int rsk__set_copy_cap(rsk_ctx *c, int cap) {
+    if (!c || cap < 0 || cap > 16) return RSK_EINVAL;
+    c->copy_cap = cap;
+    return RSK_OK;
+}
+
+// Internal (tests, tools): the two-pass form in chunks of `packets` (0: the whole batch in one pass each)
+int rsk__set_two_pass_chunk(rsk_ctx *c, uint32_t packets) {
+    if (!c) return RSK_EINVAL;
+    c->tp_chunk = packets;
     return RSK_OK;
 }
 
@@ -3211,12 +3312,29 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         // the two-pass form (batches of long frames): header records, then one wave per packet
         void *hp = nullptr;
         if (rsk::stream_ws_if(c, st, rsk::WS_ENC, 32ull * n, &hp) == RSK_OK) {
-            hipLaunchKernelGGL(k_encode_heads, dim3(grid_for(n)), bd, 0, st, a, c->ks, static_cast<uint4 *>(hp),
-                               c->enc_stat_dev);
-            for (uint64_t b0 = 0; b0 < n; b0 += kCopyMaxPackets) {  // one launch up to 2^25 packets
-                const uint64_t m = n - b0 < kCopyMaxPackets ? n - b0 : kCopyMaxPackets;
-                hipLaunchKernelGGL(k_encode_copy<3>, dim3((unsigned)((m + 3ull) / 4ull)), bd, 0, st, a,
-                                   static_cast<const uint32_t *>(hp), b0);
+            const int ck = c->copy_k ? c->copy_k : 1;
+            // chunked (rsk__set_two_pass_chunk): heads then copy per chunk, so a chunk's records and
+            // first payload lines may still be in the Infinity Cache when its copy reads them
+            const uint64_t chunk = c->tp_chunk ? c->tp_chunk : (uint64_t)n;
+            for (uint64_t c0 = 0; c0 < n; c0 += chunk) {
+                EncArgs ac = a;
+                ac.n = (uint32_t)std::min<uint64_t>(n, c0 + chunk);
+                hipLaunchKernelGGL(k_encode_heads, dim3(grid_for(ac.n - c0)), bd, 0, st, ac, c->ks,
+                                   static_cast<uint4 *>(hp), c0 == 0 ? c->enc_stat_dev : nullptr, c0);
+                for (uint64_t b0 = c0; b0 < ac.n; b0 += kCopyMaxPackets) {  // one launch up to 2^25 packets
+                    const uint64_t m = ac.n - b0 < kCopyMaxPackets ? ac.n - b0 : kCopyMaxPackets;
+                    const dim3 cg((unsigned)((m + 4ull * ck - 1ull) / (4ull * ck)));
+                    const uint32_t *hr = static_cast<const uint32_t *>(hp);
+                    const bool cl = !(c->fused_nt & 8);
+                    // A/B (rsk__set_copy_cap): at most `cap` copy blocks per CU, by dynamic LDS
+                    const size_t lds = c->copy_cap ? (size_t)(163840 / (c->copy_cap + 1)) + 64 : 0;
+                    if (ck == 2) { if (cl) hipLaunchKernelGGL((k_encode_copy<3, 2>), cg, bd, lds, st, ac, hr, b0);
+                                   else hipLaunchKernelGGL((k_encode_copy<3, 2, false>), cg, bd, lds, st, ac, hr, b0); }
+                    else if (ck == 4) { if (cl) hipLaunchKernelGGL((k_encode_copy<3, 4>), cg, bd, lds, st, ac, hr, b0);
+                                        else hipLaunchKernelGGL((k_encode_copy<3, 4, false>), cg, bd, lds, st, ac, hr, b0); }
+                    else { if (cl) hipLaunchKernelGGL((k_encode_copy<3, 1>), cg, bd, lds, st, ac, hr, b0);
+                           else hipLaunchKernelGGL((k_encode_copy<3, 1, false>), cg, bd, lds, st, ac, hr, b0); }
+                }
             }
             c->enc_last_path.store(2, std::memory_order_relaxed);
             return launch_check("k_encode_heads / k_encode_copy");
@@ -3232,12 +3350,22 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
             const uint64_t ng = (n + G - 1ull) / G;
             if (gb >= ng) break;
             const uint64_t m = std::min<uint64_t>(ng - gb, kFusedMaxGroups);
-            const dim3 fg((unsigned)((m * WPG + kWavesPerBlock - 1) / kWavesPerBlock));
+            const int hv = c->fused_hv;
+            // XCD grouping (hv bit 2): whole rounds of 8 groups, one per blockIdx % 8
+            const uint64_t mb = hv & 4 ? (m + 7ull) / 8ull * 8ull : m;
+            const dim3 fg((unsigned)((mb * WPG + kWavesPerBlock - 1) / kWavesPerBlock));
             uint32_t *sp = gb == 0 ? c->enc_stat_dev : nullptr;
-#define RSK_FUSED(KK, NN) hipLaunchKernelGGL((k_encode_fused<KK, NN>), fg, bd, 0, st, a, c->ks, sp, gb)
-            if (fk == 1) { if (fnt == 3) RSK_FUSED(1, 3); else if (fnt == 2) RSK_FUSED(1, 2); else RSK_FUSED(1, 0); }
-            else if (fk == 2) { if (fnt == 3) RSK_FUSED(2, 3); else if (fnt == 2) RSK_FUSED(2, 2); else RSK_FUSED(2, 0); }
-            else { if (fnt == 3) RSK_FUSED(4, 3); else if (fnt == 2) RSK_FUSED(4, 2); else RSK_FUSED(4, 0); }
+#define RSK_FUSED(KK, NN, HH) hipLaunchKernelGGL((k_encode_fused<KK, NN, HH>), fg, bd, 0, st, a, c->ks, sp, gb)
+#define RSK_FUSED_HV(KK, NN) \
+    switch (hv) { case 1: RSK_FUSED(KK, NN, 1); break; case 3: RSK_FUSED(KK, NN, 3); break; \
+                  case 4: RSK_FUSED(KK, NN, 4); break; case 5: RSK_FUSED(KK, NN, 5); break; \
+                  case 7: RSK_FUSED(KK, NN, 7); break; \
+                  case 9: hipLaunchKernelGGL((k_encode_fused8<KK, NN, 1>), fg, bd, 0, st, a, c->ks, sp, gb); break; \
+                  default: RSK_FUSED(KK, NN, 0); break; }
+            if (fk == 1) { if (fnt == 3) { RSK_FUSED_HV(1, 3) } else if (fnt == 2) { RSK_FUSED_HV(1, 2) } else { RSK_FUSED_HV(1, 0) } }
+            else if (fk == 2) { if (fnt == 3) { RSK_FUSED_HV(2, 3) } else { RSK_FUSED_HV(2, 0) } }
+            else { if (fnt == 3) { RSK_FUSED_HV(4, 3) } else { RSK_FUSED_HV(4, 0) } }
+#undef RSK_FUSED_HV
 #undef RSK_FUSED
             gb += m;
         }

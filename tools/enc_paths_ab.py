@@ -17,8 +17,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def parse_variant(v):
+    """path[:k[:nt[:chunk[:cap]]]] -- k packets per copy wave (paths 2, 4), nt store policy + header variant
+    << 4 (path 4), chunk packets per heads / copy pair (path 2; 0 = the whole batch), cap copy blocks per CU
+    (path 2; 0 = no limit)"""
     f = [int(x) for x in v.split(":")]
-    return (f[0], f[1] if len(f) > 1 else 0, f[2] if len(f) > 2 else 3)
+    return (f[0], f[1] if len(f) > 1 else 0, f[2] if len(f) > 2 else 3, f[3] if len(f) > 3 else 0,
+            f[4] if len(f) > 4 else 0)
 
 
 def main():
@@ -61,16 +65,18 @@ def main():
     variants = [parse_variant(v) for v in args.variants.split(",")]
 
     def run(v):
-        p, k, nt = v
+        p, k, nt, chunk, cap = v
         cx.set_encode_path(p)
-        if p == 4:
-            cx.set_fused(k, nt)
+        if p in (2, 4):
+            cx.set_fused(k, nt)  # also the two-pass copy's packets per wave
+        cx.set_two_pass_chunk(chunk)
+        cx.set_copy_cap(cap)
         cx.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off, w.status,
                         id_uniform=workload.ID_UNIFORM, pad16=pad == 16, pad128=pad == 128, stream=s)
 
     with torch.cuda.stream(s):
         w.frame.zero_()
-        run((1, 0, 3))
+        run((1, 0, 3, 0, 0))
         s.synchronize()
         ref_f, ref_s = w.frame.clone(), w.status.clone()
         for v in variants:

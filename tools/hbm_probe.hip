@@ -79,9 +79,27 @@ __global__ __launch_bounds__(256) void k_tilecopy(const uint4 *__restrict__ s, u
     }
 }
 
+// The C4 ceiling (round 5): the encode's exact 16-B chunks as a grid-stride
+// gather-copy -- destination chunk j of a precomputed list (every chunk the encode writes: the frame's
+// chunks up to its PAD128 end, 1536-B slots) takes source chunk sidx[j] (the payload chunk whose bytes
+// land there; ~0 for header / pad chunks).  Plain aligned copies: no funnel, no header, no MD5 (wrong
+// bytes); the list's 4 B per chunk are extra reads the kernel does not have.
+__global__ __launch_bounds__(256) void k_gather16(const uint4 *__restrict__ s, uint4 *__restrict__ d,
+                                                  const uint32_t *__restrict__ didx, const uint32_t *__restrict__ sidx,
+                                                  uint64_t n) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) d[didx[i]] = s[sidx[i]];
+}
+
 }  // namespace
 
 extern "C" {
+// the gather-copy above over n listed chunks (didx / sidx: 16-B chunk indices into dst / src)
+int probe_gather(void *src, void *dst, const void *didx, const void *sidx, uint64_t n, int grid, void *stream) {
+    hipLaunchKernelGGL(k_gather16, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const uint4 *)src, (uint4 *)dst,
+                       (const uint32_t *)didx, (const uint32_t *)sidx, n);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 // each wave copies a contiguous tile of tile_bytes (multiple of 16)
 int probe_tile(int unroll, void *src, void *dst, uint64_t bytes, uint32_t tile_bytes, void *stream) {
     const uint64_t n = bytes / 16u;
