@@ -42,7 +42,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # tag modes (rsk_set_tag_mode): the headline computes MD5 per lane, as the reference does per packet
 TAG_LABEL = {"md5": "md5_per_lane", "table": "tag_table_lut"}
 # rsk__last_encode_path: the library picks the encode path per call (rsk_encode_batch, enc_path)
-ENC_PATH_TEXT = {1: "k_encode", 2: "k_encode_heads + k_encode_copy (two-pass, one wave per packet)",
+ENC_PATH_TEXT = {1: "k_encode", 2: "k_encode_heads + k_encode_copy (two-pass, {k} packet(s) per copy wave)",
                  3: "k_encode (short frames: every set on the flat chunk list)"}
 TAG_TEXT = {"md5": "one MD5 compression per packet and lane",
             "table": "lookup in the key's 256-entry tag table staged in LDS (MD5 run once per key, 256 tags)"}
@@ -361,7 +361,7 @@ def main() -> None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed_max = float(t.item())
 
-    enc_path = ENC_PATH_TEXT.get(cx.last_encode_path, "?")
+    enc_path = ENC_PATH_TEXT.get(cx.last_encode_path, "?").format(k=cx.last_copy_k)
     enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
     total_pkts = (n_total if strong else world * d.n) * args.steps

@@ -144,15 +144,12 @@ int rsk_get_tag_mode(const rsk_ctx *ctx);
  *   RSK_ENC_PATH_TWO_PASS a header pass (MD5 tags 64 to a wave, 32-B records in the stream's scratch),
  *                         then one wave per packet (batches of long frames);
  *   RSK_ENC_PATH_SHORT    the per-set kernel with every set on the flat chunk list (batches of short
- *                         frames; AUTO takes it when the last sampled mean payload is <= 160 B);
- *   RSK_ENC_PATH_FUSED    one launch: per group of ~63 packets one header wave (MD5 tags 64 to a wave,
- *                         header chunks stored in place) beside copy waves of 1, 2 or 4 packets each.
+ *                         frames; AUTO takes it when the last sampled mean payload is <= 160 B).
  * Read when a call is issued, as the tag mode; RSK_EINVAL for an unknown path. */
 #define RSK_ENC_PATH_AUTO 0
 #define RSK_ENC_PATH_PER_SET 1
 #define RSK_ENC_PATH_TWO_PASS 2
 #define RSK_ENC_PATH_SHORT 3
-#define RSK_ENC_PATH_FUSED 4
 int rsk_set_encode_path(rsk_ctx *ctx, int path);
 
 /* Streams: a context may be used from several streams at once.  Its device scratch (compaction

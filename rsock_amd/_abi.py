@@ -62,7 +62,7 @@ class EncodeOut(ctypes.Structure):
 
 ENC_ZERO_PAD16 = 0x1
 ENC_ZERO_PAD128 = 0x2
-ENC_PATH_AUTO, ENC_PATH_PER_SET, ENC_PATH_TWO_PASS, ENC_PATH_SHORT, ENC_PATH_FUSED = 0, 1, 2, 3, 4
+ENC_PATH_AUTO, ENC_PATH_PER_SET, ENC_PATH_TWO_PASS, ENC_PATH_SHORT = 0, 1, 2, 3
 
 
 class WireIn(ctypes.Structure):

@@ -263,25 +263,30 @@ class Codec:
     def set_encode_path(self, path: int) -> None:
         """rsk_set_encode_path for output_batch: 0 = chosen per call from the last sampled batch's mean
         payload (default), 1 = the per-set kernel k_encode, 2 = the two-pass form for long frames
-        (k_encode_heads + one wave per packet, k_encode_copy), 3 = the short-frame kernel (k_encode
-        with every set on the flat chunk list), 4 = the fused form (k_encode_fused: header waves beside
-        copy waves of 1 / 2 / 4 packets, one launch).  Every path gives identical bytes."""
+        (k_encode_heads, then k_encode_copy: 1 / 2 / 4 packets per wave, set_copy_k), 3 = the short-frame
+        kernel (k_encode with every set on the flat chunk list).  Every path gives identical bytes."""
         _check(lib().rsk_set_encode_path(self._ctx, path), "rsk_set_encode_path")
 
     @property
     def last_encode_path(self) -> int:
-        """The path the last output_batch took (1 .. 4 as set_encode_path; 0 before any)."""
+        """The path the last output_batch took (1 .. 3 as set_encode_path; 0 before any)."""
         fn = lib().rsk__last_encode_path
         fn.argtypes = [ctypes.c_void_p]
         return int(fn(self._ctx))
 
-    def set_fused(self, k: int = 0, nt: int = 3) -> None:
-        """Internal knob of the fused encode path (rsk__set_fused): k packets per copy wave (1, 2, 4; 0 =
-        chosen from the last sampled mean payload) and the copy waves' store policy nt (bit 0
-        nontemporal loads, bit 1 nontemporal stores; 0, 2 or 3)."""
-        fn = lib().rsk__set_fused
-        fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
-        _check(fn(self._ctx, k, nt), "rsk__set_fused")
+    @property
+    def last_copy_k(self) -> int:
+        """Packets per copy wave of the last two-pass output_batch (1, 2, 4; 0 before any)."""
+        fn = lib().rsk__last_copy_k
+        fn.argtypes = [ctypes.c_void_p]
+        return int(fn(self._ctx))
+
+    def set_copy_k(self, k: int = 0) -> None:
+        """Internal knob of the two-pass encode (rsk__set_copy_k): packets per copy wave (1, 2, 4; 0 = chosen
+        from the last sampled mean payload: 1 for long frames, 4 below 960 B)."""
+        fn = lib().rsk__set_copy_k
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        _check(fn(self._ctx, k), "rsk__set_copy_k")
 
     def set_two_pass_chunk(self, packets: int = 0) -> None:
         """Internal knob of the two-pass encode (rsk__set_two_pass_chunk): header pass then copy per chunk
@@ -289,12 +294,6 @@ class Codec:
         fn = lib().rsk__set_two_pass_chunk
         fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
         _check(fn(self._ctx, packets), "rsk__set_two_pass_chunk")
-
-    def set_copy_cap(self, cap: int = 0) -> None:
-        """Internal A/B knob (rsk__set_copy_cap): at most `cap` two-pass copy blocks per CU (0 = no limit)."""
-        fn = lib().rsk__set_copy_cap
-        fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
-        _check(fn(self._ctx, cap), "rsk__set_copy_cap")
 
     def set_send_seq_groupby(self, v: int) -> None:
         """Internal knob for rsk_tcp_send_seq_batch: 0 the per-tile table path when n_conn < 2048

@@ -32,12 +32,10 @@ struct rsk_ctx {
     // encode path (rsk_encode_batch): 0 = chosen per call from the previous batch's statistic, else
     // RSK_ENC_PATH_* (rsk_set_encode_path)
     int enc_path = 0;
-    int fused_k = 0, fused_nt = 3, fused_hv = 0;  // the fused form's packets per copy wave / store policy /
-                                                  // header-store variant (rsk__set_fused)
-    int copy_k = 0;  // the two-pass copy's packets per wave (0: 1)
-    int copy_cap = 0;  // A/B: two-pass copy blocks per CU (rsk__set_copy_cap)
+    int copy_k = 0;  // the two-pass copy's packets per wave (0: by the sampled mean payload; rsk__set_copy_k)
     uint32_t tp_chunk = 0;  // the two-pass form's chunk of packets (0: whole batch; rsk__set_two_pass_chunk)
     std::atomic<int> enc_last_path{0};  // the path the last rsk_encode_batch took (rsk__last_encode_path)
+    std::atomic<int> enc_last_k{0};     // its packets per copy wave, two-pass form (rsk__last_copy_k)
     // set once any call of this context was captured into a graph: its replays may run on streams the
     // context never saw, so rsk_check_device_errors waits for the device instead of its streams
     std::atomic<bool> captured{false};

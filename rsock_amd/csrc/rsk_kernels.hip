@@ -185,21 +185,25 @@ __device__ __forceinline__ void encode_tag(const EncArgs &a, const KeySched &ks,
 
 // The batch statistic behind the next calls' choice of encode path (rsk_encode_batch, enc_path): one
 // wave reads pay_len at 64 evenly spaced packets and stores their mean payload length (bit 31 set:
-// valid) to a host-mapped word of the context.  k_encode_heads does it in its block 0; calls that take
-// the per-set kernel launch k_enc_sample now and then (the per-set kernel itself carries no extra
+// valid) to a host-mapped word of the context.  k_encode_heads does it in its block 0; calls on the
+// other paths launch k_enc_sample behind the encode (the per-set kernel itself carries no extra
 // argument: one more pointer in its arguments cost C4 12 % through SGPR spills, gpurun_out/r04o).
 constexpr uint32_t kStatValid = 0x80000000u;
-// the two-pass form's batches (enc_path): at least this many packets whose previous batch's sampled
-// mean payload was at least this long (C3's 1400 B take it; C4's mixed lengths, mean ~700 B, and
-// C2's 64 B keep the per-set kernel: one packet per wave idles their lanes).  Measured crossover
-// (profiles/r04aa_path_threshold.json): two-pass +6 % at a uniform 900 B, -6.5 % at 1000 B.
+// AUTO's choice (rsk_encode_batch, enc_path / copy_k): batches of at least kTwoPassMinPackets by the mean
+// payload of the context's last sampled batch (below that, and before any sample, the per-set kernel).
+// Measured on uniform and mixed lengths, 2M packets per case, one process per box
+// (tools/path_threshold.py, profiles/r05_path_threshold.json): the per-set kernel is fastest up to a
+// mean of ~200 B, except C2's 64 B where the short-frame kernel is (profiles/r05_enc_paths.json); the
+// short-frame kernel (every set on the flat chunk list) at 250-350 B, where the per-set kernel's sets
+// cross its 256-B flat limit; the two-pass form with 4 packets per copy wave from 450 B (and C4's
+// mixed 64-1400 B), 2 packets around 900-1100 B and mixed 700-1400 B, 1 packet from 1200 B (C3).
 constexpr uint32_t kTwoPassMinPackets = 16384;
-[[maybe_unused]] constexpr uint64_t kCopyMaxPackets = 1ull << 25;  // per k_encode_copy launch (2^31 work-items)
-constexpr uint32_t kTwoPassMinPayload = 960;
-constexpr uint64_t kFusedMaxGroups = 1ull << 19;  // per k_encode_fused launch (<= 2^25 waves, 2^31 work-items)
-// batches whose sampled mean payload is at most this take the flat-only per-set kernel (RSK_ENC_PATH_SHORT):
-// every set of such a batch has a mean frame under the flat path's 256 B (kFlatBelowMeanBytes) anyway
-[[maybe_unused]] constexpr uint32_t kFlatMaxPayload = 160;
+constexpr uint32_t kAutoShortMax = 96;     // mean payload <= this: the short-frame kernel (C2)
+constexpr uint32_t kAutoPerSetBelow = 224;  // .. below this: the per-set kernel
+constexpr uint32_t kAutoShortBelow = 400;   // .. below this: the short-frame kernel again
+constexpr uint32_t kAutoK4Below = 880;      // .. below this: two-pass, 4 packets per copy wave (C4)
+constexpr uint32_t kAutoK2Below = 1160;     // .. below this: two-pass, 2 packets per copy wave; above: 1 (C3)
+constexpr uint64_t kCopyMaxPackets = 1ull << 25;  // per k_encode_copy launch (2^31 work-items)
 __device__ __forceinline__ void enc_sample(const uint16_t *pay_len, uint32_t n, uint32_t *stat) {
     if (stat == nullptr || blockIdx.x != 0u || threadIdx.x >= 64u) return;  // one wave of block 0
     uint32_t v = pay_len[((uint64_t)threadIdx.x * n) >> 6];
@@ -945,7 +949,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_heads(EncArgs a, KeySched ks,
     }
 }
 
-// ---- K packets per wave, one wave-instruction stream: the copy of the two-pass and fused forms -------
+// ---- K packets per wave, one wave-instruction stream: the two-pass form's copy ------------------------
 // Issue: lanes 0..K-1 load the K packets' pay_len / pay_off / frame_off together (ONE dependent round
 // trip for all descriptors; pay_len has no scalar 16-bit load, and a vector load per packet made the
 // compiler wait for every earlier packet's chunk loads before the next packet's descriptors -- K
@@ -960,7 +964,7 @@ struct CopyK {
     uint32_t flen[K];  // frame bytes counted from g.d0 (31 + P + r); 0: packet not framed
 };
 
-template <int K, int NT, bool CL = true>
+template <int K, int NT>
 __device__ __forceinline__ void copyk_issue(const EncArgs &a, uint64_t i0, uint32_t lane, CopyK<K> &c) {
     uint32_t dP = 0;
     uint64_t dpo = 0, dfo = 0;
@@ -1008,20 +1012,14 @@ __device__ __forceinline__ void copyk_issue(const EncArgs &a, uint64_t i0, uint3
             c.A[p][q] = make_uint4(0u, 0u, 0u, 0u);
             if (!on || m_hi < m_lo || (q == 1 && c.g[p].nst < 64u)) continue;  // uniform
             const int32_t m = (int32_t)(lane + 64u * q) - 2;
-            if constexpr (CL) {
-                const int32_t mc = m < m_lo ? m_lo : m > m_hi ? m_hi : m;
-                c.A[p][q] = ld16<NT>(c.g[p].srcp + 16 * mc);  // uniform base + lane offset
-            } else {  // A/B: exec-masked loads of the live chunks only
-                if (m >= m_lo && m <= m_hi) c.A[p][q] = ld16<NT>(c.g[p].srcp + 16 * m);
-            }
+            const int32_t mc = m < m_lo ? m_lo : m > m_hi ? m_hi : m;
+            c.A[p][q] = ld16<NT>(c.g[p].srcp + 16 * mc);  // uniform base + lane offset
         }
     }
 }
 
-// Store packet p's chunks: TAG (two-pass) every chunk incl. the header chunks from the packet's 8
-// header words Hj; !TAG (fused) only chunks k >= 2 (chunk 2 from its first payload byte), the header
-// wave stores the rest.
-template <int K, int NT, bool TAG>
+// Store packet p's chunks, the header chunks from the packet's 8 header words Hj (its pass-1 record).
+template <int K, int NT>
 __device__ __forceinline__ void copyk_store(const EncArgs &a, const CopyK<K> &c, int p, uint32_t lane,
                                             const uint32_t (&Hj)[8]) {
     const FrameGeo &g = c.g[p];
@@ -1041,14 +1039,9 @@ __device__ __forceinline__ void copyk_store(const EncArgs &a, const CopyK<K> &c,
         const uint32_t k = lane + 64u * q;
         if (q == 1 && nst <= 64u) continue;  // uniform
         const uint4 V = rsk::funnel16(c.A[p][q], B[q], g.sh);
-        if constexpr (TAG) {
-            const uint4 v = k < (g.r >= 2u ? 3u : 2u) ? head_chunk(Hj, k, g.r, V) : V;
-            if (k >= nst) continue;
-            store_piece<NT>(g.d0 + 16u * k, v, k == 0u ? g.r : 0u, (int)fl - 16 * (int)k, a.pad != 0u);
-        } else {
-            if (k >= nst || k < 2u) continue;
-            store_piece<NT>(g.d0 + 16u * k, V, k == 2u ? chunk2_lo(g.r) : 0u, (int)fl - 16 * (int)k, a.pad != 0u);
-        }
+        const uint4 v = k < (g.r >= 2u ? 3u : 2u) ? head_chunk(Hj, k, g.r, V) : V;
+        if (k >= nst) continue;
+        store_piece<NT>(g.d0 + 16u * k, v, k == 0u ? g.r : 0u, (int)fl - 16 * (int)k, a.pad != 0u);
     }
 }
 
@@ -1059,118 +1052,22 @@ __device__ __forceinline__ void copyk_store(const EncArgs &a, const CopyK<K> &c,
 // ~2 G waves/s), so short frames need several per wave to keep the memory system busy.
 // base: the launch's first packet (a grid is limited to 2^32 - 1 work-items, i.e. 2^26 packets at 64
 // per packet: larger batches take several launches, kCopyMaxPackets each).
-template <int NT, int K = 1, bool CL = true>
+template <int NT, int K = 1>
 __global__ __launch_bounds__(kBlock) void k_encode_copy(EncArgs a, const uint32_t *heads, uint64_t base = 0) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const uint64_t i0 = base + ((uint64_t)blockIdx.x * kWavesPerBlock + w) * K;
     if (i0 >= a.n) return;
     CopyK<K> c;
-    copyk_issue<K, NT, CL>(a, i0, lane, c);
+    copyk_issue<K, NT>(a, i0, lane, c);
 #pragma unroll
     for (int p = 0; p < K; ++p) {
         if (!c.flen[p]) continue;  // uniform
         uint32_t Hj[8];
 #pragma unroll
         for (int t = 0; t < 8; ++t) Hj[t] = heads[8 * (i0 + p) + t];  // uniform address: scalar loads
-        copyk_store<K, NT, true>(a, c, p, lane, Hj);
+        copyk_store<K, NT>(a, c, p, lane, Hj);
     }
-}
-
-// ---- the two-pass form in ONE launch (round 5): header waves interleaved with copy waves ----------
-// The two-pass form's cost beyond its copy is the header pass: 0.15 ms on C3, bound by the rate of
-// its scattered payload[0] sector reads while the chip does nothing else, plus the records written
-// and read back (0.27 GB) and the first payload line fetched by both passes.  Here the
-// grid is cut into groups of G packets; wave 0 of a group is its HEADER wave (one lane per packet:
-// status, payload[0], the MD5 tag -- 64 compressions per wave instruction stream, as in pass 1 --
-// EncHead, and the header chunks stored straight into the frames, store_head), the other G / K waves
-// are COPY waves, K packets each (descriptors by scalar loads, every chunk load of the K packets
-// issued before any store, the DPP funnel of k_encode_copy, payload chunks k >= 2 only).  No wave
-// waits for another: a frame's first 32 bytes and the rest are written by two waves, as neighbouring
-// frames already share their boundary lines.  The header wave runs beside its group's copy waves, so
-// its latency-bound byte loads overlap the copy's bandwidth and hit the lines the copy waves fetch
-// at the same moment, and no records exist.  K = 1 for long frames (C3); K = 2 / 4 give a copy wave
-// the bytes in flight of a long frame on mid-length batches (C4).
-template <int K>
-struct FusedGeo {
-    static constexpr uint32_t G = K == 1 ? 63u : K == 2 ? 62u : K == 3 ? 63u : 60u;  // packets per group
-    static constexpr uint32_t WPG = 1u + G / K;                                    // waves per group
-    static_assert(G % K == 0 && G <= 64u, "group geometry");
-};
-
-// HV (header-store variants, measured): bit 0 -- aligned frames' 32 header bytes stored by lane pairs
-// (lane 2j chunk 0, lane 2j + 1 chunk 1 of packet j: one 32-B piece per packet per instruction instead
-// of two 16-B stores from one lane); bit 1 -- nontemporal header stores; bit 2 -- XCD grouping: a
-// group's blocks all have the same blockIdx % 8 (one XCD, one L2, under round-robin placement: speed
-// only), so the header bytes and the rest of a frame's first line meet in one L2.
-template <int HV>
-__device__ __forceinline__ void fused_store_heads(const EncArgs &a, const Lane1 &L, uint32_t lane, uint32_t G) {
-    const bool al = L.st <= 0 || (reinterpret_cast<uintptr_t>(a.frame + L.fo) & 15u) == 0u;
-    if (!(HV & 1) || __ballot(!al) != 0ull) {
-        if (L.st > 0) store_head(L.H, a.frame + L.fo);
-        return;
-    }
-    const uint32_t h = lane & 1u;
-#pragma unroll
-    for (int rd = 0; rd < 2; ++rd) {
-        const uint32_t j = (lane >> 1) + 32u * rd;
-        uint32_t v[8];
-#pragma unroll
-        for (int t = 0; t < 8; ++t) v[t] = (uint32_t)__shfl((int)L.H[t], (int)j);
-        const int32_t st = __shfl(L.st, (int)j);
-        const uint64_t fo = shfl64(L.fo, j);
-        const uint4 w4 = h ? make_uint4(v[4], v[5], v[6], v[7]) : make_uint4(v[0], v[1], v[2], v[3]);
-        if (j < G && st > 0) st16<(HV & 2) ? 2 : 0>(a.frame + fo + 16u * h, w4);
-    }
-}
-
-template <int K, int NT, int HV>
-__device__ __forceinline__ void encode_fused(const EncArgs &a, const KeySched &ks, uint32_t *stat, uint64_t gbase) {
-    using FG = FusedGeo<K>;
-    stage_tags(ks);  // RSK_TAG_TABLE: every wave of the block takes the barrier before any exit
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    uint64_t grp;
-    uint32_t role;
-    if constexpr (HV & 4) {
-        constexpr uint32_t BPG = FG::WPG / kWavesPerBlock;  // blocks per group
-        static_assert(FG::WPG % kWavesPerBlock == 0, "whole blocks per group");
-        const uint32_t x = blockIdx.x % 8u, j = blockIdx.x / 8u;
-        grp = gbase + (uint64_t)(j / BPG) * 8u + x;
-        role = (j % BPG) * kWavesPerBlock + wv;
-    } else {
-        const uint64_t w = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
-        grp = gbase + w / FG::WPG;
-        role = (uint32_t)(w % FG::WPG);
-    }
-    const uint64_t g0 = grp * FG::G;
-    if (g0 >= a.n) return;  // wave-uniform
-    if (role == 0u) {
-        // header wave: lane j frames packet g0 + j (j < G)
-        if (blockIdx.x == 0u) enc_sample(a.pay_len, a.n, stat);  // group 0's header wave (wave 0 of block 0)
-        const uint64_t i = g0 + lane;
-        const Lane1 L = encode_phase1<true, true>(a, ks, lane < FG::G && i < a.n ? i : a.n);
-        fused_store_heads<HV>(a, L, lane, FG::G);
-        return;
-    }
-    const uint64_t i0 = g0 + (uint64_t)(role - 1u) * K;
-    CopyK<K> c;
-    copyk_issue<K, NT>(a, i0, lane, c);
-    const uint32_t none[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int p = 0; p < K; ++p)
-        if (c.flen[p]) copyk_store<K, NT, false>(a, c, p, lane, none);  // uniform
-}
-
-// HV bit 3: held to 8 waves per SIMD (the key schedule's SGPRs otherwise allow 7)
-template <int K, int NT, int HV = 0>
-__global__ __launch_bounds__(kBlock) void k_encode_fused(EncArgs a, KeySched ks, uint32_t *stat, uint64_t gbase) {
-    encode_fused<K, NT, HV>(a, ks, stat, gbase);
-}
-template <int K, int NT, int HV = 0>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_encode_fused8(
-    EncArgs a, KeySched ks, uint32_t *stat, uint64_t gbase) {
-    encode_fused<K, NT, HV>(a, ks, stat, gbase);
 }
 
 // Grouped-interleave mapping (shipped: GRP 8, SBW 1024).  A super-block of SBW consecutive waves owns
@@ -3168,32 +3065,21 @@ int rsk_release_stream(rsk_ctx *c, void *stream) {
 // Encode path of this context's calls (rsk_codec.h): RSK_ENC_PATH_AUTO (chosen per call, enc_path),
 // RSK_ENC_PATH_PER_SET (k_encode), RSK_ENC_PATH_TWO_PASS (k_encode_heads + k_encode_copy).
 int rsk_set_encode_path(rsk_ctx *c, int path) {
-    if (!c || path < RSK_ENC_PATH_AUTO || path > RSK_ENC_PATH_FUSED) return RSK_EINVAL;
+    if (!c || path < RSK_ENC_PATH_AUTO || path > RSK_ENC_PATH_SHORT) return RSK_EINVAL;
     c->enc_path = path;
     return RSK_OK;
 }
 
-// Internal (tests, tools): the fused form's packets per copy wave k (1, 2, 4; 0 = from the sampled mean
-// payload) and its copy waves' store policy nt (bit 0 nontemporal loads, bit 1 nontemporal stores).
-int rsk__set_fused(rsk_ctx *c, int k, int nt) {
-    const int hv = nt >> 4;  // header-store variant (k_encode_fused HV) in bits 4..7
-    nt &= 15;  // bit 3: the two-pass copy with exec-masked loads (A/B)
-    if (!c || !(k == 0 || k == 1 || k == 2 || k == 4) || !((nt & 7) == 0 || (nt & 7) == 2 || (nt & 7) == 3) ||
-        !(hv == 0 || hv == 1 || hv == 3 || hv == 4 || hv == 5 || hv == 7 || hv == 9))
-        return RSK_EINVAL;
-    c->fused_k = k;
-    c->fused_nt = nt;
-    c->fused_hv = hv;
-    c->copy_k = k;  // the two-pass copy's packets per wave too
+// Internal (tests, tools): the two-pass copy's packets per wave k (1, 2, 4; 0 = from the sampled mean
+// payload, copy_k below).
+int rsk__set_copy_k(rsk_ctx *c, int k) {
+    if (!c || !(k == 0 || k == 1 || k == 2 || k == 4)) return RSK_EINVAL;
+    c->copy_k = k;
     return RSK_OK;
 }
 
-// Internal (tools): at most `cap` two-pass copy blocks per CU (0: no limit), by unused dynamic LDS (A/B).
-int rsk__set_copy_cap(rsk_ctx *c, int cap) {
-    if (!c || cap < 0 || cap > 16) return RSK_EINVAL;
-    c->copy_cap = cap;
-    return RSK_OK;
-}
+// Internal (tests, bench): packets per copy wave of the context's last two-pass encode (0 before any).
+int rsk__last_copy_k(const rsk_ctx *c) { return c ? c->enc_last_k.load(std::memory_order_relaxed) : RSK_EINVAL; }
 
 // Internal (tests, tools): the two-pass form in chunks of `packets` (0: the whole batch in one pass each)
 int rsk__set_two_pass_chunk(rsk_ctx *c, uint32_t packets) {
@@ -3260,27 +3146,33 @@ int rsk_reserve_stream(rsk_ctx *c, uint32_t n_max, void *stream) {
     return RSK_OK;
 }
 
-// Encode path per call: the context's forced path (rsk_set_encode_path), else the two-pass form for
-// batches of at least kTwoPassMinPackets when the context's last sampled batch (enc_sample: every
-// two-pass call, and k_enc_sample behind the first and every kSampleEvery-th per-set call) had a mean
-// payload of at least kTwoPassMinPayload bytes, else the per-set kernel.  The first call on a context
-// has no statistic yet and takes the per-set kernel; either path gives identical bytes.
-// packets per copy wave of the fused form: forced (rsk__set_fused), else from the sampled mean payload
-static int fused_k(rsk_ctx *c) {
-    if (c->fused_k) return c->fused_k;
+// The batch statistic behind AUTO (enc_sample: k_encode_heads in every two-pass call, k_enc_sample
+// behind every other uncaptured call of >= kTwoPassMinPackets packets).  The first call on a context
+// has no statistic yet and takes the per-set kernel; every path gives identical bytes.
+// The context's last sampled mean payload (bit 31 set: valid), or 0.
+static uint32_t sampled_mean(const rsk_ctx *c) {
     const uint32_t s = c->enc_stat_host ? __atomic_load_n(c->enc_stat_host, __ATOMIC_RELAXED) : 0u;
-    const uint32_t mean = (s & kStatValid) ? s & ~kStatValid : 1400u;
-    return mean >= 960u ? 1 : mean >= 480u ? 2 : 4;
+    return s;
 }
 
-[[maybe_unused]] static int enc_path(rsk_ctx *c, uint32_t n) {
+// packets per copy wave of the two-pass form: forced (rsk__set_copy_k), else by the sampled mean payload
+static int copy_k(rsk_ctx *c) {
+    if (c->copy_k) return c->copy_k;
+    const uint32_t s = sampled_mean(c);
+    const uint32_t mean = (s & kStatValid) ? s & ~kStatValid : 1400u;
+    return mean < kAutoK4Below ? 4 : mean < kAutoK2Below ? 2 : 1;
+}
+
+// Encode path per call: the context's forced path (rsk_set_encode_path), else AUTO's table above.
+static int enc_path(rsk_ctx *c, uint32_t n) {
     if (c->enc_path) return c->enc_path;
-    const uint32_t s = c->enc_stat_host ? __atomic_load_n(c->enc_stat_host, __ATOMIC_RELAXED) : 0u;
+    const uint32_t s = sampled_mean(c);
     if (n < kTwoPassMinPackets || !(s & kStatValid)) return RSK_ENC_PATH_PER_SET;
     const uint32_t mean = s & ~kStatValid;
-    return mean >= kTwoPassMinPayload ? RSK_ENC_PATH_TWO_PASS
-           : mean <= kFlatMaxPayload  ? RSK_ENC_PATH_SHORT
-                                      : RSK_ENC_PATH_PER_SET;
+    return mean <= kAutoShortMax      ? RSK_ENC_PATH_SHORT
+           : mean < kAutoPerSetBelow  ? RSK_ENC_PATH_PER_SET
+           : mean < kAutoShortBelow   ? RSK_ENC_PATH_SHORT
+                                      : RSK_ENC_PATH_TWO_PASS;
 }
 
 int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_encode_out *out,
@@ -3312,7 +3204,7 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         // the two-pass form (batches of long frames): header records, then one wave per packet
         void *hp = nullptr;
         if (rsk::stream_ws_if(c, st, rsk::WS_ENC, 32ull * n, &hp) == RSK_OK) {
-            const int ck = c->copy_k ? c->copy_k : 1;
+            const int ck = copy_k(c);
             // chunked (rsk__set_two_pass_chunk): heads then copy per chunk, so a chunk's records and
             // first payload lines may still be in the Infinity Cache when its copy reads them
             const uint64_t chunk = c->tp_chunk ? c->tp_chunk : (uint64_t)n;
@@ -3325,52 +3217,16 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
                     const uint64_t m = ac.n - b0 < kCopyMaxPackets ? ac.n - b0 : kCopyMaxPackets;
                     const dim3 cg((unsigned)((m + 4ull * ck - 1ull) / (4ull * ck)));
                     const uint32_t *hr = static_cast<const uint32_t *>(hp);
-                    const bool cl = !(c->fused_nt & 8);
-                    // A/B (rsk__set_copy_cap): at most `cap` copy blocks per CU, by dynamic LDS
-                    const size_t lds = c->copy_cap ? (size_t)(163840 / (c->copy_cap + 1)) + 64 : 0;
-                    if (ck == 2) { if (cl) hipLaunchKernelGGL((k_encode_copy<3, 2>), cg, bd, lds, st, ac, hr, b0);
-                                   else hipLaunchKernelGGL((k_encode_copy<3, 2, false>), cg, bd, lds, st, ac, hr, b0); }
-                    else if (ck == 4) { if (cl) hipLaunchKernelGGL((k_encode_copy<3, 4>), cg, bd, lds, st, ac, hr, b0);
-                                        else hipLaunchKernelGGL((k_encode_copy<3, 4, false>), cg, bd, lds, st, ac, hr, b0); }
-                    else { if (cl) hipLaunchKernelGGL((k_encode_copy<3, 1>), cg, bd, lds, st, ac, hr, b0);
-                           else hipLaunchKernelGGL((k_encode_copy<3, 1, false>), cg, bd, lds, st, ac, hr, b0); }
+                    if (ck == 2) hipLaunchKernelGGL((k_encode_copy<3, 2>), cg, bd, 0, st, ac, hr, b0);
+                    else if (ck == 4) hipLaunchKernelGGL((k_encode_copy<3, 4>), cg, bd, 0, st, ac, hr, b0);
+                    else hipLaunchKernelGGL((k_encode_copy<3, 1>), cg, bd, 0, st, ac, hr, b0);
                 }
             }
             c->enc_last_path.store(2, std::memory_order_relaxed);
+            c->enc_last_k.store(ck, std::memory_order_relaxed);
             return launch_check("k_encode_heads / k_encode_copy");
         }
         g_last_error[0] = 0;  // no records (a capture that would grow them, or no memory): one pass
-    }
-    if (path == RSK_ENC_PATH_FUSED) {
-        // header waves interleaved with copy waves, one launch per 2^19 groups (2^31 work-items)
-        const int fk = fused_k(c), fnt = c->fused_nt;
-        for (uint64_t gb = 0; ; ) {
-            const uint32_t G = fk == 1 ? FusedGeo<1>::G : fk == 2 ? FusedGeo<2>::G : FusedGeo<4>::G;
-            const uint32_t WPG = fk == 1 ? FusedGeo<1>::WPG : fk == 2 ? FusedGeo<2>::WPG : FusedGeo<4>::WPG;
-            const uint64_t ng = (n + G - 1ull) / G;
-            if (gb >= ng) break;
-            const uint64_t m = std::min<uint64_t>(ng - gb, kFusedMaxGroups);
-            const int hv = c->fused_hv;
-            // XCD grouping (hv bit 2): whole rounds of 8 groups, one per blockIdx % 8
-            const uint64_t mb = hv & 4 ? (m + 7ull) / 8ull * 8ull : m;
-            const dim3 fg((unsigned)((mb * WPG + kWavesPerBlock - 1) / kWavesPerBlock));
-            uint32_t *sp = gb == 0 ? c->enc_stat_dev : nullptr;
-#define RSK_FUSED(KK, NN, HH) hipLaunchKernelGGL((k_encode_fused<KK, NN, HH>), fg, bd, 0, st, a, c->ks, sp, gb)
-#define RSK_FUSED_HV(KK, NN) \
-    switch (hv) { case 1: RSK_FUSED(KK, NN, 1); break; case 3: RSK_FUSED(KK, NN, 3); break; \
-                  case 4: RSK_FUSED(KK, NN, 4); break; case 5: RSK_FUSED(KK, NN, 5); break; \
-                  case 7: RSK_FUSED(KK, NN, 7); break; \
-                  case 9: hipLaunchKernelGGL((k_encode_fused8<KK, NN, 1>), fg, bd, 0, st, a, c->ks, sp, gb); break; \
-                  default: RSK_FUSED(KK, NN, 0); break; }
-            if (fk == 1) { if (fnt == 3) { RSK_FUSED_HV(1, 3) } else if (fnt == 2) { RSK_FUSED_HV(1, 2) } else { RSK_FUSED_HV(1, 0) } }
-            else if (fk == 2) { if (fnt == 3) { RSK_FUSED_HV(2, 3) } else { RSK_FUSED_HV(2, 0) } }
-            else { if (fnt == 3) { RSK_FUSED_HV(4, 3) } else { RSK_FUSED_HV(4, 0) } }
-#undef RSK_FUSED_HV
-#undef RSK_FUSED
-            gb += m;
-        }
-        c->enc_last_path.store(RSK_ENC_PATH_FUSED, std::memory_order_relaxed);
-        return launch_check("k_encode_fused");
     }
     if (path == RSK_ENC_PATH_SHORT) {
         // batches of short frames: the per-set kernel with every set on the flat chunk list, compiled

@@ -6,24 +6,24 @@ from __future__ import annotations
 
 import contextlib
 
-# (path, packets per copy wave of the fused form; 0 = not the fused form)
-#   1 = the per-set kernel k_encode; 2 = the two-pass form (k_encode_heads + k_encode_copy);
-#   3 = the short-frame kernel (every set on the flat chunk list); 4 = the fused form
-#   (k_encode_fused: header waves beside copy waves of k packets)
-ENC_PATHS = [(1, 0), (2, 0), (3, 0), (4, 1), (4, 2), (4, 4)]
+# (path, packets per copy wave of the two-pass form; 0 = not the two-pass form)
+#   1 = the per-set kernel k_encode; 2 = the two-pass form (k_encode_heads, then k_encode_copy with k
+#   packets per wave: 1 for long frames, 4 for mid-length ones); 3 = the short-frame kernel (every set
+#   on the flat chunk list)
+ENC_PATHS = [(1, 0), (2, 1), (2, 2), (2, 4), (3, 0)]
 
 
 def path_id(pk) -> str:
     p, k = pk
-    return f"path{p}" + (f"k{k}" if p == 4 else "")
+    return f"path{p}" + (f"k{k}" if p == 2 else "")
 
 
 @contextlib.contextmanager
 def held(codec, path: int, k: int = 0):
     """codec held to encode path `path` (and fused k); every output_batch inside asserts the path."""
     codec.set_encode_path(path)
-    if path == 4:
-        codec.set_fused(k)
+    if path == 2:
+        codec.set_copy_k(k)
     cls_fn = type(codec).output_batch
 
     def checked(*a, **kw):
@@ -37,4 +37,4 @@ def held(codec, path: int, k: int = 0):
     finally:
         del codec.output_batch
         codec.set_encode_path(0)
-        codec.set_fused(0)
+        codec.set_copy_k(0)

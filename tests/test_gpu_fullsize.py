@@ -44,25 +44,40 @@ def test_fullsize_roundtrip(pcodec, gpu, oracle, cfg, pad16):
     _roundtrip(pcodec, gpu, oracle, workload.describe(cfg), pad16)
 
 
+# what AUTO (path 0) takes for each BASELINE config once it has sampled one batch of it
+# (rsk_kernels.hip, enc_path / copy_k: by the sampled mean payload): (path, packets per copy wave)
+AUTO_EXPECT = {"c2": (3, 0), "c3": (2, 1), "c4": (2, 4)}
+
+
 def test_encode_path_choice(codec, gpu):
-    """Path 0 (the default) picks per call from the previous batch's sampled mean payload: both
-    paths give the same frames whichever the library picks, call after call (C3 long frames, then
-    C4's mixed lengths)."""
+    """Path 0 (the default) picks per call from the previous batch's sampled mean payload:
+    the frames are the same whichever path runs, and after ONE call of a new traffic mix the next call
+    takes that mix's path -- C2 then C3 then C4 then C2 then C3, each switch within one call."""
     import torch
 
-    for cfg in ("c3", "c4", "c3"):
+    ref = {}
+    for cfg in ("c3", "c4", "c2"):
         d = workload.describe(cfg, 0, 40_000, n=40_000)
         w = workload.DeviceWorkload(d, gpu)
-        frames = []
-        for path in (1, 0, 0, 2, 3):
-            codec.set_encode_path(path)
+        codec.set_encode_path(1)
+        w.frame.zero_()
+        codec.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
+                           w.status, id_uniform=workload.ID_UNIFORM, pad16=True)
+        torch.cuda.synchronize()
+        ref[cfg] = (w, w.frame.clone())
+    codec.set_encode_path(0)
+    for cfg in ("c2", "c3", "c4", "c2", "c3"):
+        w, rf = ref[cfg]
+        for call in range(2):
             w.frame.zero_()
-            codec.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame,
-                               w.frame_off, w.status, id_uniform=workload.ID_UNIFORM, pad16=True)
+            codec.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
+                               w.status, id_uniform=workload.ID_UNIFORM, pad16=True)
             torch.cuda.synchronize()
-            frames.append(w.frame.clone())
-        codec.set_encode_path(0)
-        assert all(torch.equal(frames[0], f) for f in frames[1:])
+            assert torch.equal(w.frame, rf), (cfg, call)
+        path, k = AUTO_EXPECT[cfg]
+        assert codec.last_encode_path == path, (cfg, codec.last_encode_path)
+        if path == 2:
+            assert codec.last_copy_k == k, (cfg, codec.last_copy_k)
 
 
 @pytest.mark.parametrize("rank", [7, 0])
@@ -165,11 +180,11 @@ def test_compaction_large_random(codec, gpu, oracle):
 
 
 def test_encode_paths_beyond_one_grid(codec, gpu, oracle):
-    """A batch of 2^26 + 4097 packets: one grid of the two-pass copy (64 work-items per packet) or of the
-    fused form (64 per packet + a header wave per group) would exceed the 2^32 - 1 work-items a grid may
-    hold (r04's C5-on-one-GPU run failed exactly there: "invalid configuration argument"), so both run
-    in several launches; every path's frames must equal the per-set kernel's, and the tags the oracle's
-    table at payload[0] (C2-shaped: ~11 GB of arenas)."""
+    """A batch of 2^26 + 4097 packets: one grid of the two-pass copy (64 work-items per packet, or per K
+    packets) would exceed the 2^32 - 1 work-items a grid may hold for K = 1 (r04's C5-on-one-GPU run
+    failed exactly there: "invalid configuration argument"), so the copy runs in launches of 2^25
+    packets; every path's frames must equal the per-set kernel's, and the tags the oracle's table at
+    payload[0] (C2-shaped: ~11 GB of arenas)."""
     import torch
 
     n = (1 << 26) + 4097
@@ -177,7 +192,7 @@ def test_encode_paths_beyond_one_grid(codec, gpu, oracle):
     d = workload.describe("c2", 0, n, n=n)
     w = workload.DeviceWorkload(d, gpu)
     ref = None
-    for pk in [(1, 0), (2, 0), (4, 1), (4, 2), (4, 4)]:
+    for pk in [(1, 0), (2, 1), (2, 4), (3, 0)]:
         with held(codec, *pk):
             w.frame.zero_()
             codec.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,

@@ -307,38 +307,43 @@ def test_two_pass_encode_two_streams(codec, gpu):
         assert torch.equal(w.frame, f) and torch.equal(w.status, st)
 
 
-def test_fused_encode_in_captured_graph(gpu):
-    """The fused encode (header waves beside copy waves, one launch, no scratch) captured into a hipGraph
-    on a stream that was never reserved, replayed: the per-set kernel's bytes, for every copy-wave size."""
+def test_two_pass_copy_k_in_captured_graph(gpu):
+    """The two-pass encode with 1, 2 and 4 packets per copy wave, in several chunks of heads / copy
+    (rsk__set_two_pass_chunk: each chunk's launches start at a packet offset), captured into a hipGraph on
+    a reserved stream and replayed: the per-set kernel's bytes."""
     import torch
 
     from rsock_amd.codec import Codec
 
-    n = 1 << 17
-    d = workload.describe("c3", 0, n, n=n)
+    n = (1 << 17) + 77
+    d = workload.describe("c4", 0, n, n=n)
     w = workload.DeviceWorkload(d, gpu)
     cx = Codec(b"hello135", 0)
     try:
         ref_f, ref_s = _c3_frames(cx, gpu, w, 1)
-        for k in (1, 2, 4):
+        for k, chunk in ((1, 0), (2, 50_000), (4, 0), (4, 33_333)):
             s = torch.cuda.Stream(gpu)
-            cx.set_encode_path(4)
-            cx.set_fused(k)
+            cx.set_encode_path(2)
+            cx.set_copy_k(k)
+            cx.set_two_pass_chunk(chunk)
+            cx.reserve(n, stream=s)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=s):
                 cx.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
                                 w.status, id_uniform=workload.ID_UNIFORM, pad16=True, stream=s)
-            assert cx.last_encode_path == 4
+            assert cx.last_encode_path == 2
             for _ in range(2):
                 w.frame.zero_()
                 w.status.fill_(-9)
                 torch.cuda.synchronize()
                 g.replay()
                 torch.cuda.synchronize()
-                assert torch.equal(w.frame, ref_f) and torch.equal(w.status, ref_s)
+                assert torch.equal(w.frame, ref_f) and torch.equal(w.status, ref_s), (k, chunk)
             del g
+            cx.release_stream(s)
         cx.set_encode_path(0)
-        cx.set_fused(0)
+        cx.set_copy_k(0)
+        cx.set_two_pass_chunk(0)
         assert cx.check_device_errors() == 0  # a captured context waits for the device here
     finally:
         cx.close()

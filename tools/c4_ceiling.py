@@ -80,8 +80,7 @@ def main():
     for v in args.paths.split(","):
         f = [int(x) for x in v.split(":")]
         cx.set_encode_path(f[0])
-        if len(f) > 1:
-            cx.set_fused(f[1], 3)
+        cx.set_copy_k(f[1] if len(f) > 1 else 0)
         ms = timeit(lambda: cx.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame,
                                             w.frame_off, w.status, id_uniform=workload.ID_UNIFORM, pad128=True))
         out["rows"][f"encode_path{v}"] = {"ms": round(ms, 4), "alg_TBs": round(alg / ms / 1e9, 3)}

@@ -1,8 +1,7 @@
 #!/usr/bin/env python3
 """In-process A/B of rsk_encode_batch's paths on one config (device-resident, HIP events on the launch
-stream, interleaved rounds): each variant = (encode path, fused packets per copy wave k, fused store
-policy nt).  Every variant's frames and statuses are compared with the per-set kernel's before timing.
-    python tools/enc_paths_ab.py --config c3 [--variants 1,2,4:1:3,4:1:2] [--rounds 6] [--reps 10]
+stream, interleaved rounds): each variant = (encode path, two-pass packets per copy wave k, two-pass chunk).  Every variant's frames and statuses are compared with the per-set kernel's before timing.
+    python tools/enc_paths_ab.py --config c3 [--variants 1,2:1,2:4,2:1:1048576] [--rounds 6] [--reps 10]
                                  [--layout slots|packed|odd] [--pad 16|128|0]
 One JSON line: per variant the median over rounds of the mean encode time, and its fraction of 8 TB/s
 by the algorithmic bytes (2P + 66 per packet)."""
@@ -17,19 +16,17 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def parse_variant(v):
-    """path[:k[:nt[:chunk[:cap]]]] -- k packets per copy wave (paths 2, 4), nt store policy + header variant
-    << 4 (path 4), chunk packets per heads / copy pair (path 2; 0 = the whole batch), cap copy blocks per CU
-    (path 2; 0 = no limit)"""
+    """path[:k[:chunk]] -- k packets per copy wave (path 2; 0 = chosen by the library), chunk packets per
+    heads / copy pair (path 2; 0 = the whole batch)"""
     f = [int(x) for x in v.split(":")]
-    return (f[0], f[1] if len(f) > 1 else 0, f[2] if len(f) > 2 else 3, f[3] if len(f) > 3 else 0,
-            f[4] if len(f) > 4 else 0)
+    return (f[0], f[1] if len(f) > 1 else 0, f[2] if len(f) > 2 else 0)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3")
     ap.add_argument("--packets", type=int, default=0)
-    ap.add_argument("--variants", default="1,2,4:1:3")
+    ap.add_argument("--variants", default="1,2:1,2:4")
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--layout", default="slots", choices=["slots", "packed", "odd"],
@@ -65,18 +62,16 @@ def main():
     variants = [parse_variant(v) for v in args.variants.split(",")]
 
     def run(v):
-        p, k, nt, chunk, cap = v
+        p, k, chunk = v
         cx.set_encode_path(p)
-        if p in (2, 4):
-            cx.set_fused(k, nt)  # also the two-pass copy's packets per wave
+        cx.set_copy_k(k)
         cx.set_two_pass_chunk(chunk)
-        cx.set_copy_cap(cap)
         cx.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off, w.status,
                         id_uniform=workload.ID_UNIFORM, pad16=pad == 16, pad128=pad == 128, stream=s)
 
     with torch.cuda.stream(s):
         w.frame.zero_()
-        run((1, 0, 3, 0, 0))
+        run((1, 0, 0))
         s.synchronize()
         ref_f, ref_s = w.frame.clone(), w.status.clone()
         for v in variants:

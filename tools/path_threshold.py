@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
-"""Where the two-pass encode starts to pay (rsk_encode_batch's kTwoPassMinPayload): encode time of
-both paths (rsk_set_encode_path 1 = per-set kernel, 2 = two-pass) on synthetic batches of uniform
-and mixed payload lengths, device-resident, HIP events, interleaved rounds in one process.  Frames
-of both paths are compared byte for byte before timing.
-    python tools/path_threshold.py [--packets 2097152] [--rounds 4] [--reps 5]"""
+"""Where each encode path pays (rsk_encode_batch's thresholds): encode time of the per-set kernel
+(path 1), the short-frame kernel (3) and the two-pass form with k packets per copy wave (2:k) on
+synthetic batches of uniform and mixed payload lengths, device-resident, HIP events, interleaved rounds
+in one process.  Every variant's frames are compared with path 1's byte for byte before timing.
+    python tools/path_threshold.py [--packets 2097152] [--rounds 4] [--reps 5] [--variants 1,2:1,2:4]"""
 import argparse
 import json
 import os
@@ -14,8 +14,10 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 # (pmin, pmax): uniform lengths, then mixed ranges (pmin < pmax: uniform in [pmin, pmax])
-CASES = [(400, 400), (600, 600), (800, 800), (900, 900), (1000, 1000), (1100, 1100), (1200, 1200),
-         (1400, 1400), (700, 1400), (900, 1400), (1, 1469)]
+CASES = [(100, 100), (160, 160), (200, 200), (300, 300), (400, 400), (600, 600), (800, 800), (900, 900),
+         (1000, 1000), (1100, 1100), (1200, 1200), (1400, 1400), (64, 1400), (700, 1400), (900, 1400), (1, 1469),
+         (64, 64), (128, 128), (250, 250), (350, 350), (450, 450), (500, 500), (1, 600), (1, 900), (100, 700),
+         (256, 700), (1, 300)]
 
 
 def main():
@@ -23,7 +25,11 @@ def main():
     ap.add_argument("--packets", type=int, default=1 << 21)
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--variants", default="1,3,2:1,2:2,2:4")
+    ap.add_argument("--cases", default="", help="subset of CASES as pmin_pmax,... (default: all)")
     args = ap.parse_args()
+    variants = [tuple(int(x) for x in v.split(":")) for v in args.variants.split(",")]
+    vname = lambda v: ":".join(map(str, v))  # noqa: E731
     import torch
 
     from bench import enc_bytes_per_pkt
@@ -36,6 +42,8 @@ def main():
     out = {}
     for k, (pmin, pmax) in enumerate(CASES):
         name = f"t{pmin}_{pmax}"
+        if args.cases and f"{pmin}_{pmax}" not in args.cases.split(","):
+            continue
         workload.CONFIGS[name] = (20 + k, args.packets, pmin, pmax, 1, False, 0)
         d = workload.describe(name, 0, args.packets, n=args.packets)
         w = workload.DeviceWorkload(d, dev)
@@ -45,20 +53,27 @@ def main():
                             w.status, id_uniform=workload.ID_UNIFORM, pad16=d.pad == 16, pad128=d.pad == 128,
                             stream=s)
 
-        frames = []
-        for p in (1, 2):
-            cx.set_encode_path(p)
+        def setv(v):
+            cx.set_encode_path(v[0])
+            cx.set_copy_k(v[1] if len(v) > 1 else 0)
+
+        setv((1,))
+        w.frame.zero_()
+        enc()
+        torch.cuda.synchronize()
+        ref = w.frame.clone()
+        for v in variants:
+            setv(v)
             w.frame.zero_()
             enc()
             torch.cuda.synchronize()
-            frames.append(w.frame.clone())
-        if not torch.equal(frames[0], frames[1]):
-            raise SystemExit(f"{name}: the two paths' frames differ")
-        del frames
-        t = {1: [], 2: []}
+            if not torch.equal(ref, w.frame):
+                raise SystemExit(f"{name}: variant {vname(v)} frames differ from the per-set kernel's")
+        del ref
+        t = {v: [] for v in variants}
         for _ in range(args.rounds):
-            for p in (1, 2):
-                cx.set_encode_path(p)
+            for v in variants:
+                setv(v)
                 enc()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(s)
@@ -66,17 +81,18 @@ def main():
                     enc()
                 e1.record(s)
                 torch.cuda.synchronize()
-                t[p].append(e0.elapsed_time(e1) / args.reps)
+                t[v].append(e0.elapsed_time(e1) / args.reps)
         byts = int(enc_bytes_per_pkt(d.pay_len.astype(np.int64)).sum())
-        m1, m2 = float(np.median(t[1])), float(np.median(t[2]))
         out[name] = {"mean_payload": round(float(d.pay_len.mean()), 1), "frame_pitch": d.frame_pitch,
-                     "per_set_ms": round(m1, 4), "two_pass_ms": round(m2, 4), "two_pass_over_per_set": round(m2 / m1, 4),
-                     "per_set_frac": round(byts / (m1 * 1e-3) / 8e12, 4), "two_pass_frac": round(byts / (m2 * 1e-3) / 8e12, 4)}
+                     "ms": {vname(v): round(float(np.median(t[v])), 4) for v in variants}}
+        out[name]["frac_8TBs"] = {k: round(byts / (ms * 1e-3) / 8e12, 4) for k, ms in out[name]["ms"].items()}
+        out[name]["best"] = min(out[name]["ms"], key=out[name]["ms"].get)
         del w
         torch.cuda.empty_cache()
         print(json.dumps({name: out[name]}), file=sys.stderr, flush=True)
     cx.set_encode_path(0)
-    print(json.dumps({"packets": args.packets, "cases": out}))
+    cx.set_copy_k(0)
+    print(json.dumps({"packets": args.packets, "variants": [vname(v) for v in variants], "cases": out}))
 
 
 if __name__ == "__main__":
