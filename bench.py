@@ -309,6 +309,8 @@ def main() -> None:
         if nv != expect_valid:
             raise SystemExit(f"bench: decode verified {nv} of {expect_valid} packets ({when}, tag {cx.tag_mode})")
 
+    captured_path = [None]
+
     def timed(mode: str, steps: int, warmup: int, sync_ranks: bool):
         """Warm up, capture the step as a graph (the tag mode is fixed at capture), time `steps`
         replays between barriers, then per-kernel HIP events on the step's stream."""
@@ -325,10 +327,14 @@ def main() -> None:
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph, stream=stream):
                 step()
+            captured_path[0] = (cx.last_encode_path, cx.last_copy_k)  # the path the graph replays
             w.dec.n_valid.zero_()
             graph.replay()
             torch.cuda.synchronize()
             gate("graph replay")
+            for _ in range(warmup):  # the warmup steps again, as replays of the graph
+                graph.replay()
+            torch.cuda.synchronize()
         evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
         if sync_ranks:
             dist.barrier()
@@ -361,7 +367,13 @@ def main() -> None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed_max = float(t.item())
 
-    enc_path = ENC_PATH_TEXT.get(cx.last_encode_path, "?").format(k=cx.last_copy_k)
+    # the path the timed region ran: the graph's (captured) path, else the eager calls'
+    run_path = captured_path[0] if graph_mode else (cx.last_encode_path, cx.last_copy_k)
+    enc_path = ENC_PATH_TEXT.get(run_path[0], "?").format(k=run_path[1])
+    if graph_mode and run_path != (cx.last_encode_path, cx.last_copy_k):
+        # the per-kernel events time the eager calls after the timed region: they must be the same path
+        raise SystemExit(f"bench: graph captured encode path {run_path}, eager calls took "
+                         f"{(cx.last_encode_path, cx.last_copy_k)}")
     enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
     total_pkts = (n_total if strong else world * d.n) * args.steps

@@ -159,9 +159,11 @@ int rsk_set_encode_path(rsk_ctx *ctx, int path);
  * kernels read is the immutable key schedule and tag table (and the tag mode, passed by value).
  *
  * Pre-size the scratch of `stream` (rsk_reserve: the legacy default stream, NULL) for batches of up
- * to n packets: the compaction state and, for n >= 16384, the 32-B-per-packet header records of the
- * two-pass encode (rsk_encode_batch).  Batch calls grow it on demand, which waits for that stream to
- * drain and allocates; reserve first if batch calls will be captured into a hipGraph. */
+ * to n packets: the compaction state and, for n >= 16384 unless the context is held to a one-pass encode
+ * path (RSK_ENC_PATH_PER_SET / _SHORT), the 32-B-per-packet header records of the two-pass encode
+ * (rsk_encode_batch; a failed records allocation is not an error: eager calls allocate them on demand,
+ * a captured call then takes the per-set kernel).  Batch calls grow the scratch on demand, which waits
+ * for that stream to drain and allocates; reserve first if batch calls will be captured into a hipGraph. */
 int rsk_reserve(rsk_ctx *ctx, uint32_t n_max);
 int rsk_reserve_stream(rsk_ctx *ctx, uint32_t n_max, void *stream);
 /* Scratch stays allocated per stream until the context is destroyed or the stream is released:
@@ -225,13 +227,17 @@ typedef struct rsk_encode_out {
 
 /* frame_i = tag(8) | EncHead(23) | payload(P), written to frame_arena + frame_off[i].
  * Frames must not overlap each other or the payload arena.
- * Two device paths, identical bytes: batches of long frames (>= 16384 packets, the context's last
- * sampled batch at a mean payload >= 960 B) run a header pass (the MD5 tags 64 to a wave, 32-B
- * records in the stream's scratch) and then one wave per packet; other batches run the per-set kernel.
- * The choice reads a host-mapped statistic the previous calls' kernels left (no synchronisation); a
- * call captured into a hipGraph keeps the path it was captured with, and one captured on a stream
- * without reserved records takes the per-set kernel.  rsk_set_encode_path fixes the
- * path for a context (e.g. one fed alternating long- and short-frame batches). */
+ * Three device paths, identical bytes (rsk_set_encode_path): the per-set kernel (64 packets per wave),
+ * the short-frame kernel (every set on the flat chunk list) and the two-pass form (a header pass: the
+ * MD5 tags 64 to a wave into 32-B records in the stream's scratch; then copy waves of 1, 2 or 4
+ * packets).  AUTO chooses per call of >= 16384 packets by the mean payload of the context's last
+ * sampled batch: <= 96 B short-frame, < 224 B per-set, < 400 B short-frame, < 880 B two-pass with 4
+ * packets per copy wave, < 1160 B 2, else 1; smaller batches and a context's first
+ * call take the per-set kernel.  The statistic is a host-mapped word the previous calls' kernels left
+ * (read without synchronisation: calls issued back to back see it late, which only delays the switch);
+ * a call captured into a hipGraph keeps the path it was captured with, and one captured on a stream
+ * without reserved records takes the per-set kernel.  rsk_set_encode_path fixes the path for a context
+ * (e.g. one fed alternating long- and short-frame batches). */
 int rsk_encode_batch(rsk_ctx *ctx, uint32_t n, const rsk_encode_in *in, const rsk_encode_out *out,
                      void *stream);
 

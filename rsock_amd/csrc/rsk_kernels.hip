@@ -3134,10 +3134,14 @@ int rsk_reserve_stream(rsk_ctx *c, uint32_t n_max, void *stream) {
     if (!g.ok) return RSK_EDEVICE;
     Compact ck;
     const int r = ensure_compact(c, n_max, (hipStream_t)stream, ck);
-    if (r || n_max < kTwoPassMinPackets || c->enc_path != RSK_ENC_PATH_TWO_PASS) return r;
-    // the two-pass encode's header records (32 B per packet), for a context held to that path only; a
-    // failed allocation is not an error: rsk_encode_batch then allocates on demand, or a
-    // captured call takes the per-set kernel
+    if (r || n_max < kTwoPassMinPackets || (c->enc_path != RSK_ENC_PATH_AUTO && c->enc_path != RSK_ENC_PATH_TWO_PASS))
+        return r;
+    // the two-pass encode's header records (32 B per packet) unless the context is held to a one-pass
+    // path.  A capture cannot allocate them, and an AUTO context's eager calls issued back to back all
+    // run before the first batch statistic reaches the host (they take the per-set kernel and never
+    // allocate): without this reserve bench.py's graph captured the per-set kernel (r05z kernel trace).
+    // A failed allocation is not an error: eager calls allocate on demand, a captured call
+    // takes the per-set kernel.
     void *p = nullptr;
     if (rsk::stream_ws(c, (hipStream_t)stream, rsk::WS_ENC, 32ull * n_max, &p) != RSK_OK) {
         (void)hipGetLastError();

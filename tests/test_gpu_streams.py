@@ -384,3 +384,41 @@ def test_check_errors_after_stream_destroyed_unreleased(gpu):
         assert int(o.n_valid.item()) == n and cx.check_device_errors() == 0
     finally:
         cx.close()
+
+
+def test_auto_capture_takes_two_pass_after_back_to_back_calls(gpu):
+    """bench.py's sequence on an AUTO context: reserve the stream, a few eager calls issued back to back
+    (all of them run before the first batch statistic reaches the host, so they take the per-set kernel),
+    synchronize, capture.  The capture must take the two-pass form with its reserved records -- in r05's
+    first build the records were not reserved for AUTO contexts and the graph silently captured the
+    per-set kernel (4 % of the bench line)."""
+    import torch
+
+    from rsock_amd.codec import Codec
+
+    n = 1 << 17
+    d = workload.describe("c3", 0, n, n=n)
+    w = workload.DeviceWorkload(d, gpu)
+    cx = Codec(b"hello135", 0)
+    try:
+        s = torch.cuda.Stream(gpu)
+        cx.reserve(n, stream=s)
+        with torch.cuda.stream(s):
+            for _ in range(5):
+                cx.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
+                                w.status, id_uniform=workload.ID_UNIFORM, pad16=True, stream=s)
+        torch.cuda.synchronize()
+        ref = w.frame.clone()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            cx.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
+                            w.status, id_uniform=workload.ID_UNIFORM, pad16=True, stream=s)
+        assert (cx.last_encode_path, cx.last_copy_k) == (2, 1)
+        w.frame.zero_()
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(w.frame, ref)
+        del g
+    finally:
+        cx.close()
