@@ -102,10 +102,12 @@ __device__ __forceinline__ void stage_tags(const KeySched &ks) {
 
 // LANE: the payload-word-specialised schedule (rsk_md5.h md5_tag_lane: 4 VALU per step instead of 5,
 // 16 instantiations behind one scalar branch).  Who uses it: the decode kernels (registers to spare,
-// ~1 %), and the per-set k_encode<12> for its FLAT sets' tag only (profiles/r04q_md5_flat.json).  The
-// per-packet sets and the short-frame build k_encode<19> keep the generic schedule: there the
-// specialised one raised the register budget past 128 VGPRs (3 waves per SIMD instead of 4) and cost
-// C2 / C4 13-16 % (profiles/r04_ab_md5_isa.json).
+// ~1 %) and the two-pass header pass.  The framing kernels keep the generic schedule: in k_encode's
+// per-packet sets the specialised one raised the register budget past 128 VGPRs (3 waves per SIMD
+// instead of 4) and cost C2 / C4 13-16 % (profiles/r04_ab_md5_isa.json); for its flat sets (MODE 12)
+// round 4 measured a gain on an A/B build that specialised key word 2 only -- on the full build MODE 11
+// (generic) is as fast or 1 % faster (C2 0.0498-0.0501 vs 0.0499-0.0503 ms; 128 / 200-B batches -1 %,
+// profiles/r05_md5_mode11_vs_12.json), so the shipped per-set kernel is k_encode<11>.
 template <bool LANE = false>
 __device__ __forceinline__ void tag_of(const KeySched &ks, uint32_t b, uint32_t &t0, uint32_t &t1) {
     if (ks.tag_mode == RSK_TAG_TABLE) {
@@ -3241,7 +3243,7 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         // the per-set kernel: per-wave hybrid (flat chunk list for short frames, with the tag behind the
         // first chunk loads; software-pipelined one-load DPP per-packet copy, 4 packets per batch, for
         // the rest), tag in the copy loop for long-frame sets, per-set store policy
-        hipLaunchKernelGGL((k_encode<12, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, 0, st, a, c->ks);
+        hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, 0, st, a, c->ks);
         c->enc_last_path.store(RSK_ENC_PATH_PER_SET, std::memory_order_relaxed);
     }
     // the statistic for the next call, on every call this path takes (a sample every 256th
