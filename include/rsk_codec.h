@@ -137,14 +137,13 @@ int rsk_set_tag_mode(rsk_ctx *ctx, int mode);
 int rsk_get_tag_mode(const rsk_ctx *ctx);
 
 /* Encode path of this context's rsk_encode_batch calls (outputs are identical):
- *   RSK_ENC_PATH_AUTO     (default) chosen per call from the context's last sampled batch (>= 16384
- *                         packets): mean payload >= 960 B the two-pass form, <= 160 B the short-frame
- *                         kernel, else the per-set kernel (see rsk_encode_batch);
+ *   RSK_ENC_PATH_AUTO     (default) chosen per call of >= 16384 packets from the mean payload of the
+ *                         context's last sampled batch (table under rsk_encode_batch);
  *   RSK_ENC_PATH_PER_SET  one kernel, 64 packets per wave (every batch shape);
  *   RSK_ENC_PATH_TWO_PASS a header pass (MD5 tags 64 to a wave, 32-B records in the stream's scratch),
  *                         then one wave per packet (batches of long frames);
  *   RSK_ENC_PATH_SHORT    the per-set kernel with every set on the flat chunk list (batches of short
- *                         frames; AUTO takes it when the last sampled mean payload is <= 160 B).
+ *                         frames).
  * Read when a call is issued, as the tag mode; RSK_EINVAL for an unknown path. */
 #define RSK_ENC_PATH_AUTO 0
 #define RSK_ENC_PATH_PER_SET 1
@@ -232,11 +231,13 @@ typedef struct rsk_encode_out {
  * MD5 tags 64 to a wave into 32-B records in the stream's scratch; then copy waves of 1, 2 or 4
  * packets).  AUTO chooses per call of >= 16384 packets by the mean payload of the context's last
  * sampled batch: <= 96 B short-frame, < 224 B per-set, < 400 B short-frame, < 880 B two-pass with 4
- * packets per copy wave, < 1160 B 2, else 1; smaller batches and a context's first
- * call take the per-set kernel.  The statistic is a host-mapped word the previous calls' kernels left
- * (read without synchronisation: calls issued back to back see it late, which only delays the switch);
- * a call captured into a hipGraph keeps the path it was captured with, and one captured on a stream
- * without reserved records takes the per-set kernel.  rsk_set_encode_path fixes the path for a context
+ * packets per copy wave, < 1160 B 2, else 1; smaller batches take the per-set kernel.
+ * The statistic is a host-mapped word the previous calls' kernels left (read without synchronisation:
+ * calls issued back to back see it late, which only delays a switch of traffic mix); the first such call
+ * on a context, which has no statistic yet, samples its own batch and waits for that one 64-thread
+ * launch on `stream` (a call being captured does not wait: it takes the per-set kernel).  A call
+ * captured into a hipGraph keeps the path it was captured with, and one captured on a stream without
+ * reserved records takes the per-set kernel.  rsk_set_encode_path fixes the path for a context
  * (e.g. one fed alternating long- and short-frame batches). */
 int rsk_encode_batch(rsk_ctx *ctx, uint32_t n, const rsk_encode_in *in, const rsk_encode_out *out,
                      void *stream);

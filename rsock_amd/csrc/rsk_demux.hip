@@ -13,14 +13,16 @@
 // kernels that produce the counts, and the radix sort is onesweep, one launch per pass):
 //   fill            key table + look-back state words to all-ones
 //   k_dm_flags_prep per-wave ballots of VALID and VALID-control packets, block offsets by look-back;
-//                   cidx[j] = packet of compacted slot j, cep[j] = its epoch (CTRL for singletons)
-//   k_dm_insert     open-addressing table: a slot holds a key fingerprint and the compacted index of
+//                   cidx[j] = packet of compacted slot j, cep[j] = its epoch (CTRL for singletons),
+//                   pep[packet] = the same epoch (CMD_BARRIER only)
+//   k_dm_insert     open-addressing table: a slot holds a key fingerprint and the packet index of
 //                   its key's first packet (lowered by CAS), so key confirmation reads the immutable
-//                   input arrays (no lane ever waits on another lane's write); keys whose epoch lies
-//                   inside one tile are grouped in LDS only
-//   k_dm_leader_rank leader of j = the slot's index (or j for a control packet); leader ranks = dense
-//                   segment ids in first-occurrence order by look-back; rank_at, seg_first, n_seg;
-//                   the followers (non-leaders) compacted with their leader
+//                   input arrays at that index (no lane ever waits on another lane's write); keys
+//                   whose epoch lies inside one tile are grouped in LDS only
+//   k_dm_leader_rank leader of j = the packet its slot names (or j's own packet for a control
+//                   packet); leader ranks = dense segment ids in first-occurrence order by look-back;
+//                   rank_at[packet], seg_first, n_seg; the followers (non-leaders) compacted with
+//                   their leader
 //   k_dm_segof_hist radix keys = segment id of each follower, global digit histograms of every pass
 //                   (<= 1024 followers: sorted here by one block)
 //   k_dm_onesweep   stable LSD pass of the FOLLOWERS by segment id (8-bit or narrower digits, as many
@@ -142,6 +144,7 @@ struct DmIn {
     const uint32_t *conv;
     const uint64_t *key;
     const uint32_t *dst;
+    uint32_t *pep;  // with CMD_BARRIER: epoch of each VALID data packet, by packet index (else null: 0)
     uint32_t n, fields;
 };
 
@@ -269,22 +272,24 @@ __device__ __forceinline__ uint64_t key_hash(const Key &k) {
 // compare-and-swap (the fingerprint half never changes once claimed).  A relaxed load comes first:
 // a hot key's slot is read, not written, by every later tile (no RMW unless the index drops); a new
 // key costs the load and one CAS (round 2, first half: a load, a CAS and a separate atomicMin word).
-template <int V = 0>
-__device__ __forceinline__ uint32_t global_probe(const DmIn &a, const uint32_t *cidx, const uint32_t *cep,
+__device__ __forceinline__ uint32_t global_probe(const DmIn &a,
                                                  unsigned long long *slots, uint32_t mask, const Key &k,
                                                  uint64_t hv, uint32_t j) {
+    // j is the packet index (monotone with the compacted index, so the minimum is the same packet):
+    // a slot's owner is confirmed on the inputs at that index directly (round 5: one dependent
+    // gather less than through cidx / cep, C3 0.400 -> 0.372 ms with the 512-packet tiles)
     const uint32_t fp = (uint32_t)(hv >> 32);
     const unsigned long long mine = ((unsigned long long)fp << 32) | j;
     uint32_t h = (uint32_t)hv & mask;
     for (;;) {
-        unsigned long long e = V == 2 ? slots[h] : __hip_atomic_load(slots + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned long long e = __hip_atomic_load(slots + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (e == ~0ull) {
             e = atomicCAS(slots + h, ~0ull, mine);
             if (e == ~0ull) return h;  // claimed
         }
         if ((uint32_t)(e >> 32) == fp) {
             const uint32_t o = (uint32_t)e;
-            if (V == 3 || key_eq(load_key(a, cidx[o], cep[o]), k)) {  // V 3 (A/B timing only): no confirmation
+            if (key_eq(load_key(a, o, a.pep ? a.pep[o] : 0u), k)) {
                 while ((uint32_t)e > j) {  // lower the key's first index to j
                     const unsigned long long f = atomicCAS(slots + h, e, mine);
                     if (f == e) break;
@@ -307,14 +312,11 @@ __device__ __forceinline__ uint32_t global_probe(const DmIn &a, const uint32_t *
 // and last data packets cannot occur outside the tile: its block minimum IS its first packet and it
 // never touches the global table (hslot = kLeadTag | leader).  Only the tile's first and last epochs
 // go to the table: C4 (5 % control packets) sends ~2 % of its keys there instead of all of them.
-constexpr uint32_t kInsItems = 4;
+constexpr uint32_t kInsItems = 2;  // round 5: 2 (512-packet tiles; 4: C3 +4 %, 1: 64 connections +7 %)
 constexpr uint32_t kLeadTag = 0x80000000u;  // hslot: leader index (table slots are < 2^31)
-constexpr uint32_t kInsTile = kBlock * kInsItems;  // 1024 packets (24 KB LDS: 6 waves per SIMD)
+constexpr uint32_t kInsTile = kBlock * kInsItems;  // 512 packets (12 KB LDS)
 constexpr uint32_t kLtab = 2 * kInsTile;           // LDS table slots (power of 2)
 
-// V (A/B build, RSK_DM_VARIANT, timing only -- 1 and 3 give wrong segments): 1 = no global probe,
-// 2 = the probe's first load a plain (L2-cached) load, 3 = no key confirmation.
-template <int V = 0>
 __global__ __launch_bounds__(kBlock) void k_dm_insert(DmIn a, const uint32_t *nvp, const uint32_t *cidx,
                                                       const uint32_t *cep, unsigned long long *slots,
                                                       uint32_t mask, uint32_t *hslot) {
@@ -336,7 +338,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_insert(DmIn a, const uint32_t *nv
     // (keys stay in registers; confirming another packet's key reads the immutable inputs: keeping
     // the tile's keys in LDS too cost more occupancy than it saved, 157 -> 179 us on C3)
     Key kr[kInsItems];
-    uint32_t lpos[kInsItems];
+    uint32_t lpos[kInsItems], pkr[kInsItems];
 #pragma unroll
     for (uint32_t it = 0; it < kInsItems; ++it) {
         const uint32_t li = it * kBlock + t, j = base + li;
@@ -345,7 +347,8 @@ __global__ __launch_bounds__(kBlock) void k_dm_insert(DmIn a, const uint32_t *nv
         if (j >= nv) continue;
         const uint32_t ep = cep[j];
         if (ep == kCtrl) continue;
-        kr[it] = load_key(a, cidx[j], ep);
+        pkr[it] = cidx[j];
+        kr[it] = load_key(a, pkr[it], ep);
         const Key &k = kr[it];
         const uint64_t hv = key_hash(k);
         const uint32_t fp = (uint32_t)(hv >> 32);
@@ -393,10 +396,10 @@ __global__ __launch_bounds__(kBlock) void k_dm_insert(DmIn a, const uint32_t *nv
 #pragma unroll
     for (uint32_t it = 0; it < kInsItems; ++it) {
         if (!((rep >> it) & 1u)) continue;
-        const uint32_t j = base + it * kBlock + t;
+        const uint32_t j = pkr[it];  // leaders are named by packet index
         const Key &k = kr[it];
-        lmin[lpos[it]] = V != 1 && (k.ep == elo || k.ep == ehi)
-                             ? global_probe<V>(a, cidx, cep, slots, mask, k, key_hash(k), j)
+        lmin[lpos[it]] = (k.ep == elo || k.ep == ehi)
+                             ? global_probe(a, slots, mask, k, key_hash(k), j)
                              : kLeadTag | j;
     }
     __syncthreads();
@@ -504,7 +507,10 @@ __global__ __launch_bounds__(kBlock) void k_dm_flags_prep(DmIn a, unsigned long 
             const uint32_t i = b * kTile + r * kBlock + t;
             const uint32_t j = accv + bv + (uint32_t)__popcll(mv[r][w] & lt);
             cidx[j] = i;
-            cep[j] = ((flags >> (16 + r)) & 1u) ? kCtrl : accc + bc + (uint32_t)__popcll(mc[r][w] & lt);
+            const bool ctl = ((flags >> (16 + r)) & 1u) != 0u;
+            const uint32_t ev = accc + bc + (uint32_t)__popcll(mc[r][w] & lt);
+            cep[j] = ctl ? kCtrl : ev;
+            if (a.pep && !ctl) a.pep[i] = ev;
         }
         accv += tv;
         accc += tc;
@@ -530,20 +536,21 @@ __global__ __launch_bounds__(kBlock) void k_dm_leader_rank(const uint32_t *nvp, 
         for (uint32_t q = t; q < 4u * 256u; q += kBlock) ghist[q] = 0u;
     uint32_t isl = 0;  // bit r: row r's item is its key's leader
     uint32_t hs[kRows], lead[kRows];
+    uint32_t pks[kRows];  // packet indices, loaded with the slots (before the look-back)
 #pragma unroll
     for (uint32_t r = 0; r < kRows; ++r) {
         const uint32_t j = b * kTile + r * kBlock + t;
         hs[r] = j < nv ? hslot[j] : kNone;
+        pks[r] = j < nv ? cidx[j] : kNone;
     }
+    // leaders by packet index (the table and the epoch-local tag hold packet indices)
+#pragma unroll
+    for (uint32_t r = 0; r < kRows; ++r)
+        lead[r] = hs[r] == kNone ? pks[r] : (hs[r] & kLeadTag) ? hs[r] & ~kLeadTag : (uint32_t)slots[hs[r]];
 #pragma unroll
     for (uint32_t r = 0; r < kRows; ++r) {
         const uint32_t j = b * kTile + r * kBlock + t;
-        lead[r] = hs[r] == kNone ? j : (hs[r] & kLeadTag) ? hs[r] & ~kLeadTag : (uint32_t)slots[hs[r]];
-    }
-#pragma unroll
-    for (uint32_t r = 0; r < kRows; ++r) {
-        const uint32_t j = b * kTile + r * kBlock + t;
-        const bool l = j < nv && lead[r] == j;
+        const bool l = j < nv && lead[r] == pks[r];
         const uint64_t bl = __ballot(l);
         if (lane == 0u) ml[r][w] = bl;
         isl |= l ? 1u << r : 0u;
@@ -577,9 +584,9 @@ __global__ __launch_bounds__(kBlock) void k_dm_leader_rank(const uint32_t *nvp, 
         const uint32_t before = acc + bw + (uint32_t)__popcll(ml[r][w] & lt);  // leaders before j
         acc += tw;
         if (j >= nv) continue;
-        const uint32_t pk = cidx[j];
+        const uint32_t pk = pks[r];
         if ((isl >> r) & 1u) {
-            rank_at[j] = before;
+            rank_at[pk] = before;  // by packet index: followers name their leader by it
             seg_first[before] = pk;
         } else {
             fkey[j - before] = lead[r];
@@ -661,10 +668,19 @@ __global__ __launch_bounds__(kBlock) void k_dm_segof_hist(const uint32_t *nvp, c
     for (uint32_t p = 0; p < np; ++p) {  // np is block-uniform
 #pragma unroll
         for (uint32_t r = 0; r < kItems; ++r) {
+            // one LDS atomic per lane; a row whose valid lanes all hold one digit (a hot segment)
+            // adds its count once (round 5: the per-bit ballot match of every row cost C3 ~20 us)
             const bool v = base + r * kBlock + t < nf;
             const uint32_t d = (kk[r] >> (width * p)) & dm;
-            const uint64_t peers = digit_peers(v, d, width);
-            if (v && (peers & lanemask_lt(lane)) == 0) atomicAdd(&lh[p][d], (uint32_t)__popcll(peers));
+            const uint64_t bv = __ballot(v);
+            if (bv == 0ull) continue;  // wave-uniform
+            const uint32_t first = (uint32_t)__builtin_ctzll(bv);
+            const uint32_t df = (uint32_t)__shfl((int)d, (int)first);
+            if (__ballot(v && d == df) == bv) {
+                if (lane == first) atomicAdd(&lh[p][df], (uint32_t)__popcll(bv));
+            } else if (v) {
+                atomicAdd(&lh[p][d], 1u);
+            }
         }
     }
     __syncthreads();
@@ -806,7 +822,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_final(const uint32_t *nvp, const 
 
 // ---- workspace ------------------------------------------------------------------------------
 struct DmWs {
-    uint32_t *cidx, *cep, *hslot, *rank_at;
+    uint32_t *cidx, *cep, *hslot, *rank_at, *pep;
     uint32_t *kA, *vA, *kB, *vB;
     uint32_t *ghist;
     unsigned long long *slots;  // slots | look-back states: one 0xff fill per call
@@ -835,6 +851,7 @@ size_t dm_layout(uint32_t n, uint8_t *base, DmWs *w) {
     d.cep = (uint32_t *)take(4ull * n);
     d.hslot = (uint32_t *)take(4ull * n);
     d.rank_at = (uint32_t *)take(4ull * n);
+    d.pep = (uint32_t *)take(4ull * n);
     d.kA = (uint32_t *)take(4ull * n);
     d.vA = (uint32_t *)take(4ull * n);
     d.kB = (uint32_t *)take(4ull * n);
@@ -893,13 +910,14 @@ extern "C" int rsk_demux_batch(rsk_ctx *c, uint32_t n, const rsk_demux_in *in, u
     a.dst = in->dst;
     a.n = n;
     a.fields = fields;
+    a.pep = (fields & RSK_DEMUX_CMD_BARRIER) ? w.pep : nullptr;
     // one fill: the key table and every look-back state word start as all-ones
     hipError_t e = hipMemsetAsync(w.slots, 0xff, w.fill_bytes, s);
     if (e != hipSuccess) { rsk::set_error("hipMemsetAsync(table)", e); return RSK_EDEVICE; }
     const uint32_t nb = w.nb;
     hipLaunchKernelGGL(k_dm_flags_prep, dim3(w.nt), dim3(kBlock), 0, s, a, w.st_v, w.st_c, w.cidx, w.cep, w.nv,
                        c->err_dev);
-    hipLaunchKernelGGL(k_dm_insert<0>, dim3((n + kInsTile - 1) / kInsTile), dim3(kBlock), 0, s, a, w.nv, w.cidx,
+    hipLaunchKernelGGL(k_dm_insert, dim3((n + kInsTile - 1) / kInsTile), dim3(kBlock), 0, s, a, w.nv, w.cidx,
                        w.cep, w.slots, w.tsize - 1u, w.hslot);
     hipLaunchKernelGGL(k_dm_leader_rank, dim3(w.nt), dim3(kBlock), 0, s, w.nv, w.hslot, w.slots, w.cidx, w.st_l,
                        w.kA, w.vA, w.rank_at, out->seg_first, w.nseg, w.ghist, c->err_dev);

@@ -192,7 +192,8 @@ __device__ __forceinline__ void encode_tag(const EncArgs &a, const KeySched &ks,
 // argument: one more pointer in its arguments cost C4 12 % through SGPR spills, gpurun_out/r04o).
 constexpr uint32_t kStatValid = 0x80000000u;
 // AUTO's choice (rsk_encode_batch, enc_path / copy_k): batches of at least kTwoPassMinPackets by the mean
-// payload of the context's last sampled batch (below that, and before any sample, the per-set kernel).
+// payload of the context's last sampled batch (below that, and in a capture before any sample, the
+// per-set kernel).
 // Measured on uniform and mixed lengths, 2M packets per case, one process per box
 // (tools/path_threshold.py, profiles/r05_path_threshold.json): the per-set kernel is fastest up to a
 // mean of ~200 B, except C2's 64 B where the short-frame kernel is (profiles/r05_enc_paths.json); the
@@ -3153,8 +3154,8 @@ int rsk_reserve_stream(rsk_ctx *c, uint32_t n_max, void *stream) {
 }
 
 // The batch statistic behind AUTO (enc_sample: k_encode_heads in every two-pass call, k_enc_sample
-// behind every other uncaptured call of >= kTwoPassMinPackets packets).  The first call on a context
-// has no statistic yet and takes the per-set kernel; every path gives identical bytes.
+// behind every other uncaptured call of >= kTwoPassMinPackets packets; enc_path samples before the
+// first such call on a context).  Every path gives identical bytes.
 // The context's last sampled mean payload (bit 31 set: valid), or 0.
 static uint32_t sampled_mean(const rsk_ctx *c) {
     const uint32_t s = c->enc_stat_host ? __atomic_load_n(c->enc_stat_host, __ATOMIC_RELAXED) : 0u;
@@ -3170,8 +3171,16 @@ static int copy_k(rsk_ctx *c) {
 }
 
 // Encode path per call: the context's forced path (rsk_set_encode_path), else AUTO's table above.
-static int enc_path(rsk_ctx *c, uint32_t n) {
+// The first AUTO call of >= kTwoPassMinPackets packets on a context samples its own batch and waits
+// for that one 64-thread launch on its stream, so it already takes the table's path (without that,
+// back-to-back eager calls ran the per-set kernel until the first sample landed: 5 calls in
+// gpurun_out/r05f1/c3).  A capture never waits: it takes the per-set kernel when no sample exists.
+static int enc_path(rsk_ctx *c, uint32_t n, const uint16_t *pay_len, hipStream_t st) {
     if (c->enc_path) return c->enc_path;
+    if (n >= kTwoPassMinPackets && c->enc_stat_dev && !(sampled_mean(c) & kStatValid) && !rsk::capturing(st)) {
+        hipLaunchKernelGGL(k_enc_sample, dim3(1), dim3(64), 0, st, pay_len, n, c->enc_stat_dev);
+        (void)hipStreamSynchronize(st);
+    }
     const uint32_t s = sampled_mean(c);
     if (n < kTwoPassMinPackets || !(s & kStatValid)) return RSK_ENC_PATH_PER_SET;
     const uint32_t mean = s & ~kStatValid;
@@ -3205,7 +3214,7 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
     hipStream_t st = (hipStream_t)stream;
     const dim3 gd(grid), bd(kBlock);
     (void)gd;
-    const int path = enc_path(c, n);
+    const int path = enc_path(c, n, in->pay_len, st);
     if (path == RSK_ENC_PATH_TWO_PASS) {
         // the two-pass form (batches of long frames): header records, then one wave per packet
         void *hp = nullptr;

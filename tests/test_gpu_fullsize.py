@@ -80,6 +80,32 @@ def test_encode_path_choice(codec, gpu):
             assert codec.last_copy_k == k, (cfg, codec.last_copy_k)
 
 
+@pytest.mark.parametrize("cfg", ["c3", "c4", "c2"])
+def test_encode_path_first_call(gpu, cfg):
+    """A fresh context has no batch statistic: its first AUTO call of >= 16384 packets samples its own
+    batch (one 64-thread launch, waited for once) and already takes the table's path, and so do calls
+    issued back to back after it without synchronisation (gpurun_out/r05f1/c3 showed 5 eager calls on
+    the per-set kernel before this)."""
+    import torch
+    from rsock_amd.codec import Codec
+
+    d = workload.describe(cfg, 0, 40_000, n=40_000)
+    w = workload.DeviceWorkload(d, gpu)
+    path, k = AUTO_EXPECT[cfg]
+    c = Codec(b"hello135", 0)
+    try:
+        for call in range(3):
+            c.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
+                           w.status, id_uniform=workload.ID_UNIFORM, pad16=True)
+            assert c.last_encode_path == path, (cfg, call, c.last_encode_path)
+            if path == 2:
+                assert c.last_copy_k == k, (cfg, call, c.last_copy_k)
+        torch.cuda.synchronize()
+        assert torch.equal(w.status.to(torch.int64), (w.pay_len.to(torch.int64) & 0xFFFF) + 31)
+    finally:
+        c.close()
+
+
 @pytest.mark.parametrize("rank", [7, 0])
 def test_c5_shard_roundtrip(pcodec, gpu, oracle, rank):
     """BASELINE config 5 (64M x 1400-B packets sharded 8 ways): the shard rank `rank` of 8 runs on

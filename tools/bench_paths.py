@@ -24,7 +24,7 @@ def main():
                          "mixed lengths, else 16)")
     ap.add_argument("--only", default="", help="time only these paths (comma list), e.g. demux,demux_64conn")
     ap.add_argument("--encode-path", type=int, default=0,
-                    help="rsk_set_encode_path for the encode paths: 0 chosen per call, 1 k_encode, 2 two-pass, 3 short, 4 fused")
+                    help="rsk_set_encode_path for the encode paths: 0 chosen per call, 1 k_encode, 2 two-pass, 3 short")
     args = ap.parse_args()
     import torch
 
