@@ -13,8 +13,8 @@
 // kernels that produce the counts, and the radix sort is onesweep, one launch per pass):
 //   fill            key table + look-back state words to all-ones
 //   k_dm_flags_prep per-wave ballots of VALID and VALID-control packets, block offsets by look-back;
-//                   cidx[j] = packet of compacted slot j, cep[j] = its epoch (CTRL for singletons),
-//                   pep[packet] = the same epoch (CMD_BARRIER only)
+//                   cidx[j] = packet of compacted slot j; with CMD_BARRIER pep[packet] = its epoch
+//                   (CTRL for singletons; without, every epoch is 0 and nothing is stored)
 //   k_dm_insert     open-addressing table: a slot holds a key fingerprint and the packet index of
 //                   its key's first packet (lowered by CAS), so key confirmation reads the immutable
 //                   input arrays at that index (no lane ever waits on another lane's write); keys
@@ -49,7 +49,7 @@ constexpr int kWaves = kBlock / 64;
 constexpr uint32_t kItems = RSK_DM_ITEMS;       // radix: items per thread per tile (A/B builds: -DRSK_DM_ITEMS)
 constexpr uint32_t kTile = kBlock * kItems;     // 4096 packets per radix tile
 constexpr uint32_t kNone = 0xffffffffu;
-constexpr uint32_t kCtrl = 0xffffffffu;         // cep[] marker: control packet (singleton segment)
+constexpr uint32_t kCtrl = 0xffffffffu;         // pep[] marker: control packet (singleton segment)
 constexpr uint32_t kScanChunk = 4096;           // elements per block in the multi-block scan
 
 __device__ __forceinline__ uint64_t lanemask_lt(uint32_t lane) { return (1ull << lane) - 1ull; }
@@ -277,7 +277,7 @@ __device__ __forceinline__ uint32_t global_probe(const DmIn &a,
                                                  uint64_t hv, uint32_t j) {
     // j is the packet index (monotone with the compacted index, so the minimum is the same packet):
     // a slot's owner is confirmed on the inputs at that index directly (round 5: one dependent
-    // gather less than through cidx / cep, C3 0.400 -> 0.372 ms with the 512-packet tiles)
+    // gather less than through the compacted index, C3 0.400 -> 0.372 ms with the 512-packet tiles)
     const uint32_t fp = (uint32_t)(hv >> 32);
     const unsigned long long mine = ((unsigned long long)fp << 32) | j;
     uint32_t h = (uint32_t)hv & mask;
@@ -318,7 +318,7 @@ constexpr uint32_t kInsTile = kBlock * kInsItems;  // 512 packets (12 KB LDS)
 constexpr uint32_t kLtab = 2 * kInsTile;           // LDS table slots (power of 2)
 
 __global__ __launch_bounds__(kBlock) void k_dm_insert(DmIn a, const uint32_t *nvp, const uint32_t *cidx,
-                                                      const uint32_t *cep, unsigned long long *slots,
+                                                      unsigned long long *slots,
                                                       uint32_t mask, uint32_t *hslot) {
     __shared__ unsigned long long ltab[kLtab];
     __shared__ uint32_t lmin[kLtab];  // block-minimum index per key, then (phase 2b) the key's global slot
@@ -340,15 +340,18 @@ __global__ __launch_bounds__(kBlock) void k_dm_insert(DmIn a, const uint32_t *nv
     Key kr[kInsItems];
     uint32_t lpos[kInsItems], pkr[kInsItems];
 #pragma unroll
+    for (uint32_t it = 0; it < kInsItems; ++it) {  // every item's loads in flight before the LDS work
+        const uint32_t j = base + it * kBlock + t;
+        pkr[it] = j < nv ? cidx[j] : kNone;
+    }
+#pragma unroll
+    for (uint32_t it = 0; it < kInsItems; ++it)
+        kr[it] = pkr[it] == kNone ? Key{kCtrl, 0, 0, 0, 0} : load_key(a, pkr[it], a.pep ? a.pep[pkr[it]] : 0u);
+#pragma unroll
     for (uint32_t it = 0; it < kInsItems; ++it) {
         const uint32_t li = it * kBlock + t, j = base + li;
         lpos[it] = kNone;
-        kr[it] = Key{kCtrl, 0, 0, 0, 0};
-        if (j >= nv) continue;
-        const uint32_t ep = cep[j];
-        if (ep == kCtrl) continue;
-        pkr[it] = cidx[j];
-        kr[it] = load_key(a, pkr[it], ep);
+        if (kr[it].ep == kCtrl) continue;  // past the batch, or a control packet
         const Key &k = kr[it];
         const uint64_t hv = key_hash(k);
         const uint32_t fp = (uint32_t)(hv >> 32);
@@ -362,7 +365,8 @@ __global__ __launch_bounds__(kBlock) void k_dm_insert(DmIn a, const uint32_t *nv
             }
             if ((uint32_t)(e >> 32) == fp) {
                 const uint32_t jo = base + (uint32_t)e;
-                if (key_eq(load_key(a, cidx[jo], cep[jo]), k)) break;
+                const uint32_t po = cidx[jo];
+                if (key_eq(load_key(a, po, a.pep ? a.pep[po] : 0u), k)) break;
             }
             h = (h + 1u) & (kLtab - 1u);
         }
@@ -438,10 +442,11 @@ constexpr uint32_t kRows = kTile / kBlock;
 
 // flags + both block scans + prep in one pass: per-row ballots of VALID and VALID-control packets,
 // the tile's exclusive offsets by decoupled look-back (wave 0: compacted index, wave 1: epoch), then
-// cidx[j] = packet of compacted slot j, cep[j] = its epoch (CTRL for singletons); the last tile
+// cidx[j] = packet of compacted slot j, pep[packet] = its epoch (CTRL for singletons; CMD_BARRIER
+// only); the last tile
 // writes n_valid.
 __global__ __launch_bounds__(kBlock) void k_dm_flags_prep(DmIn a, unsigned long long *st_v,
-                                                          unsigned long long *st_c, uint32_t *cidx, uint32_t *cep,
+                                                          unsigned long long *st_c, uint32_t *cidx,
                                                           uint32_t *nvp, uint32_t *err) {
     __shared__ uint64_t mv[kRows][kWaves], mc[kRows][kWaves];
     __shared__ uint32_t pre[2];
@@ -507,10 +512,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_flags_prep(DmIn a, unsigned long 
             const uint32_t i = b * kTile + r * kBlock + t;
             const uint32_t j = accv + bv + (uint32_t)__popcll(mv[r][w] & lt);
             cidx[j] = i;
-            const bool ctl = ((flags >> (16 + r)) & 1u) != 0u;
-            const uint32_t ev = accc + bc + (uint32_t)__popcll(mc[r][w] & lt);
-            cep[j] = ctl ? kCtrl : ev;
-            if (a.pep && !ctl) a.pep[i] = ev;
+            if (a.pep) a.pep[i] = ((flags >> (16 + r)) & 1u) ? kCtrl : accc + bc + (uint32_t)__popcll(mc[r][w] & lt);
         }
         accv += tv;
         accc += tc;
@@ -822,7 +824,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_final(const uint32_t *nvp, const 
 
 // ---- workspace ------------------------------------------------------------------------------
 struct DmWs {
-    uint32_t *cidx, *cep, *hslot, *rank_at, *pep;
+    uint32_t *cidx, *hslot, *rank_at, *pep;
     uint32_t *kA, *vA, *kB, *vB;
     uint32_t *ghist;
     unsigned long long *slots;  // slots | look-back states: one 0xff fill per call
@@ -848,7 +850,6 @@ size_t dm_layout(uint32_t n, uint8_t *base, DmWs *w) {
     };
     DmWs d;
     d.cidx = (uint32_t *)take(4ull * n);
-    d.cep = (uint32_t *)take(4ull * n);
     d.hslot = (uint32_t *)take(4ull * n);
     d.rank_at = (uint32_t *)take(4ull * n);
     d.pep = (uint32_t *)take(4ull * n);
@@ -915,10 +916,10 @@ extern "C" int rsk_demux_batch(rsk_ctx *c, uint32_t n, const rsk_demux_in *in, u
     hipError_t e = hipMemsetAsync(w.slots, 0xff, w.fill_bytes, s);
     if (e != hipSuccess) { rsk::set_error("hipMemsetAsync(table)", e); return RSK_EDEVICE; }
     const uint32_t nb = w.nb;
-    hipLaunchKernelGGL(k_dm_flags_prep, dim3(w.nt), dim3(kBlock), 0, s, a, w.st_v, w.st_c, w.cidx, w.cep, w.nv,
+    hipLaunchKernelGGL(k_dm_flags_prep, dim3(w.nt), dim3(kBlock), 0, s, a, w.st_v, w.st_c, w.cidx, w.nv,
                        c->err_dev);
     hipLaunchKernelGGL(k_dm_insert, dim3((n + kInsTile - 1) / kInsTile), dim3(kBlock), 0, s, a, w.nv, w.cidx,
-                       w.cep, w.slots, w.tsize - 1u, w.hslot);
+                       w.slots, w.tsize - 1u, w.hslot);
     hipLaunchKernelGGL(k_dm_leader_rank, dim3(w.nt), dim3(kBlock), 0, s, w.nv, w.hslot, w.slots, w.cidx, w.st_l,
                        w.kA, w.vA, w.rank_at, out->seg_first, w.nseg, w.ghist, c->err_dev);
     hipLaunchKernelGGL(k_dm_segof_hist, dim3(w.nt), dim3(kBlock), 0, s, w.nv, w.nseg, w.rank_at, w.kA, w.vA,

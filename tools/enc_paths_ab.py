@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """In-process A/B of rsk_encode_batch's paths on one config (device-resident, HIP events on the launch
-stream, interleaved rounds): each variant = (encode path, two-pass packets per copy wave k, two-pass chunk).  Every variant's frames and statuses are compared with the per-set kernel's before timing.
-    python tools/enc_paths_ab.py --config c3 [--variants 1,2:1,2:4,2:1:1048576] [--rounds 6] [--reps 10]
+stream, interleaved rounds): each variant = (encode path, two-pass packets per copy wave k, two-pass chunk,
+sub-batches): sub-batches > 1 issues the batch as that many consecutive slices alternating over two
+streams forked from and joined back to the timing stream (the header pass of one slice beside the copy
+of another).  Every variant's frames and statuses are compared with the per-set kernel's before timing.
+    python tools/enc_paths_ab.py --config c3 [--variants 1,2:1,2:4,2:1:1048576,2:4:0:2] [--rounds 6] [--reps 10]
                                  [--layout slots|packed|odd] [--pad 16|128|0]
 One JSON line: per variant the median over rounds of the mean encode time, and its fraction of 8 TB/s
 by the algorithmic bytes (2P + 66 per packet)."""
@@ -16,10 +19,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def parse_variant(v):
-    """path[:k[:chunk]] -- k packets per copy wave (path 2; 0 = chosen by the library), chunk packets per
-    heads / copy pair (path 2; 0 = the whole batch)"""
-    f = [int(x) for x in v.split(":")]
-    return (f[0], f[1] if len(f) > 1 else 0, f[2] if len(f) > 2 else 0)
+    """path[:k[:chunk[:sub]]] -- k packets per copy wave (path 2; 0 = chosen by the library), chunk packets
+    per heads / copy pair (path 2; 0 = the whole batch), sub-batches over two streams (0 / 1 = one call)"""
+    f = [int(x) for x in v.split(":")] + [0, 0, 0]
+    return (f[0], f[1], f[2], max(f[3], 1))
 
 
 def main():
@@ -59,19 +62,34 @@ def main():
         w.frame = torch.zeros(int(off[-1]) + 2048, dtype=torch.uint8, device=dev)
     cx = rc.Codec(b"hello135", 0, tag_mode=args.tag)
     s = torch.cuda.Stream(dev)
+    s2 = torch.cuda.Stream(dev)
     variants = [parse_variant(v) for v in args.variants.split(",")]
 
     def run(v):
-        p, k, chunk = v
+        p, k, chunk, sub = v
         cx.set_encode_path(p)
         cx.set_copy_k(k)
         cx.set_two_pass_chunk(chunk)
-        cx.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off, w.status,
-                        id_uniform=workload.ID_UNIFORM, pad16=pad == 16, pad128=pad == 128, stream=s)
+        if sub == 1:
+            cx.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
+                            w.status, id_uniform=workload.ID_UNIFORM, pad16=pad == 16, pad128=pad == 128, stream=s)
+            return
+        fork = torch.cuda.Event()
+        fork.record(s)
+        s2.wait_event(fork)
+        for q in range(sub):
+            lo, hi = n * q // sub, n * (q + 1) // sub
+            sl = slice(lo, hi)
+            cx.output_batch(w.payload, w.pay_off[sl], w.pay_len[sl], w.cmd[sl], w.conv[sl], w.conn_key[sl], w.frame,
+                            w.frame_off[sl], w.status[sl], id_uniform=workload.ID_UNIFORM, pad16=pad == 16,
+                            pad128=pad == 128, stream=s if q % 2 == 0 else s2)
+        join = torch.cuda.Event()
+        join.record(s2)
+        s.wait_event(join)
 
     with torch.cuda.stream(s):
         w.frame.zero_()
-        run((1, 0, 0))
+        run((1, 0, 0, 1))
         s.synchronize()
         ref_f, ref_s = w.frame.clone(), w.status.clone()
         for v in variants:
