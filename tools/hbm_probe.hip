@@ -5,6 +5,7 @@
 //   write16     dst[i] = const, 16 B/lane                                    (write-only)
 //   shift2ld    dst chunk k = src bytes [16k+1, 16k+17): two 16-B loads + v_alignbyte
 //   shiftdpp    same, second operand from lane+1 via DPP wave_shl:1 (one load per chunk)
+//   strided     isolated 16- / 32-B reads at a pitch, one lane per item (decode / header-pass ceiling)
 // Build: hipcc -O3 --offload-arch=gfx950 -shared -fPIC -o tools/libhbm_probe.so tools/hbm_probe.hip
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -90,9 +91,43 @@ __global__ __launch_bounds__(256) void k_gather16(const uint4 *__restrict__ s, u
     for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) d[didx[i]] = s[sidx[i]];
 }
 
+// The decode / header-pass ceiling (round 5): one lane per item reads NB 16-B
+// chunks at src + i * stride (isolated header reads: k_decode reads each frame's first 32 B at the
+// frame pitch, k_encode_heads each payload's first bytes at the payload pitch), and with W writes a
+// 16-B record per item to dst (dense).  One lane per item, as the kernels do.
+template <int NB, bool W>
+__global__ __launch_bounds__(256) void k_strided(const uint8_t *__restrict__ s, uint4 *__restrict__ d, uint32_t *out,
+                                                 uint64_t n, uint64_t stride) {
+    const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
+    if (i >= n) return;
+    const uint4 *p = reinterpret_cast<const uint4 *>(s + i * stride);
+    uint4 v = p[0];
+    if (NB > 1) {
+        const uint4 b = p[1];
+        v.x ^= b.x; v.y ^= b.y; v.z ^= b.z; v.w ^= b.w;
+    }
+    if (W) d[i] = v;
+    else if ((v.x ^ v.y ^ v.z ^ v.w) == 0x12345678u) out[0] = 1u;  // keeps the loads live
+}
+
 }  // namespace
 
 extern "C" {
+// the isolated-read pattern above: nb 16-B chunks per item (1 or 2), write = 1 adds a dense 16-B
+// record per item; stride in bytes (a multiple of 16)
+int probe_strided(void *src, void *dst, uint64_t n, uint64_t stride, int nb, int write, void *stream) {
+    hipStream_t st = (hipStream_t)stream;
+    const unsigned grid = (unsigned)((n + 255) / 256);
+    const uint8_t *s = (const uint8_t *)src;
+    uint4 *d = (uint4 *)dst;
+    uint32_t *o = (uint32_t *)dst;
+    if (nb == 2 && write) hipLaunchKernelGGL((k_strided<2, true>), dim3(grid), dim3(256), 0, st, s, d, o, n, stride);
+    else if (nb == 2) hipLaunchKernelGGL((k_strided<2, false>), dim3(grid), dim3(256), 0, st, s, d, o, n, stride);
+    else if (write) hipLaunchKernelGGL((k_strided<1, true>), dim3(grid), dim3(256), 0, st, s, d, o, n, stride);
+    else hipLaunchKernelGGL((k_strided<1, false>), dim3(grid), dim3(256), 0, st, s, d, o, n, stride);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 // the gather-copy above over n listed chunks (didx / sidx: 16-B chunk indices into dst / src)
 int probe_gather(void *src, void *dst, const void *didx, const void *sidx, uint64_t n, int grid, void *stream) {
     hipLaunchKernelGGL(k_gather16, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const uint4 *)src, (uint4 *)dst,
