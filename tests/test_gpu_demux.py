@@ -144,3 +144,20 @@ def test_demux_decoded_c4(codec, gpu, oracle):
     exp = oracle.demux_batch(st, h(dec.cmd, np.uint8), fields, h(dec.id, np.uint8), h(dec.conv, np.uint32),
                              h(dec.conn_key, np.uint64), None)
     assert out.segments() == exp[0]
+
+
+@pytest.mark.parametrize("shape,fields", [((1 << 20, 7000, 0.0, 0.97), A.DEMUX_ID | A.DEMUX_CONN_KEY | A.DEMUX_CMD_BARRIER),
+                                          ((1 << 20, 64, 0.001, 1.0), A.DEMUX_ID | A.DEMUX_CONN_KEY | A.DEMUX_CMD_BARRIER),
+                                          ((1 << 20, 7000, 0.0, 0.8), A.DEMUX_CONN_KEY)])
+def test_demux_bench_shapes(codec, gpu, oracle, shape, fields):
+    """The bench's demux shapes at 1M packets (tools/bench_paths.py: C3-like thousands of keys spread over
+    every tile -- every packet probes the global table, whose slots name packet indices and are lowered
+    by CAS across concurrent tiles; 64 connections with 0.1 % control packets -- epochs by packet index,
+    2-3 radix passes), with invalid packets between the valid ones, against the oracle."""
+    n, nkeys, p_ctrl, p_valid = shape
+    rng = np.random.default_rng(nkeys + int(p_valid * 100))
+    case = make_case(rng, n, nkeys, p_ctrl, p_valid)
+    got = run_gpu(codec, gpu, *case[:2], fields, *case[2:])
+    exp = oracle.demux_batch(case[0], case[1], fields, *case[2:])
+    assert got[1] == exp[1] and len(got[0]) == len(exp[0])
+    assert got[0] == exp[0]
