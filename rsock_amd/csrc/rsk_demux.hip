@@ -43,10 +43,7 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
-#ifndef RSK_DM_ITEMS
-#define RSK_DM_ITEMS 16
-#endif
-constexpr uint32_t kItems = RSK_DM_ITEMS;       // radix: items per thread per tile (A/B builds: -DRSK_DM_ITEMS)
+constexpr uint32_t kItems = 16;  // items per thread per radix / look-back tile (8: C3 +4 % r03, +13 % r05)
 constexpr uint32_t kTile = kBlock * kItems;     // 4096 packets per radix tile
 constexpr uint32_t kNone = 0xffffffffu;
 constexpr uint32_t kCtrl = 0xffffffffu;         // pep[] marker: control packet (singleton segment)
