@@ -141,7 +141,8 @@ struct DmIn {
     const uint32_t *conv;
     const uint64_t *key;
     const uint32_t *dst;
-    uint32_t *pep;  // with CMD_BARRIER: epoch of each VALID data packet, by packet index (else null: 0)
+    uint32_t *pep;   // with CMD_BARRIER: epoch of each VALID data packet, by packet index (else null: 0)
+    uint32_t *cpos;  // with CMD_BARRIER: packet index of the c-th VALID control packet; cpos[n_ctrl] = n
     uint32_t n, fields;
 };
 
@@ -269,9 +270,11 @@ __device__ __forceinline__ uint64_t key_hash(const Key &k) {
 // compare-and-swap (the fingerprint half never changes once claimed).  A relaxed load comes first:
 // a hot key's slot is read, not written, by every later tile (no RMW unless the index drops); a new
 // key costs the load and one CAS (round 2, first half: a load, a CAS and a separate atomicMin word).
+// [es, ee): the packets of the key's epoch (with CMD_BARRIER; cpos) -- an owner outside it has another
+// epoch, so its epoch is checked by its index instead of a third gather (round 5)
 __device__ __forceinline__ uint32_t global_probe(const DmIn &a,
                                                  unsigned long long *slots, uint32_t mask, const Key &k,
-                                                 uint64_t hv, uint32_t j) {
+                                                 uint64_t hv, uint32_t j, uint32_t es, uint32_t ee) {
     // j is the packet index (monotone with the compacted index, so the minimum is the same packet):
     // a slot's owner is confirmed on the inputs at that index directly (round 5: one dependent
     // gather less than through the compacted index, C3 0.400 -> 0.372 ms with the 512-packet tiles)
@@ -286,7 +289,7 @@ __device__ __forceinline__ uint32_t global_probe(const DmIn &a,
         }
         if ((uint32_t)(e >> 32) == fp) {
             const uint32_t o = (uint32_t)e;
-            if (key_eq(load_key(a, o, a.pep ? a.pep[o] : 0u), k)) {
+            if (o >= es && o < ee && key_eq(load_key(a, o, k.ep), k)) {
                 while ((uint32_t)e > j) {  // lower the key's first index to j
                     const unsigned long long f = atomicCAS(slots + h, e, mine);
                     if (f == e) break;
@@ -320,6 +323,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_insert(DmIn a, const uint32_t *nv
     __shared__ unsigned long long ltab[kLtab];
     __shared__ uint32_t lmin[kLtab];  // block-minimum index per key, then (phase 2b) the key's global slot
     __shared__ uint32_t elo, ehi;     // epochs of the tile's first and last data packets
+    __shared__ uint32_t erng[4];      // their packet ranges [start, end) (CMD_BARRIER)
     const uint32_t nv = *nvp;
     const uint32_t base = blockIdx.x * kInsTile, t = threadIdx.x;
     if (base >= nv) return;  // block-uniform
@@ -389,6 +393,17 @@ __global__ __launch_bounds__(kBlock) void k_dm_insert(DmIn a, const uint32_t *nv
         }
     }
     __syncthreads();
+    if (t == 0u) {  // the packets of epochs elo and ehi: between consecutive control packets
+        uint32_t r[4] = {0u, ~0u, 0u, ~0u};
+        if (a.cpos && elo != kNone) {
+            r[0] = elo == 0u ? 0u : a.cpos[elo - 1u] + 1u;
+            r[1] = a.cpos[elo];
+            r[2] = ehi == 0u ? 0u : a.cpos[ehi - 1u] + 1u;
+            r[3] = a.cpos[ehi];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) erng[q] = r[q];
+    }
     uint32_t rep = 0;  // bit it: this thread's item `it` is its key's first packet in the block
 #pragma unroll
     for (uint32_t it = 0; it < kInsItems; ++it)
@@ -399,8 +414,9 @@ __global__ __launch_bounds__(kBlock) void k_dm_insert(DmIn a, const uint32_t *nv
         if (!((rep >> it) & 1u)) continue;
         const uint32_t j = pkr[it];  // leaders are named by packet index
         const Key &k = kr[it];
-        lmin[lpos[it]] = (k.ep == elo || k.ep == ehi)
-                             ? global_probe(a, slots, mask, k, key_hash(k), j)
+        const bool lo = k.ep == elo;
+        lmin[lpos[it]] = (lo || k.ep == ehi)
+                             ? global_probe(a, slots, mask, k, key_hash(k), j, erng[lo ? 0 : 2], erng[lo ? 1 : 3])
                              : kLeadTag | j;
     }
     __syncthreads();
@@ -487,7 +503,10 @@ __global__ __launch_bounds__(kBlock) void k_dm_flags_prep(DmIn a, unsigned long 
         }
     } else if (w == 1u) {
         const uint32_t e = dlb_wave(st_c, b, ac, lane, err);
-        if (lane == 0u) pre[1] = e;
+        if (lane == 0u) {
+            pre[1] = e;
+            if (b == gridDim.x - 1u && a.cpos) a.cpos[e + ac] = a.n;  // sentinel: the last epoch ends at n
+        }
     }
     __syncthreads();
     const uint64_t lt = lanemask_lt(lane);
@@ -509,7 +528,12 @@ __global__ __launch_bounds__(kBlock) void k_dm_flags_prep(DmIn a, unsigned long 
             const uint32_t i = b * kTile + r * kBlock + t;
             const uint32_t j = accv + bv + (uint32_t)__popcll(mv[r][w] & lt);
             cidx[j] = i;
-            if (a.pep) a.pep[i] = ((flags >> (16 + r)) & 1u) ? kCtrl : accc + bc + (uint32_t)__popcll(mc[r][w] & lt);
+            if (a.pep) {
+                const bool ctl = ((flags >> (16 + r)) & 1u) != 0u;
+                const uint32_t ec = accc + bc + (uint32_t)__popcll(mc[r][w] & lt);  // control packets before i
+                a.pep[i] = ctl ? kCtrl : ec;
+                if (ctl) a.cpos[ec] = i;
+            }
         }
         accv += tv;
         accc += tc;
@@ -821,7 +845,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_final(const uint32_t *nvp, const 
 
 // ---- workspace ------------------------------------------------------------------------------
 struct DmWs {
-    uint32_t *cidx, *hslot, *rank_at, *pep;
+    uint32_t *cidx, *hslot, *rank_at, *pep, *cpos;
     uint32_t *kA, *vA, *kB, *vB;
     uint32_t *ghist;
     unsigned long long *slots;  // slots | look-back states: one 0xff fill per call
@@ -850,6 +874,7 @@ size_t dm_layout(uint32_t n, uint8_t *base, DmWs *w) {
     d.hslot = (uint32_t *)take(4ull * n);
     d.rank_at = (uint32_t *)take(4ull * n);
     d.pep = (uint32_t *)take(4ull * n);
+    d.cpos = (uint32_t *)take(4ull * n + 4ull);
     d.kA = (uint32_t *)take(4ull * n);
     d.vA = (uint32_t *)take(4ull * n);
     d.kB = (uint32_t *)take(4ull * n);
@@ -909,6 +934,7 @@ extern "C" int rsk_demux_batch(rsk_ctx *c, uint32_t n, const rsk_demux_in *in, u
     a.n = n;
     a.fields = fields;
     a.pep = (fields & RSK_DEMUX_CMD_BARRIER) ? w.pep : nullptr;
+    a.cpos = (fields & RSK_DEMUX_CMD_BARRIER) ? w.cpos : nullptr;
     // one fill: the key table and every look-back state word start as all-ones
     hipError_t e = hipMemsetAsync(w.slots, 0xff, w.fill_bytes, s);
     if (e != hipSuccess) { rsk::set_error("hipMemsetAsync(table)", e); return RSK_EDEVICE; }
