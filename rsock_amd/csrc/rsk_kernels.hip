@@ -945,7 +945,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_heads(EncArgs a, KeySched ks,
     stage_tags(ks);
     enc_sample(a.pay_len, a.n, stat);
     const uint64_t i = base + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    const Lane1 L = encode_phase1<true>(a, ks, i < a.n ? i : a.n);
+    const Lane1 L = encode_phase1<true, true>(a, ks, i < a.n ? i : a.n);
     if (i < a.n && L.st > 0) {
         heads[2 * i] = make_uint4(L.H[0], L.H[1], L.H[2], L.H[3]);
         heads[2 * i + 1] = make_uint4(L.H[4], L.H[5], L.H[6], L.H[7]);
