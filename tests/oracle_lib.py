@@ -14,6 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle.so")
 REF_SO = os.path.join(ROOT, "oracle", "_ref", "librsk_ref.so")
 REF_PARSE_SO = os.path.join(ROOT, "oracle", "_ref", "librsk_ref_parse.so")
+REF_DEMUX_SO = os.path.join(ROOT, "oracle", "_ref", "librsk_ref_demux.so")
 
 _vp = ctypes.c_void_p
 
@@ -390,6 +391,79 @@ class RefParse:
         for k in ("ret", "payload_len", "base_ret"):
             r[k] = int(np.int32(np.uint32(r[k])))
         return r
+
+
+class RefDemux:
+    """The reference's own receive routing (oracle/_ref/librsk_ref_demux.so: ServerGroup, SubGroup,
+    ClientGroup, IAppGroup, INetGroup, IGroup, IConn, INetConn, CConn compiled from /root/reference;
+    oracle/ref_demux_harness.cpp records what reaches each conn).  RTLD_LAZY as RefParse."""
+
+    SERVER, CLIENT = 0, 1
+    EV_CREATE, EV_DELIVER, EV_RST_IN, EV_KA_IN, EV_CONV_RST, EV_NETCONN_RST, EV_DEFAULT_IN = range(1, 8)
+    LV_GROUP, LV_NET, LV_LEAF = 0, 1, 2
+
+    def __init__(self, path: str = REF_DEMUX_SO):
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        L = self.L = ctypes.CDLL(path, mode=os.RTLD_LAZY)
+        L.ref_demux_run.argtypes = [ctypes.c_int, ctypes.c_uint32] + [_vp] * 7 + [ctypes.c_uint32, _vp,
+                                    ctypes.c_uint32, _vp, ctypes.c_uint32, _vp, _vp, ctypes.c_uint32, _vp,
+                                    _vp, _vp, _vp, _vp, ctypes.c_uint32, _vp]
+
+    def run(self, stack: int, status, cmd, ids, conv, conn_key, dst, order=None, known_keys=(),
+            known_convs=()) -> dict:
+        """Route the VALID packets in `order` (default: arrival order).  Returns the raw log:
+        ret [n] int32 (0 for packets not routed), ev [k, 4] int64 (kind, conn, pkt, aux) and the conn
+        table (level, parent, key bytes)."""
+        n = len(status)
+        c = lambda a, t: np.ascontiguousarray(np.asarray(a, t))
+        valid = c(np.asarray(status) == 1, np.int8)  # RSK_RECV_VALID: what RConn::OnRecv passes up
+        cmd, conv, dst = c(cmd, np.uint8), c(conv, np.uint32), c(dst, np.uint32)
+        ids, conn_key = c(ids, np.uint8).reshape(-1), c(conn_key, np.uint64)
+        order = c(np.arange(n) if order is None else order, np.uint32)
+        kk, kc = c(list(known_keys), np.uint64), c(list(known_convs), np.uint32)
+        ret = np.zeros(n, np.int32)
+        ev_cap = 4 * n + 16
+        conn_cap = 3 * n + len(kk) + len(kc) + 16
+        ev = np.zeros((ev_cap, 4), np.int64)
+        lvl, par = np.zeros(conn_cap, np.int32), np.zeros(conn_cap, np.int32)
+        key, klen = np.zeros((conn_cap, 48), np.uint8), np.zeros(conn_cap, np.uint32)
+        n_ev, n_conn = np.zeros(1, np.uint32), np.zeros(1, np.uint32)
+        rc = self.L.ref_demux_run(stack, n, _p(valid), _p(cmd), _p(ids), _p(conv), _p(conn_key), _p(dst),
+                                  _p(order), len(order), _p(kk), len(kk), _p(kc), len(kc), _p(ret), _p(ev),
+                                  ev_cap, _p(n_ev), _p(lvl), _p(par), _p(key), _p(klen), conn_cap, _p(n_conn))
+        assert rc == 0, rc
+        nc = int(n_conn[0])
+        conns = [(int(lvl[i]), int(par[i]), bytes(key[i, :klen[i]])) for i in range(nc)]
+        return {"ret": ret, "ev": ev[:int(n_ev[0])].copy(), "conns": conns}
+
+    @classmethod
+    def conn_path(cls, conns, c: int) -> tuple:
+        """A conn's identity: its (level, key) and those of the groups above it."""
+        out = []
+        while c >= 0:
+            lv, par, k = conns[c]
+            out.append((lv, k))
+            c = par
+        return tuple(reversed(out))
+
+    @classmethod
+    def trace(cls, log: dict) -> dict:
+        """The observable effect of a routing run: per conn (by identity) the packets it received in
+        order, the order each level created its conns, and the control / reset events in order."""
+        conns, per_conn, created, events = log["conns"], {}, {}, []
+        for kind, c, pkt, aux in log["ev"].tolist():
+            if kind == cls.EV_CREATE:
+                created.setdefault(conns[c][0], []).append(cls.conn_path(conns, c))
+            elif kind == cls.EV_DELIVER:
+                per_conn.setdefault(cls.conn_path(conns, c), []).append(pkt)
+            else:
+                events.append((kind, pkt, aux))
+        return {"per_conn": per_conn, "created": created, "events": events, "ret": log["ret"]}
+
+
+def ref_demux_available() -> bool:
+    return os.path.exists(REF_DEMUX_SO)
 
 
 def ref_available() -> bool:

@@ -161,3 +161,49 @@ def test_demux_bench_shapes(codec, gpu, oracle, shape, fields):
     exp = oracle.demux_batch(case[0], case[1], fields, *case[2:])
     assert got[1] == exp[1] and len(got[0]) == len(exp[0])
     assert got[0] == exp[0]
+
+
+def _golden():
+    from tests.test_demux_ref import golden_cases
+
+    return golden_cases()
+
+
+@pytest.mark.parametrize("ci", range(10))
+def test_demux_golden_reference_routing(codec, gpu, oracle, ci):
+    """rsk_demux_batch against the REFERENCE's own routing (tests/golden/demux.npz: what rsock's
+    ServerGroup / SubGroup / ClientGroup / IAppGroup / INetGroup did with each packet, in arrival
+    order; tests/golden/make_demux_golden.py): delivering the GPU's segments in order gives every
+    leaf conn its packets in the reference's order, creates leaves and groups in its order, keeps
+    control packets in place and needs one lookup per segment (tests/demux_ref.check_segments)."""
+    from tests import demux_ref as D
+
+    cases = _golden()
+    assert len(cases) == 10
+    c = cases[ci]
+    got, nv = run_gpu(codec, gpu, c["status"], c["cmd"], c["fields"], c["id"], c["conv"], c["conn_key"], c["dst"])
+    assert nv == int((c["status"] == A.RECV_VALID).sum())
+    D.check_segments(got, c["status"], c["cmd"], c, c["stack"] == D.SERVER)
+    exp = oracle.demux_batch(c["status"], c["cmd"], c["fields"], c["id"], c["conv"], c["conn_key"], c["dst"])
+    assert got == exp[0]
+
+
+@pytest.mark.parametrize("fields", [A.DEMUX_ID | A.DEMUX_CONN_KEY | A.DEMUX_CMD_BARRIER,
+                                    A.DEMUX_CONN_KEY | A.DEMUX_CMD_BARRIER, ALL | A.DEMUX_CMD_BARRIER])
+def test_demux_epoch_edges_same_key(codec, gpu, oracle, fields):
+    """The same (IdBuf, connKey) on both sides of control packets placed at insert / look-back tile
+    edges (511/512, 1023/1024, 4095/4096/4097, 8191/8192), one epoch spanning several tiles, and
+    back-to-back barriers — the owner-epoch range test of the insert kernel."""
+    n = 20000
+    status = np.ones(n, np.int8)
+    cmd = np.zeros(n, np.uint8)
+    for i in (511, 512, 1023, 1024, 4095, 4096, 4097, 8191, 8192, 8193, 8194):
+        cmd[i] = 1 + i % 4
+    ids = np.tile(np.frombuffer(b"ABCDEFGH", np.uint8), n)
+    ckey = np.where(np.arange(n) % 3 == 0, 0x27111000, 0x27128001).astype(np.uint64)
+    conv = (np.arange(n) % 2).astype(np.uint32)
+    dst = np.full(n, 0x0200000a, np.uint32)
+    got = run_gpu(codec, gpu, status, cmd, fields, ids, conv, ckey, dst)
+    exp = oracle.demux_batch(status, cmd, fields, ids, conv, ckey, dst)
+    assert got[1] == exp[1]
+    assert got[0] == exp[0]
