@@ -16,7 +16,10 @@ the step's stream around the same launches issued one by one right after the tim
 
 Workload: N = 1 defaults to C3 (4M x 1400-B packets, the metric's target config); N > 1 defaults
 to C5 (BASELINE configs[4]: 64M x 1400-B packets in total, contiguous shards, strong scaling), so
-`--gpus 8` IS config 5 and `--gpus 1 --config c5` is the scaling curve's N = 1 point.
+`--gpus 8` IS config 5.  The scaling curve's N = 1 point is the `scale_n1_c5` key of the default
+N = 1 line: after the C3 headline (and its tag variant) the C3 arenas are freed and C5 is timed whole
+on the same GPU with the same step (`--gpus 1 --config c5` makes it the headline instead).  A
+1/2/4/8 curve therefore reads scale_n1_c5.value at N = 1 and value at N = 2, 4, 8.
 
 N > 1: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set) this process is one rank;
 without a launcher, `--gpus N` starts the N rank processes itself (from this parent, which never
@@ -215,6 +218,119 @@ def launch_ranks(n: int) -> int:
     return rc if rc >= 0 else 128 - rc
 
 
+def make_runner(torch, dist, workload, d, w, cx, stream, graph_mode: bool):
+    """The timed step on one shard: returns timed(mode, steps, warmup, sync_ranks) -> (elapsed, evs)
+    and the holder of the encode path the captured graph replays."""
+    cx.reserve(d.n, stream=stream)
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        cx.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
+                        w.status, id_uniform=workload.ID_UNIFORM, pad16=d.pad == 16, pad128=d.pad == 128,
+                        stream=stream)
+        if ev is not None:
+            ev[1].record(stream)
+        cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, w.dec, stream=stream)
+        if ev is not None:
+            ev[2].record(stream)
+
+    # correctness gate on the measured data: every packet must verify
+    expect_valid = int(((d.pay_len >= 1) & (d.pay_len <= 1469)).sum())
+
+    def gate(when):
+        nv = int(w.dec.n_valid.item())
+        if nv != expect_valid:
+            raise SystemExit(f"bench: decode verified {nv} of {expect_valid} packets ({when}, tag {cx.tag_mode})")
+
+    captured_path = [None]
+
+    def timed(mode: str, steps: int, warmup: int, sync_ranks: bool):
+        """Warm up, capture the step as a graph (the tag mode is fixed at capture), time `steps`
+        replays between barriers, then per-kernel HIP events on the step's stream."""
+        cx.set_tag_mode(mode)
+        with torch.cuda.stream(stream):
+            for _ in range(warmup):
+                step()
+        torch.cuda.synchronize()
+        gate("warmup")
+        graph = None
+        if graph_mode:
+            # the whole step (k_encode, k_decode, k_compact) as one HIP graph: one launch per step from
+            # the host instead of three library calls, so the timed region measures the GPU, not Python
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=stream):
+                step()
+            captured_path[0] = (cx.last_encode_path, cx.last_copy_k)  # the path the graph replays
+            w.dec.n_valid.zero_()
+            graph.replay()
+            torch.cuda.synchronize()
+            gate("graph replay")
+            for _ in range(warmup):  # the warmup steps again, as replays of the graph
+                graph.replay()
+            torch.cuda.synchronize()
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+        if sync_ranks:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            if graph is not None:
+                graph.replay()
+            else:
+                step(evs[k])
+        torch.cuda.synchronize()
+        if sync_ranks:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        gate("timed region")
+        cx.check_device_errors()  # raises if a compaction look-back gave up (rsk_check_device_errors)
+        if graph is not None:
+            # per-kernel durations for the roofline: HIP events on the step's stream around the same
+            # launches, issued one by one (the graph replays the identical kernels and arguments)
+            with torch.cuda.stream(stream):
+                for k in range(steps):
+                    step(evs[k])
+            torch.cuda.synchronize()
+            del graph
+        return el, evs
+
+    return timed, captured_path
+
+
+def scale_anchor_c5(torch, dist, rc, workload, dev, gpu, tag: str, steps: int, warmup: int, graph_mode: bool):
+    """The 1 -> 8 GPU curve's N = 1 point: BASELINE config 5 whole (64M x 1400-B
+    packets, ~185 GB of arenas) on this one GPU, the same step and timing as the N > 1 default
+    (`--gpus N` runs C5 split N ways, strong scaling).  Reported under `scale_n1_c5`, never as value."""
+    n_total = workload.CONFIGS["c5"][1]
+    d = workload.describe("c5", 0, n_total, n=n_total)
+    w = workload.DeviceWorkload(d, dev)
+    cx = rc.Codec(b"hello135", gpu, tag_mode=tag)
+    stream = torch.cuda.Stream(dev) if graph_mode else torch.cuda.current_stream()
+    try:
+        timed, captured = make_runner(torch, dist, workload, d, w, cx, stream, graph_mode)
+        el, evs = timed(tag, steps, warmup, False)
+        enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+        dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+        enc_bytes = int(enc_bytes_per_pkt(d.pay_len.astype(np.int64)).sum())
+        path = captured[0] if graph_mode else (cx.last_encode_path, cx.last_copy_k)
+        return {
+            "label": "NOT the headline: the scaling curve's N = 1 point -- C5 (64M x 1400-B packets, BASELINE "
+                     "configs[4]) whole on one GPU, the workload `--gpus N` (N > 1) splits N ways",
+            "config": "c5", "packets": d.n, "steps": steps, "warmup": warmup,
+            "value": round(d.n * steps / el / 1e6, 2), "unit": "Mpkt/s",
+            "ms_per_step": round(el / steps * 1e3, 4),
+            "kernels_ms": {"encode": round(enc_ms, 4), "decode+compact": round(dec_ms, 4)},
+            "encode_path": ENC_PATH_TEXT.get(path[0], "?").format(k=path[1]),
+            "roofline_frac": round(enc_bytes / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        }
+    finally:
+        cx.close()
+        del w
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -243,6 +359,8 @@ def main() -> None:
     ap.add_argument("--cpu-baseline-ref", action="store_true",
                     help="time the reference's own codec (oracle/_ref, build container only) as the CPU "
                          "baseline instead of the clean-room restatement")
+    ap.add_argument("--no-scale-anchor", action="store_true",
+                    help="skip the C5-on-one-GPU point (`scale_n1_c5`) timed after the C3 headline at N = 1")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal only: every rank uses GPU 0 (N ranks on a 1-GPU box)")
     args = ap.parse_args()
@@ -287,79 +405,7 @@ def main() -> None:
     # graph capture needs a stream other than the null stream; the codec's per-stream workspaces are
     # sized on it by the warmup, before the capture
     stream = torch.cuda.Stream(dev) if graph_mode else torch.cuda.current_stream()
-    cx.reserve(d.n, stream=stream)
-
-    def step(ev=None):
-        if ev is not None:
-            ev[0].record(stream)
-        cx.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
-                        w.status, id_uniform=workload.ID_UNIFORM, pad16=d.pad == 16, pad128=d.pad == 128,
-                        stream=stream)
-        if ev is not None:
-            ev[1].record(stream)
-        cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, w.dec, stream=stream)
-        if ev is not None:
-            ev[2].record(stream)
-
-    # correctness gate on the measured data: every packet must verify
-    expect_valid = int(((d.pay_len >= 1) & (d.pay_len <= 1469)).sum())
-
-    def gate(when):
-        nv = int(w.dec.n_valid.item())
-        if nv != expect_valid:
-            raise SystemExit(f"bench: decode verified {nv} of {expect_valid} packets ({when}, tag {cx.tag_mode})")
-
-    captured_path = [None]
-
-    def timed(mode: str, steps: int, warmup: int, sync_ranks: bool):
-        """Warm up, capture the step as a graph (the tag mode is fixed at capture), time `steps`
-        replays between barriers, then per-kernel HIP events on the step's stream."""
-        cx.set_tag_mode(mode)
-        with torch.cuda.stream(stream):
-            for _ in range(warmup):
-                step()
-        torch.cuda.synchronize()
-        gate(f"warmup")
-        graph = None
-        if graph_mode:
-            # the whole step (k_encode, k_decode, k_compact) as one HIP graph: one launch per step from
-            # the host instead of three library calls, so the timed region measures the GPU, not Python
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph, stream=stream):
-                step()
-            captured_path[0] = (cx.last_encode_path, cx.last_copy_k)  # the path the graph replays
-            w.dec.n_valid.zero_()
-            graph.replay()
-            torch.cuda.synchronize()
-            gate("graph replay")
-            for _ in range(warmup):  # the warmup steps again, as replays of the graph
-                graph.replay()
-            torch.cuda.synchronize()
-        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
-        if sync_ranks:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for k in range(steps):
-            if graph is not None:
-                graph.replay()
-            else:
-                step(evs[k])
-        torch.cuda.synchronize()
-        if sync_ranks:
-            dist.barrier()
-        el = time.perf_counter() - t0
-        gate("timed region")
-        cx.check_device_errors()  # raises if a compaction look-back gave up (rsk_check_device_errors)
-        if graph is not None:
-            # per-kernel durations for the roofline: HIP events on the step's stream around the same
-            # launches, issued one by one (the graph replays the identical kernels and arguments)
-            with torch.cuda.stream(stream):
-                for k in range(steps):
-                    step(evs[k])
-            torch.cuda.synchronize()
-            del graph
-        return el, evs
+    timed, captured_path = make_runner(torch, dist, workload, d, w, cx, stream, graph_mode)
 
     elapsed, evs = timed(args.tag, args.steps, args.warmup, world > 1)
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
@@ -392,6 +438,17 @@ def main() -> None:
         enc_o = float(np.mean([e[0].elapsed_time(e[1]) for e in evs_o]))
         dec_o = float(np.mean([e[1].elapsed_time(e[2]) for e in evs_o]))
         other = (omode, el_o, enc_o, dec_o)
+
+    anchor = None
+    if world == 1 and cfg == "c3" and not args.packets and not args.no_scale_anchor:
+        # free the C3 arenas, then the curve's N = 1 point on the same GPU (C5 whole: 185 of 288 GB)
+        cx.close()
+        cx = None
+        del w
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        anchor = scale_anchor_c5(torch, dist, rc, workload, dev, gpu, args.tag, min(args.steps, 10),
+                                 min(args.warmup, 3), graph_mode)
 
     if rank == 0:
         tr = load_traffic(cfg, d.n, d.frame_pitch)
@@ -450,11 +507,14 @@ def main() -> None:
                 "kernels_ms": {"encode": round(enc_o, 4), "decode+compact": round(dec_o, 4)},
                 "roofline_frac": round(enc_bytes / (enc_o * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             }
+        if anchor is not None:
+            line["scale_n1_c5"] = anchor
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(cfg, min(args.cpu_sample, d.n), args.cpu_seconds,
                                                 use_ref=args.cpu_baseline_ref)
         print(json.dumps(line), flush=True)
-    cx.close()
+    if cx is not None:
+        cx.close()
     if world > 1:
         dist.destroy_process_group()
 

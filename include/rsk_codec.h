@@ -141,7 +141,8 @@ int rsk_get_tag_mode(const rsk_ctx *ctx);
  *                         context's last sampled batch (table under rsk_encode_batch);
  *   RSK_ENC_PATH_PER_SET  one kernel, 64 packets per wave (every batch shape);
  *   RSK_ENC_PATH_TWO_PASS a header pass (MD5 tags 64 to a wave, 32-B records in the stream's scratch),
- *                         then one wave per packet (batches of long frames);
+ *                         then copy waves of 1, 2 or 4 packets: 4 below a mean payload of 880 B, 2 below
+ *                         1160 B, 1 above (batches of long frames);
  *   RSK_ENC_PATH_SHORT    the per-set kernel with every set on the flat chunk list (batches of short
  *                         frames).
  * Read when a call is issued, as the tag mode; RSK_EINVAL for an unknown path. */
@@ -158,9 +159,10 @@ int rsk_set_encode_path(rsk_ctx *ctx, int path);
  * kernels read is the immutable key schedule and tag table (and the tag mode, passed by value).
  *
  * Pre-size the scratch of `stream` (rsk_reserve: the legacy default stream, NULL) for batches of up
- * to n packets: the compaction state and, for n >= 16384 unless the context is held to a one-pass encode
- * path (RSK_ENC_PATH_PER_SET / _SHORT), the 32-B-per-packet header records of the two-pass encode
- * (rsk_encode_batch; a failed records allocation is not an error: eager calls allocate them on demand,
+ * to n packets: the compaction state and, for n >= 16384, the 32-B-per-packet header records of the
+ * two-pass encode -- only for a context that encodes: one held to RSK_ENC_PATH_TWO_PASS, or an AUTO
+ * context that has already run an rsk_encode_batch call (so a decode- or demux-only context pays
+ * nothing for them; a failed records allocation is not an error: eager calls allocate them on demand,
  * a captured call then takes the per-set kernel).  Batch calls grow the scratch on demand, which waits
  * for that stream to drain and allocates; reserve first if batch calls will be captured into a hipGraph. */
 int rsk_reserve(rsk_ctx *ctx, uint32_t n_max);
@@ -180,12 +182,17 @@ int rsk_release_stream(rsk_ctx *ctx, void *stream);
  * tile after ~4M polls, so that call's valid_idx / n_valid / demux outputs are wrong (a compaction
  * that gave up anywhere writes n_valid = 0xFFFFFFFF); the spin limit exists so that such a stall can
  * never hang the GPU.  rsk_check_device_errors waits for the context's streams (those it has
- * scratch on, and its shim stream; not the whole device), stores the flags in *flags
- * (may be NULL) and clears them; when any flag was set it returns RSK_EDEVICE and re-initialises
- * the context's look-back state on every stream at its next call there (graphs captured earlier
- * must be captured again). */
+ * scratch on, and its shim stream; not the whole device -- except for a context with a call captured
+ * into a hipGraph, whose replays may run on streams it never saw: then the whole device, until
+ * rsk_forget_captures), stores the flags in *flags (may be NULL) and clears them; when any flag was
+ * set it returns RSK_EDEVICE and re-initialises the context's look-back state on every stream at its
+ * next call there (graphs captured earlier must be captured again). */
 #define RSK_DEVERR_LOOKBACK 0x1u
 int rsk_check_device_errors(rsk_ctx *ctx, uint32_t *flags);
+/* The caller has destroyed every graph that captured this context's calls (or replays them only on
+ * streams this context has scratch on): rsk_check_device_errors waits for the context's streams
+ * again instead of the whole device. */
+int rsk_forget_captures(rsk_ctx *ctx);
 
 /* Text of the last HIP error seen by this thread (static storage). */
 const char *rsk_last_error(void);
@@ -234,8 +241,11 @@ typedef struct rsk_encode_out {
  * packets per copy wave, < 1160 B 2, else 1; smaller batches take the per-set kernel.
  * The statistic is a host-mapped word the previous calls' kernels left (read without synchronisation:
  * calls issued back to back see it late, which only delays a switch of traffic mix); the first such call
- * on a context, which has no statistic yet, samples its own batch and waits for that one 64-thread
- * launch on `stream` (a call being captured does not wait: it takes the per-set kernel).  A call
+ * on a context, which has no statistic yet, samples its own batch with one 64-thread launch on
+ * `stream` and waits for an event recorded behind it -- i.e. for `stream`'s work up to that launch,
+ * since a stream runs in order; a failed wait returns RSK_EDEVICE.  A call being captured does not
+ * wait (it takes the per-set kernel); on the legacy NULL stream, as for any launch there, no other
+ * stream may be capturing in hipStreamCaptureModeGlobal meanwhile.  A call
  * captured into a hipGraph keeps the path it was captured with, and one captured on a stream without
  * reserved records takes the per-set kernel.  rsk_set_encode_path fixes the path for a context
  * (e.g. one fed alternating long- and short-frame batches). */

@@ -137,6 +137,7 @@ SIGNATURES = [
     ("rsk_reserve_stream", ctypes.c_int, [_vp, ctypes.c_uint32, _vp]),
     ("rsk_release_stream", ctypes.c_int, [_vp, _vp]),
     ("rsk_check_device_errors", ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_uint32)]),
+    ("rsk_forget_captures", ctypes.c_int, [_vp]),
     ("rsk_last_error", ctypes.c_char_p, []),
     ("rsk_version", ctypes.c_char_p, []),
     ("rsk_encode_batch", ctypes.c_int,

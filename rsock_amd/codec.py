@@ -283,7 +283,7 @@ class Codec:
 
     def set_copy_k(self, k: int = 0) -> None:
         """Internal knob of the two-pass encode (rsk__set_copy_k): packets per copy wave (1, 2, 4; 0 = chosen
-        from the last sampled mean payload: 1 for long frames, 4 below 960 B)."""
+        from the last sampled mean payload: 4 below 880 B, 2 below 1160 B, 1 above; rsk_kernels.hip kAutoK*)."""
         fn = lib().rsk__set_copy_k
         fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
         _check(fn(self._ctx, k), "rsk__set_copy_k")
@@ -312,6 +312,11 @@ class Codec:
         if rc != 0:
             raise RskError(f"device error flags 0x{f.value:x}: {lib().rsk_last_error().decode()}")
         return f.value
+
+    def forget_captures(self) -> None:
+        """rsk_forget_captures: the graphs that captured this context's calls are gone, so
+        check_device_errors waits for the context's streams again, not the whole device."""
+        _check(lib().rsk_forget_captures(self._ctx), "rsk_forget_captures")
 
     def release_stream(self, stream=None) -> None:
         """rsk_release_stream: wait for `stream` and free its scratch."""

@@ -7,8 +7,8 @@
 //                   RSK_TAG_TABLE mode the key's 256-entry table staged in LDS); then, per wave,
 //                   the software-pipelined per-packet copy (4-packet batches of 16-B chunks, one
 //                   aligned payload load per chunk, funnel partner from the next lane by DPP) or
-//                   the flat chunk list for short frames.  The tiled mapping, the
-//                   unpipelined copy and k_copy_probe: A/B build only.
+//                   the flat chunk list for short frames; for batches of long frames the two-pass
+//                   form k_encode_heads + k_encode_copy (K = 1, 2 or 4 packets per copy wave).
 //   k_encode_wire   RConn::Output + RawTcp::SendRawTcp (conn/RawTcp.cpp:280-341): frames plus the
 //                   IPv4/TCP headers and checksums libnet writes, two-launch hybrid.
 //   k_encode_hdr /  header-only framing / verification on 32-B slots (host-resident deployments:
@@ -105,7 +105,7 @@ __device__ __forceinline__ void stage_tags(const KeySched &ks) {
 // ~1 %) and the two-pass header pass.  The framing kernels keep the generic schedule: in k_encode's
 // per-packet sets the specialised one raised the register budget past 128 VGPRs (3 waves per SIMD
 // instead of 4) and cost C2 / C4 13-16 % (profiles/r04_ab_md5_isa.json); for its flat sets (MODE 12)
-// round 4 measured a gain on an A/B build that specialised key word 2 only -- on the full build MODE 11
+// round 4 measured a gain on a build that specialised key word 2 only -- on the full build MODE 11
 // (generic) is as fast or 1 % faster (C2 0.0498-0.0501 vs 0.0499-0.0503 ms; 128 / 200-B batches -1 %,
 // profiles/r05_md5_mode11_vs_12.json), so the shipped per-set kernel is k_encode<11>.
 template <bool LANE = false>
@@ -388,108 +388,10 @@ __device__ __forceinline__ uint4 head_chunk(const uint32_t (&H)[8], uint32_t k, 
                       (hs.w & m.w) | (V.w & ~m.w));
 }
 
-template <int PU, int NT, bool TAG>
-__device__ __forceinline__ void copy_pkt(const EncArgs &a, const KeySched &ks, const Lane1 &L, uint32_t lane,
-                                         uint64_t vm) {
-    while (vm) {
-        uint32_t js[PU];
-        bool on[PU];
-        uint32_t myj = 0;  // lane p: the packet of the iteration's slot p
-        bool mine = false;
-#pragma unroll
-        for (int p = 0; p < PU; ++p) {
-            on[p] = vm != 0ull;
-            js[p] = on[p] ? (uint32_t)__builtin_ctzll(vm) : 0u;
-            if (on[p]) vm &= vm - 1ull;
-            if (lane == (uint32_t)p) {
-                myj = js[p];
-                mine = on[p];
-            }
-        }
-        uint32_t my_b0 = 0;
-        if constexpr (TAG) {  // payload[0] of the lane's slot packet, issued before the chunk loads
-            const uint64_t po = shfl64(L.po, myj);
-            if (mine) my_b0 = rsk::gptr(a.payload)[po];
-        }
-        uint4 A[PU][2];
-        uint8_t *d0[PU];
-        uint32_t flen[PU], sh[PU], rr[PU], nst[PU];
-#pragma unroll
-        for (int p = 0; p < PU; ++p) {
-            flen[p] = on[p] ? rdl((uint32_t)L.st, js[p]) : 0u;
-            const FrameGeo g = frame_geo(a.payload + rdl64(L.po, js[p]), a.frame + rdl64(L.fo, js[p]), flen[p], a.pad);
-            d0[p] = g.d0;
-            sh[p] = g.sh;
-            rr[p] = g.r;
-            flen[p] += g.r;  // frame bytes counted from d0
-            nst[p] = on[p] ? g.nst : 0u;
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const int32_t m = (int32_t)(lane + 64u * q) - 2;
-                A[p][q] = make_uint4(0u, 0u, 0u, 0u);
-                // slot 1 (chunks 64..127; lane 0's source chunk is chunk 63's funnel partner) only
-                // for frames of 64 chunks or more: a uniform branch
-                if (q == 1 && nst[p] < 64u) continue;
-                if (on[p] && m >= 0 && src_chunk_live(m, g.first_rel, g.last_rel)) A[p][q] = ld16<NT>(g.srcp + 16 * m);
-            }
-        }
-        uint32_t t0 = 0, t1 = 0;
-        if constexpr (TAG) {
-            tag_of(ks, my_b0, t0, t1);
-        } else {
-            // lane p stores the header chunks of its slot packet (store_head) beside the payload
-            // chunks, so each frame's first line is written whole while it is in L2
-            uint32_t H[8];
-#pragma unroll
-            for (int t = 0; t < 8; ++t) H[t] = (uint32_t)__shfl((int)L.H[t], (int)myj);
-            const uint64_t my_fo = shfl64(L.fo, myj);
-            if (mine) store_head(H, a.frame + my_fo);
-        }
-#pragma unroll
-        for (int p = 0; p < PU; ++p) {
-            if (!on[p]) continue;
-            uint4 B[2];
-            B[0] = make_uint4(wave_shl1(A[p][0].x), wave_shl1(A[p][0].y), wave_shl1(A[p][0].z), wave_shl1(A[p][0].w));
-            B[1] = make_uint4(0u, 0u, 0u, 0u);
-            if (nst[p] >= 64u) {  // uniform: the frame reaches slot 1
-                const uint4 l0 = make_uint4(rdl(A[p][1].x, 0), rdl(A[p][1].y, 0), rdl(A[p][1].z, 0),
-                                            rdl(A[p][1].w, 0));  // read in uniform flow (see k_encode)
-                if (lane == 63u) B[0] = l0;
-                if (nst[p] > 64u)
-                    B[1] = make_uint4(wave_shl1(A[p][1].x), wave_shl1(A[p][1].y), wave_shl1(A[p][1].z),
-                                      wave_shl1(A[p][1].w));
-            }
-            uint32_t Hj[8];  // TAG: the packet's header words (SGPRs), tag and payload[0] from lane p
-            if constexpr (TAG) {
-#pragma unroll
-                for (int t = 2; t < 8; ++t) Hj[t] = rdl(L.H[t], js[p]);
-                Hj[0] = rdl(t0, (uint32_t)p);
-                Hj[1] = rdl(t1, (uint32_t)p);
-                Hj[7] |= rdl(my_b0, (uint32_t)p) << 24;
-            }
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const uint32_t k = lane + 64u * q;
-                if (q == 1 && nst[p] <= 64u) continue;  // uniform
-                if (k >= nst[p] || (!TAG && k < 2u)) continue;
-                const uint4 V = rsk::funnel16(A[p][q], B[q], sh[p]);
-                if constexpr (TAG) {
-                    // TAG form: the header chunks in the packet's own slot stores (lanes 0..2)
-                    const uint4 v = k < (rr[p] >= 2u ? 3u : 2u) ? head_chunk(Hj, k, rr[p], V) : V;
-                    store_piece<NT>(d0[p] + 16u * k, v, k == 0u ? rr[p] : 0u, (int)flen[p] - 16 * (int)k,
-                                    a.pad != 0u);
-                } else {
-                    store_piece<NT>(d0[p] + 16u * k, V, k == 2u ? chunk2_lo(rr[p]) : 0u, (int)flen[p] - 16 * (int)k,
-                                    a.pad != 0u);
-                }
-            }
-        }
-    }
-}
-
 // ---- software-pipelined per-packet copy: the chunk loads of the next PU packets are issued before
 // the current PU packets are shifted and stored, so each wave keeps a batch of loads in flight
-// while it stores (copy_pkt waits for its own loads, then stores, then loads again).  Two register
+// while it stores (an unpipelined copy waits for its own loads, then stores, then loads again; the
+// round-1 form, measured in profiles/r01_ab_store_policy.json and r02_ab_encode_v2.json).  Two register
 // buffers of PU packets, the roles swapped by a 2x unrolled loop.  Every load instruction runs with
 // all lanes (a dead lane reads the arena's first chunk, which stays cached) so the batch's load
 // count is static and the wait for the older batch leaves the newer one in flight.
@@ -820,16 +722,17 @@ constexpr uint32_t kFlatBelowMeanBytes = 256;
 // carries fewer bytes per MD5 (C4: +10 % with the tag deferred).
 constexpr uint32_t kDeferTagMeanBytes = 1024;
 
-// One 64-packet set per wave: phase 1, then the chosen copy path.  MODE 11 (shipped): per-wave
-// choice of path, tag deferred into the copy loop for sets of long frames and behind the first
-// chunk loads for flat sets, pipelined per-packet copy; A/B build only: 6 = unpipelined, 9 = 11
-// with the flat sets' tag in phase 1, 10 = 9 with the tag in the copy loop for every per-packet
-// set, 3 = tag always in phase 1, 7 = flat path only, 8 = per-packet path only.  NT < 0: store
-// policy per set.
-template <int MODE, int PU, int U, int NT, int GRP = 64, int TG = 0>
+// One 64-packet set per wave: phase 1, then the chosen copy path.  MODE 11 (the per-set kernel):
+// per-wave choice of path -- the flat chunk list for sets of short frames (tag and header stores
+// behind the first chunk loads), the software-pipelined per-packet copy otherwise, with the tag
+// deferred into the copy loop for sets of long frames; MODE 19 (the short path): every set on the
+// flat list, for batches of short frames only (the per-packet copy's registers out of the kernel).
+// The store policy is chosen per set (below).
+template <int MODE, int PU, int U, int GRP = 64, int TG = 0>
 __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks, uint64_t i, uint32_t lane,
                                            CopyRec *recs, uint32_t *cend) {
-    Lane1 L = encode_phase1<MODE == 3 || MODE == 7>(a, ks, i);
+    static_assert(MODE == 11 || MODE == 19, "the per-set kernel and its flat-only build");
+    Lane1 L = encode_phase1<false>(a, ks, i);
     const bool vec = L.st > 0;  // every framed packet takes a vector path, at any alignment
     const uint64_t vm = __ballot(vec);
     // set mean frame length over framed packets (wave reduction)
@@ -837,29 +740,14 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
 #pragma unroll
     for (int off = 32; off; off >>= 1) fl += __shfl_xor(fl, off);
     const uint32_t cnt = (uint32_t)__popcll(vm);
-    // MODE 16 (A/B): 12 with every set on the flat list (a launch for batches of short frames only: the
-    // per-packet path's registers out of the kernel)
-    const bool flat = MODE == 7 || MODE == 16 || MODE == 19 ? true : MODE == 8 ? false : fl < kFlatBelowMeanBytes * cnt;
-    // MODE 10 (A/B): as 9 with the tag in the copy loop for every per-packet set
-    // MODE 18 (A/B): 12 without the TAG form (the tag in phase 1 for every set: a build for mid-length
-    // batches, without the long-frame copy's registers)
-    const bool defer = MODE != 3 && MODE != 7 && MODE != 18 && !flat && (MODE == 10 || fl >= kDeferTagMeanBytes * cnt);
-    // MODE 11 (shipped): as 9 with the flat sets' tag and header stores behind the first chunk loads;
-    // MODE 12 (A/B): 11 with the flat sets' MD5 on the payload-word-specialised schedule (md5_tag_lane)
-    // MODE 13 / 14 (A/B): 12 with the frames under 256 / 512 B of a per-packet set on the flat list
-    constexpr bool kFlatTagQ = MODE == 11 || MODE == 12 || MODE == 13 || MODE == 14 || MODE == 16 || MODE == 18 ||
-                               MODE == 19;
-    if constexpr (MODE != 3 && MODE != 7) {  // the tag now, except for the sets whose copy loop takes it
-        if (!defer && !(kFlatTagQ && flat)) encode_tag(a, ks, L);
-    }
+    const bool flat = MODE == 19 ? true : fl < kFlatBelowMeanBytes * cnt;
+    const bool defer = !flat && fl >= kDeferTagMeanBytes * cnt;
+    if (!defer && !flat) encode_tag(a, ks, L);  // the flat list and the deferred copy take it themselves
     if (flat) {
-        if (!kFlatTagQ && vec) store_head(L.H, a.frame + L.fo);
-        copy_flat<U, kFlatTagQ, MODE >= 12 && MODE != 19>(a, ks, L, lane, vec, recs, cend);
+        copy_flat<U, true, false>(a, ks, L, lane, vec, recs, cend);
         return;
     }
-    if constexpr (MODE == 16 || MODE == 19) return;  // flat only (19: with the generic MD5 schedule)
-    bool nt = NT == 2;
-    if constexpr (NT < 0) {
+    if constexpr (MODE == 11) {
         // Store policy per set: frames packed back to back (each frame's padded end is the next
         // frame's start, so every line of the span is written in full) keep normal stores; any gap
         // leaves partially written lines, which nontemporal stores write without the memory-side
@@ -870,13 +758,11 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
                              ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(L.fo >> 32), 1) << 32);
         const bool nvec = __shfl_down((int)vec, 1) != 0;
         // (lanes of the last packet of a group: the next lane's packet is not the next frame)
-        nt = __ballot(vec && nvec && lane % GRP != GRP - 1u && end != nfo) != 0ull;
-    }
-    // Header chunks: sets with the tag in the copy loop (long frames) store them in the packet's
-    // first slot store (lanes 0..2, words by readlane); the others by the slot lane (store_head).
-    // Measured (A/B, profiles/r02_ab_head.json): C3 2.34 vs 2.55 ms with the first; C4 0.389 vs
-    // 0.420 ms with the second.
-    if constexpr (MODE == 9 || MODE == 10 || MODE >= 11) {  // software-pipelined per-packet copy
+        const bool nt = __ballot(vec && nvec && lane % GRP != GRP - 1u && end != nfo) != 0ull;
+        // Header chunks: sets with the tag in the copy loop (long frames) store them in the packet's
+        // first slot store (lanes 0..2, words by readlane); the others by the slot lane (store_head).
+        // Measured (profiles/r02_ab_head.json): C3 2.34 vs 2.55 ms with the first; C4 0.389 vs
+        // 0.420 ms with the second.
         // Byte-packed long frames (no pad; a frame ends mid-chunk and the next packet's frame
         // starts there): the TAG-form copy with the boundary-chunk merge (TailCarry), which writes
         // each shared chunk as one 16-B store.  Only sets that really have such a pair take it: the
@@ -887,46 +773,19 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
         bool mrg = false;
         if (a.pad == 0u && defer) {
             const uint64_t fe = reinterpret_cast<uintptr_t>(a.frame + L.fo) + (uint32_t)L.st;
-            const uint64_t nfo = (uint64_t)(uint32_t)__shfl_down((int)(uint32_t)L.fo, 1) |
-                                 ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(L.fo >> 32), 1) << 32);
-            const bool nvec = __shfl_down((int)vec, 1) != 0;
             mrg = __ballot(vec && nvec && lane % GRP != GRP - 1u && (fe & 15u) != 0u &&
                            reinterpret_cast<uintptr_t>(a.frame + nfo) == fe) != 0ull;
         }
-        if (MODE != 18 && defer) {
-            if constexpr (MODE != 18) {
-                if (mrg) copy_pkt_pipe<PU, 0, true, TG, true>(a, ks, L, lane, vm);
-                else if (nt) copy_pkt_pipe<PU, 2, true, TG>(a, ks, L, lane, vm);
-                else copy_pkt_pipe<PU, 0, true, TG>(a, ks, L, lane, vm);
-            }
+        if (defer) {
+            if (mrg) copy_pkt_pipe<PU, 0, true, TG, true>(a, ks, L, lane, vm);
+            else if (nt) copy_pkt_pipe<PU, 2, true, TG>(a, ks, L, lane, vm);
+            else copy_pkt_pipe<PU, 0, true, TG>(a, ks, L, lane, vm);
         } else {
-            uint64_t pm = vm;
-            if constexpr (MODE == 13 || MODE == 14) {  // the set's short frames on the flat list first
-                constexpr int32_t kShort = MODE == 13 ? 256 : 512;
-                const bool shp = vec && L.st < kShort;
-                const uint64_t sm = __ballot(shp);
-                if (sm) {
-                    if (shp) store_head(L.H, a.frame + L.fo);
-                    copy_flat<U, false>(a, ks, L, lane, shp, recs, cend);
-                    pm &= ~sm;
-                }
-            }
-            if (nt) copy_pkt_pipe<PU, 2, false>(a, ks, L, lane, pm);
-            else copy_pkt_pipe<PU, 0, false>(a, ks, L, lane, pm);
+            if (nt) copy_pkt_pipe<PU, 2, false>(a, ks, L, lane, vm);
+            else copy_pkt_pipe<PU, 0, false>(a, ks, L, lane, vm);
         }
-        return;
-    }
-    if (defer) {
-        if (nt) copy_pkt<PU, 2, true>(a, ks, L, lane, vm);
-        else copy_pkt<PU, 0, true>(a, ks, L, lane, vm);
-    } else {
-        if (nt) copy_pkt<PU, 2, false>(a, ks, L, lane, vm);
-        else copy_pkt<PU, 0, false>(a, ks, L, lane, vm);
     }
 }
-
-
-
 
 // ---- the two-pass form for batches of long frames (round 4) ---------------------------------------
 // Pass 1, k_encode_heads: phase 1 one lane per packet (status, the MD5 tag, EncHead, payload[0]; the
@@ -1079,38 +938,21 @@ __global__ __launch_bounds__(kBlock) void k_encode_copy(EncArgs a, const uint32_
 // packets (descriptor loads coalesced per 8-packet group), but the resident waves copy one compact
 // stretch of the arenas at a time (SBW * GRP packets per super-block) instead of each its own region
 // 64 packets from the next wave's: C3 -3.7 %, C4 -4.1 %, C2 within 1 % against the tiled mapping
-// (profiles/r02_ab_encode_mapping.json).  The grid holds only waves that own a packet (enc_grid).
-// XCD (A/B): blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md); XCD = true renumbers
-// them so that each XCD's blocks own consecutive waves (descriptor lines stay in one XCD's L2).
-template <int MODE, int PU, int U, int NT, int GRP, int SBW, bool XCD, int TG>
-__device__ __forceinline__ void encode_grid(const EncArgs &a, const KeySched &ks) {
+// (profiles/r02_ab_encode_mapping.json; renumbering the blocks so that each XCD's blocks own
+// consecutive waves measured no gain, profiles/r01_ab_xcd_map.json).  The grid holds only waves
+// that own a packet (enc_grid).
+template <int MODE, int PU, int U, int GRP, int SBW, int TG = 0>
+__global__ __launch_bounds__(kBlock) void k_encode(EncArgs a, KeySched ks) {
     __shared__ CopyRec recs[kWavesPerBlock][64];
     __shared__ uint32_t cend[kWavesPerBlock][64];
     stage_tags(ks);
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    uint32_t blk = blockIdx.x;
-    if constexpr (XCD) {
-        const uint32_t per = gridDim.x / 8u;
-        if (blk < per * 8u) blk = (blk % 8u) * per + blk / 8u;
-    }
-    const uint64_t wg = (uint64_t)blk * kWavesPerBlock + w;
+    const uint64_t wg = (uint64_t)blockIdx.x * kWavesPerBlock + w;
     const uint64_t sb = wg / SBW, wl = wg % SBW;
     const uint64_t first = sb * SBW * 64u + wl * GRP;  // the wave's smallest packet
     if (first >= a.n) return;  // wave-uniform
     const uint64_t i = sb * SBW * 64u + ((uint64_t)(lane / GRP) * SBW + wl) * GRP + lane % GRP;
-    encode_set<MODE, PU, U, NT, GRP, TG>(a, ks, i < a.n ? i : a.n, lane, recs[w], cend[w]);
-}
-
-template <int MODE, int PU, int U, int NT, int GRP, int SBW, bool XCD = false, int TG = 0>
-__global__ __launch_bounds__(kBlock) void k_encode(EncArgs a, KeySched ks) {
-    encode_grid<MODE, PU, U, NT, GRP, SBW, XCD, TG>(a, ks);
-}
-
-
-// the same kernel held to 128 VGPRs (4 waves per SIMD): W = 8 lets the compiler aim higher, W = 4 not
-template <int MODE, int PU, int U, int NT, int GRP, int SBW, int TG, int W>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, W))) void k_encode_w4(EncArgs a, KeySched ks) {
-    encode_grid<MODE, PU, U, NT, GRP, SBW, false, TG>(a, ks);
+    encode_set<MODE, PU, U, GRP, TG>(a, ks, i < a.n ? i : a.n, lane, recs[w], cend[w]);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -3091,7 +2933,8 @@ int rsk__set_two_pass_chunk(rsk_ctx *c, uint32_t packets) {
     return RSK_OK;
 }
 
-// Internal (tests, bench): the path the context's last rsk_encode_batch took (1 or 2; 0 before any).
+// Internal (tests, bench): the path the context's last rsk_encode_batch took (RSK_ENC_PATH_PER_SET,
+// _TWO_PASS or _SHORT: 1, 2 or 3; 0 before any).
 int rsk__last_encode_path(const rsk_ctx *c) { return c ? c->enc_last_path.load(std::memory_order_relaxed) : RSK_EINVAL; }
 
 // Internal (tests): the next compaction launch of this context runs with tile `tile` publishing
@@ -3131,18 +2974,25 @@ int rsk_check_device_errors(rsk_ctx *c, uint32_t *flags) {
     return RSK_EDEVICE;
 }
 
+int rsk_forget_captures(rsk_ctx *c) {
+    if (!c) return RSK_EINVAL;
+    c->captured.store(false, std::memory_order_relaxed);
+    return RSK_OK;
+}
+
 int rsk_reserve_stream(rsk_ctx *c, uint32_t n_max, void *stream) {
     if (!c) return RSK_EINVAL;
     DeviceGuard g(c->device);
     if (!g.ok) return RSK_EDEVICE;
     Compact ck;
     const int r = ensure_compact(c, n_max, (hipStream_t)stream, ck);
-    if (r || n_max < kTwoPassMinPackets || (c->enc_path != RSK_ENC_PATH_AUTO && c->enc_path != RSK_ENC_PATH_TWO_PASS))
-        return r;
-    // the two-pass encode's header records (32 B per packet) unless the context is held to a one-pass
-    // path.  A capture cannot allocate them, and an AUTO context's eager calls issued back to back all
-    // run before the first batch statistic reaches the host (they take the per-set kernel and never
-    // allocate): without this reserve bench.py's graph captured the per-set kernel (r05z kernel trace).
+    // the two-pass encode's header records (32 B per packet), for a context that encodes: held to the
+    // two-pass path, or AUTO with an encode call behind it (a decode- or demux-only context
+    // does not pay 32 B per packet for them).  A capture cannot allocate them: without this reserve
+    // bench.py's graph captured the per-set kernel (r05z kernel trace).
+    const bool encodes = c->enc_path == RSK_ENC_PATH_TWO_PASS ||
+                         (c->enc_path == RSK_ENC_PATH_AUTO && c->enc_last_path.load(std::memory_order_relaxed) != 0);
+    if (r || n_max < kTwoPassMinPackets || !encodes) return r;
     // A failed allocation is not an error: eager calls allocate on demand, a captured call
     // takes the per-set kernel.
     void *p = nullptr;
@@ -3172,14 +3022,21 @@ static int copy_k(rsk_ctx *c) {
 
 // Encode path per call: the context's forced path (rsk_set_encode_path), else AUTO's table above.
 // The first AUTO call of >= kTwoPassMinPackets packets on a context samples its own batch and waits
-// for that one 64-thread launch on its stream, so it already takes the table's path (without that,
-// back-to-back eager calls ran the per-set kernel until the first sample landed: 5 calls in
-// gpurun_out/r05f1/c3).  A capture never waits: it takes the per-set kernel when no sample exists.
+// for an event behind that one 64-thread launch on its stream, so it already takes the table's path
+// (without that, back-to-back eager calls ran the per-set kernel until the first sample landed: 5
+// calls in gpurun_out/r05f1/c3).  The event, not the stream: nothing queued on the
+// stream after the sample is waited for, and a failed wait is the call's error.  A capture never
+// waits: it takes the per-set kernel when no sample exists.  Returns the path, or RSK_EDEVICE.
 static int enc_path(rsk_ctx *c, uint32_t n, const uint16_t *pay_len, hipStream_t st) {
     if (c->enc_path) return c->enc_path;
     if (n >= kTwoPassMinPackets && c->enc_stat_dev && !(sampled_mean(c) & kStatValid) && !rsk::capturing(st)) {
         hipLaunchKernelGGL(k_enc_sample, dim3(1), dim3(64), 0, st, pay_len, n, c->enc_stat_dev);
-        (void)hipStreamSynchronize(st);
+        hipEvent_t ev = nullptr;
+        hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventRecord(ev, st);
+        if (e == hipSuccess) e = hipEventSynchronize(ev);
+        if (ev) (void)hipEventDestroy(ev);
+        if (e != hipSuccess) { set_error("enc_path: waiting for the batch sample", e); return RSK_EDEVICE; }
     }
     const uint32_t s = sampled_mean(c);
     if (n < kTwoPassMinPackets || !(s & kStatValid)) return RSK_ENC_PATH_PER_SET;
@@ -3215,6 +3072,7 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
     const dim3 gd(grid), bd(kBlock);
     (void)gd;
     const int path = enc_path(c, n, in->pay_len, st);
+    if (path < 0) return path;
     if (path == RSK_ENC_PATH_TWO_PASS) {
         // the two-pass form (batches of long frames): header records, then one wave per packet
         void *hp = nullptr;
@@ -3246,13 +3104,13 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
     if (path == RSK_ENC_PATH_SHORT) {
         // batches of short frames: the per-set kernel with every set on the flat chunk list, compiled
         // without the per-packet copy (fewer VGPRs, more waves per SIMD; profiles/r04ac_short_path.json)
-        hipLaunchKernelGGL((k_encode<19, 4, 2, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, 0, st, a, c->ks);
+        hipLaunchKernelGGL((k_encode<19, 4, 2, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, 0, st, a, c->ks);
         c->enc_last_path.store(RSK_ENC_PATH_SHORT, std::memory_order_relaxed);
     } else {
         // the per-set kernel: per-wave hybrid (flat chunk list for short frames, with the tag behind the
         // first chunk loads; software-pipelined one-load DPP per-packet copy, 4 packets per batch, for
         // the rest), tag in the copy loop for long-frame sets, per-set store policy
-        hipLaunchKernelGGL((k_encode<11, 4, 4, -1, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, 0, st, a, c->ks);
+        hipLaunchKernelGGL((k_encode<11, 4, 4, 8, 1024>), dim3(enc_grid(n, 8, 1024)), bd, 0, st, a, c->ks);
         c->enc_last_path.store(RSK_ENC_PATH_PER_SET, std::memory_order_relaxed);
     }
     // the statistic for the next call, on every call this path takes (a sample every 256th

@@ -5,7 +5,7 @@
 // payload[0] differs per lane, so one tag costs one compression for key_len <= 54 (two otherwise).
 // Round constants and rotations are compile-time literals: after full unrolling every K[i] is an
 // instruction immediate, which needs no LDS traffic and no VGPRs ("MD5 constants:
-// immediates vs LDS", measured against an LDS-staged table in the A/B build).
+// immediates vs LDS": an LDS-staged table measured slower, profiles/r03_ab_md5_lds.json).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -33,8 +33,8 @@ __host__ __device__ __forceinline__ uint32_t rotl(uint32_t x, int s) {
 }
 
 // Where the round constants come from.  KImm (shipped): K[I] is a compile-time literal, so after full
-// unrolling it is an instruction immediate.  A kernel may pass another source with a get<I>() (the
-// A/B build's LDS-staged table, rsk_kernels.hip) to measure the north star's "constants in LDS".
+// unrolling it is an instruction immediate.  A kernel may pass another source with a get<I>() (an
+// LDS-staged table, as round 3 measured for the north star's "constants in LDS").
 struct KImm {
     template <int I>
     __host__ __device__ __forceinline__ uint32_t get() const { return Md5Consts::K[I]; }

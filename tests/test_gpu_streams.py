@@ -422,3 +422,77 @@ def test_auto_capture_takes_two_pass_after_back_to_back_calls(gpu):
         del g
     finally:
         cx.close()
+
+
+def test_reserve_records_only_for_encoding_contexts(gpu):
+    """rsk_reserve_stream allocates the two-pass records (32 B per packet) only for a context
+    that encodes -- a decode-only AUTO context reserves the compaction state alone; after one encode call
+    the same reserve on a new stream also takes the records."""
+    import torch
+
+    from rsock_amd.codec import Codec
+
+    n = 1 << 22
+    cx = Codec(b"hello135", 0)
+    try:
+        s1, s2 = torch.cuda.Stream(gpu), torch.cuda.Stream(gpu)
+        torch.cuda.synchronize()
+        free0 = torch.cuda.mem_get_info(gpu)[0]
+        cx.reserve(n, stream=s1)
+        torch.cuda.synchronize()
+        used_dec = free0 - torch.cuda.mem_get_info(gpu)[0]
+        assert used_dec < 16 * n, used_dec  # the compaction state (a few B per packet), no records
+        m = 20_000
+        d = workload.describe("c3", 0, m, n=m)
+        w = workload.DeviceWorkload(d, gpu)
+        cx.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
+                        w.status, id_uniform=workload.ID_UNIFORM, pad16=True)
+        torch.cuda.synchronize()
+        free1 = torch.cuda.mem_get_info(gpu)[0]
+        cx.reserve(n, stream=s2)
+        torch.cuda.synchronize()
+        used_enc = free1 - torch.cuda.mem_get_info(gpu)[0]
+        assert used_enc >= 32 * n, used_enc
+        cx.release_stream(s1)
+        cx.release_stream(s2)
+    finally:
+        cx.close()
+
+
+def test_forget_captures(gpu):
+    """a captured call makes rsk_check_device_errors wait for the whole device; once the
+    graph is gone, rsk_forget_captures returns the context to waiting for its own streams."""
+    import torch
+
+    from rsock_amd.codec import Codec, DecodeBuffers
+
+    n = 50_000
+    d = workload.describe("c2", 0, n, n=n)
+    w = workload.DeviceWorkload(d, gpu)
+    cx = Codec(b"hello135", 0)
+    try:
+        s = torch.cuda.Stream(gpu)
+        o = DecodeBuffers.alloc(n, gpu)
+        cx.reserve(n, stream=s)
+        with torch.cuda.stream(s):
+            cx.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
+                            w.status, id_uniform=workload.ID_UNIFORM, stream=s)
+            cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, o, stream=s)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, o, stream=s)
+        o.n_valid.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert int(o.n_valid.item()) == n
+        assert cx.check_device_errors() == 0
+        del g
+        cx.forget_captures()
+        assert cx.check_device_errors() == 0
+        o.n_valid.zero_()
+        cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, o, stream=s)
+        torch.cuda.synchronize()
+        assert int(o.n_valid.item()) == n and cx.check_device_errors() == 0
+    finally:
+        cx.close()
