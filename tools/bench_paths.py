@@ -23,6 +23,7 @@ def main():
                     help="wire packet pitch alignment (bytes); 0 = the frame slot rule (128 with PAD128 for "
                          "mixed lengths, else 16)")
     ap.add_argument("--only", default="", help="time only these paths (comma list), e.g. demux,demux_64conn")
+    ap.add_argument("--demux-mode", type=int, default=0, help="rsk__set_demux_mode (A/B)")
     ap.add_argument("--encode-path", type=int, default=0,
                     help="rsk_set_encode_path for the encode paths: 0 chosen per call, 1 k_encode, 2 two-pass, 3 short")
     args = ap.parse_args()
@@ -91,8 +92,13 @@ def main():
     w.corrupt_frames()
     dmx = rc.DemuxBuffers.alloc(n, dev)
     dfields = rc._abi.DEMUX_ID | rc._abi.DEMUX_CONN_KEY | rc._abi.DEMUX_CMD_BARRIER
-    ops["demux"] = lambda: cx.demux_batch(w.dec.status, w.dec.cmd, dfields, dmx, id=w.dec.id, conv=w.dec.conv,
-                                          conn_key=w.dec.conn_key, stream=s)
+    # each demux shape on a context of its own: a context sizes its key table from its previous call
+    # (steady traffic); one context alternating between shapes is tests/test_gpu_demux.py's business
+    cx_dm = {k: rc.Codec(b"hello135", 0) for k in ("demux", "demux_64conn", "demux_server")}
+    for c_ in cx_dm.values():
+        c_.set_demux_mode(args.demux_mode)
+    ops["demux"] = lambda: cx_dm["demux"].demux_batch(w.dec.status, w.dec.cmd, dfields, dmx, id=w.dec.id,
+                                                      conv=w.dec.conv, conn_key=w.dec.conn_key, stream=s)
     # capture filter (server form) over the Ethernet wire packets: a 4M-packet capture batch
     fmatch = torch.empty(n, dtype=torch.uint8, device=dev)
     fidx = torch.empty(n, dtype=torch.int32, device=dev)
@@ -119,7 +125,19 @@ def main():
     k_key = torch.randint(0, 64, (n,), device=dev, generator=gk, dtype=torch.int64) * 0x10001 + 0x10000000
     k_id = torch.zeros(n * 8, dtype=torch.uint8, device=dev)
     dmx64 = rc.DemuxBuffers.alloc(n, dev)
-    ops["demux_64conn"] = lambda: cx.demux_batch(k_st, k_cmd, dfields, dmx64, id=k_id, conn_key=k_key, stream=s)
+    ops["demux_64conn"] = lambda: cx_dm["demux_64conn"].demux_batch(k_st, k_cmd, dfields, dmx64, id=k_id,
+                                                                    conn_key=k_key, stream=s)
+    # the server's leaf key (tests/demux_ref.py): 64 clients (IdBuf, dst) x 64 convs,
+    # 0.1 % control packets, every packet VALID -- 4096 SConns
+    A = rc._abi
+    sfields = A.DEMUX_ID | A.DEMUX_DST | A.DEMUX_CONV | A.DEMUX_CMD_BARRIER
+    grp = torch.randint(0, 64, (n,), device=dev, generator=gk, dtype=torch.int64)
+    s_id = torch.randint(0, 256, (64, 8), device=dev, generator=gk, dtype=torch.int64).to(torch.uint8)[grp].reshape(-1)
+    s_dst = (0x0a000000 + grp).to(torch.int32)
+    s_conv = torch.randint(1, 65, (n,), device=dev, generator=gk, dtype=torch.int64).to(torch.int32)
+    dmxs = rc.DemuxBuffers.alloc(n, dev)
+    ops["demux_server"] = lambda: cx_dm["demux_server"].demux_batch(k_st, k_cmd, sfields, dmxs, id=s_id,
+                                                                    conv=s_conv, dst=s_dst, stream=s)
     for k, f in ops.items():
         if k == "demux":
             cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, w.dec, stream=s)
@@ -141,7 +159,7 @@ def main():
     hlen = w.frame_len.to(torch.int32) + 21
     tcp3, sdec = rc.TcpInfoBuffers.alloc(n, dev), rc.DecodeBuffers.alloc(n, dev)
     ops["syncinput_decode"] = lambda: cx.syncinput_batch(hand, hoff, hlen, tcp3, sdec, stream=s)
-    nseg = [int(dmx.n_seg.item()), int(dmx64.n_seg.item())]
+    nseg = [int(dmx.n_seg.item()), int(dmx64.n_seg.item()), int(dmxs.n_seg.item())]
     if args.only:
         keep = args.only.split(",")
         ops = {k: f for k, f in ops.items() if k in keep}
@@ -167,6 +185,7 @@ def main():
         "parse_decode": 54 + 32 + 16 + 21 + 4 + 73 - 42,
         "demux": 1 + 1 + 8 + 8 + 4,  # status, cmd, id, conn_key in; perm out (+ per-segment words)
         "demux_64conn": 1 + 1 + 8 + 8 + 4,
+        "demux_server": 1 + 1 + 8 + 4 + 4 + 4,  # status, cmd, id, conv, dst in; perm out
         "capture_filter": 8 + 4 + 64 + 16 + 1 + 4,  # cap_off, cap_len, header windows, match, match_idx
         "filter_parse_decode": 8 + 4 + 64 + 16 + 1 + 54 + 32 + 16 + 21 + 4 + 73 - 42,
         "decode_hdr": 32 + 2 + 27 + 4,
