@@ -295,19 +295,6 @@ class Codec:
         fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
         _check(fn(self._ctx, packets), "rsk__set_two_pass_chunk")
 
-    def set_demux_test(self, slots: int = 0, fp_mask: int = 0xFFFFFFFF) -> None:
-        """Internal test knob (rsk__set_demux_test): force the demux's fingerprint table to `slots` slots
-        and keep only the fingerprint bits of `fp_mask`, so the overflow and mismatch redo paths run."""
-        fn = lib().rsk__set_demux_test
-        fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32]
-        _check(fn(self._ctx, slots, fp_mask), "rsk__set_demux_test")
-
-    def set_demux_mode(self, mode: int) -> None:
-        """Internal A/B knob (rsk__set_demux_mode): 0 the exact table insert, 1 fingerprints + verify."""
-        fn = lib().rsk__set_demux_mode
-        fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
-        _check(fn(self._ctx, mode), "rsk__set_demux_mode")
-
     def set_send_seq_groupby(self, v: int) -> None:
         """Internal knob for rsk_tcp_send_seq_batch: 0 the per-tile table path when n_conn < 2048
         (default), 1 the demux group-by path for every n_conn, 2 the table path with the one-kernel

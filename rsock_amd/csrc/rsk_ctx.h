@@ -44,10 +44,6 @@ struct rsk_ctx {
     // slower path, never different bytes)
     uint32_t *enc_stat_host = nullptr;
     uint32_t *enc_stat_dev = nullptr;
-    // the word after it (same allocation): the demux's last segment count | bit 31, stored by k_dm_final
-    // and read by the next rsk_demux_batch to size its key table (rsk_demux.hip); 0 = none yet
-    uint32_t *dm_stat_host = nullptr;
-    uint32_t *dm_stat_dev = nullptr;
     std::vector<uint8_t> key;
     rsk::KeySched ks;
     // Scratch per stream (compaction look-back state, send-seq tables, demux tables): calls on
@@ -55,9 +51,6 @@ struct rsk_ctx {
     std::mutex ws_mu;
     std::unordered_map<hipStream_t, std::array<rsk::WsBuf, rsk::WS_KINDS>> ws;
     bool sq_force_groupby = false;  // see rsk__set_send_seq_groupby
-    uint32_t dm_fp_mask = 0xffffffffu;  // demux key fingerprint bits kept (rsk__set_demux_test)
-    uint32_t dm_table = 0;              // demux fingerprint table slots forced (0: sized per call)
-    int dm_mode = 0;                    // demux insert: 0 exact, 1 fingerprints + verify (rsk__set_demux_mode)
     int sq_scan_variant = 0;
     // single-packet shim buffers
     ShimIO *shim_dev = nullptr;

@@ -144,7 +144,6 @@ struct DmIn {
     uint32_t *pep;   // with CMD_BARRIER: epoch of each VALID data packet, by packet index (else null: 0)
     uint32_t *cpos;  // with CMD_BARRIER: packet index of the c-th VALID control packet; cpos[n_ctrl] = n
     uint32_t n, fields;
-    uint32_t fp_mask;  // table fingerprint bits kept (all but in tests: rsk__set_demux_test)
 };
 
 // ---- decoupled look-back: one-pass exclusive scan of per-block counts across a grid -----------
@@ -265,39 +264,24 @@ __device__ __forceinline__ uint64_t key_hash(const Key &k) {
     return h;
 }
 
-// Global table probe: a slot is one u64, fingerprint (hash bits 32..63) << 32 | the packet index of
-// the key's first packet so far.  A slot with another fingerprint is skipped without touching that
-// packet's fields, and the index is lowered by compare-and-swap (the fingerprint half never changes
-// once claimed).  A relaxed load comes first: a hot key's slot is read, not written, by every later
-// tile (no RMW unless the index drops); a new key costs the load and one CAS (round 2, first half: a
-// load, a CAS and a separate atomicMin word).
+// Global table probe: a slot is one u64, fingerprint (hash bits 32..63) << 32 | the compacted index
+// of the key's first packet so far.  A slot with another fingerprint is skipped without touching that
+// packet's fields, a matching fingerprint is confirmed on the full key, and the index is lowered by
+// compare-and-swap (the fingerprint half never changes once claimed).  A relaxed load comes first:
+// a hot key's slot is read, not written, by every later tile (no RMW unless the index drops); a new
+// key costs the load and one CAS (round 2, first half: a load, a CAS and a separate atomicMin word).
 // [es, ee): the packets of the key's epoch (with CMD_BARRIER; cpos) -- an owner outside it has another
-// epoch, so its epoch is checked by its index instead of a gather (round 5).
-// EXACT: a matching fingerprint is confirmed on the full key at the owner's index (one dependent gather
-// into the inputs per probe -- the insert's bound through round 5: those gathers miss the XCD L2s).
-// Not EXACT (round 6): the fingerprint and the epoch range decide, so a probe is the slot chain alone,
-// and k_dm_verify checks every table-routed packet's key against its leader's afterwards; a mismatch
-// (two keys of one fingerprint in one chain) or a walk longer than kProbeMax slots (a table sized too
-// small from the previous call's key count) flags the call, and the EXACT insert redoes it in the full
-// table (k_dm_refill + k_dm_insert<true>, which return at once when nothing was flagged).
-constexpr uint32_t kProbeMax = 16;
-constexpr uint32_t kDmOverflow = 1u, kDmMismatch = 2u;
-template <bool EXACT>
+// epoch, so its epoch is checked by its index instead of a third gather (round 5)
 __device__ __forceinline__ uint32_t global_probe(const DmIn &a,
                                                  unsigned long long *slots, uint32_t mask, const Key &k,
-                                                 uint64_t hv, uint32_t j, uint32_t es, uint32_t ee, uint32_t *flag,
-                                                 uint32_t limit) {
+                                                 uint64_t hv, uint32_t j, uint32_t es, uint32_t ee) {
     // j is the packet index (monotone with the compacted index, so the minimum is the same packet):
     // a slot's owner is confirmed on the inputs at that index directly (round 5: one dependent
     // gather less than through the compacted index, C3 0.400 -> 0.372 ms with the 512-packet tiles)
-    const uint32_t fp = (uint32_t)(hv >> 32) & a.fp_mask;
+    const uint32_t fp = (uint32_t)(hv >> 32);
     const unsigned long long mine = ((unsigned long long)fp << 32) | j;
     uint32_t h = (uint32_t)hv & mask;
-    for (uint32_t walk = 0;; ++walk) {
-        if (walk == limit) {
-            __hip_atomic_fetch_or(flag, kDmOverflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return h;  // any slot: the call is redone
-        }
+    for (;;) {
         unsigned long long e = __hip_atomic_load(slots + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (e == ~0ull) {
             e = atomicCAS(slots + h, ~0ull, mine);
@@ -305,7 +289,7 @@ __device__ __forceinline__ uint32_t global_probe(const DmIn &a,
         }
         if ((uint32_t)(e >> 32) == fp) {
             const uint32_t o = (uint32_t)e;
-            if (o >= es && o < ee && (!EXACT || key_eq(load_key(a, o, k.ep), k))) {
+            if (o >= es && o < ee && key_eq(load_key(a, o, k.ep), k)) {
                 while ((uint32_t)e > j) {  // lower the key's first index to j
                     const unsigned long long f = atomicCAS(slots + h, e, mine);
                     if (f == e) break;
@@ -333,22 +317,16 @@ constexpr uint32_t kLeadTag = 0x80000000u;  // hslot: leader index (table slots 
 constexpr uint32_t kInsTile = kBlock * kInsItems;  // 512 packets (12 KB LDS)
 constexpr uint32_t kLtab = 2 * kInsTile;           // LDS table slots (power of 2)
 
-struct InsLds {
-    unsigned long long ltab[kLtab];
-    uint32_t lmin[kLtab];  // block-minimum index per key, then (phase 2b) the key's global slot
-    uint32_t elo, ehi;     // epochs of the tile's first and last data packets
-    uint32_t erng[4];      // their packet ranges [start, end) (CMD_BARRIER)
-};
-
-template <bool EXACT>
-__device__ __forceinline__ void insert_tile(const DmIn &a, uint32_t nv, uint32_t tile, const uint32_t *cidx,
-                                            unsigned long long *slots, uint32_t mask, uint32_t *hslot,
-                                            uint32_t *flag, uint32_t limit, InsLds &L) {
-    unsigned long long *ltab = L.ltab;
-    uint32_t *lmin = L.lmin;
-    uint32_t &elo = L.elo, &ehi = L.ehi;
-    uint32_t *erng = L.erng;
-    const uint32_t base = tile * kInsTile, t = threadIdx.x;
+__global__ __launch_bounds__(kBlock) void k_dm_insert(DmIn a, const uint32_t *nvp, const uint32_t *cidx,
+                                                      unsigned long long *slots,
+                                                      uint32_t mask, uint32_t *hslot) {
+    __shared__ unsigned long long ltab[kLtab];
+    __shared__ uint32_t lmin[kLtab];  // block-minimum index per key, then (phase 2b) the key's global slot
+    __shared__ uint32_t elo, ehi;     // epochs of the tile's first and last data packets
+    __shared__ uint32_t erng[4];      // their packet ranges [start, end) (CMD_BARRIER)
+    const uint32_t nv = *nvp;
+    const uint32_t base = blockIdx.x * kInsTile, t = threadIdx.x;
+    if (base >= nv) return;  // block-uniform
     for (uint32_t q = t; q < kLtab; q += kBlock) {
         ltab[q] = ~0ull;
         lmin[q] = kNone;
@@ -438,8 +416,7 @@ __device__ __forceinline__ void insert_tile(const DmIn &a, uint32_t nv, uint32_t
         const Key &k = kr[it];
         const bool lo = k.ep == elo;
         lmin[lpos[it]] = (lo || k.ep == ehi)
-                             ? global_probe<EXACT>(a, slots, mask, k, key_hash(k), j, erng[lo ? 0 : 2],
-                                                   erng[lo ? 1 : 3], flag, limit)
+                             ? global_probe(a, slots, mask, k, key_hash(k), j, erng[lo ? 0 : 2], erng[lo ? 1 : 3])
                              : kLeadTag | j;
     }
     __syncthreads();
@@ -448,68 +425,6 @@ __device__ __forceinline__ void insert_tile(const DmIn &a, uint32_t nv, uint32_t
         const uint32_t j = base + it * kBlock + t;
         if (j < nv) hslot[j] = lpos[it] == kNone ? kNone : lmin[lpos[it]];
     }
-    __syncthreads();  // the LDS table is reused by the block's next tile (EXACT redo)
-}
-
-// the insert: one tile per block, the table sized by the caller; limit: the longest walk before the
-// call is flagged for the redo in the full table (~0u when this IS the full table)
-template <bool EXACT>
-__global__ __launch_bounds__(kBlock) void k_dm_insert(DmIn a, const uint32_t *nvp, const uint32_t *cidx,
-                                                      unsigned long long *slots, uint32_t mask, uint32_t *hslot,
-                                                      uint32_t *flag, uint32_t limit) {
-    __shared__ InsLds L;
-    const uint32_t nv = *nvp;
-    if (blockIdx.x * kInsTile >= nv) return;  // block-uniform
-    insert_tile<EXACT>(a, nv, blockIdx.x, cidx, slots, mask, hslot, flag, limit, L);
-}
-
-// the exact redo, only when the fingerprint insert flagged the call: the full table (refilled by
-// k_dm_refill), tiles strided over a small grid so the usual case costs one flag read per block
-__global__ __launch_bounds__(kBlock) void k_dm_insert_exact(DmIn a, const uint32_t *nvp, const uint32_t *cidx,
-                                                            unsigned long long *slots, uint32_t mask,
-                                                            uint32_t *hslot, const uint32_t *flag) {
-    __shared__ InsLds L;
-    if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
-    const uint32_t nv = *nvp;
-    for (uint32_t tile = blockIdx.x; tile * kInsTile < nv; tile += gridDim.x)
-        insert_tile<true>(a, nv, tile, cidx, slots, mask, hslot, nullptr, ~0u, L);
-}
-
-__global__ __launch_bounds__(kBlock) void k_dm_refill(unsigned long long *slots, uint32_t nslots,
-                                                      const uint32_t *flag) {
-    if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
-    for (uint32_t q = blockIdx.x * kBlock + threadIdx.x; q < nslots; q += gridDim.x * kBlock) slots[q] = ~0ull;
-}
-
-// Every packet routed through the table: its key against its leader's (the index its slot names).
-// One pass of independent gathers (the leaders' lines are few and hot), instead of a dependent gather
-// inside every probe chain.
-__global__ __launch_bounds__(kBlock) void k_dm_verify(DmIn a, const uint32_t *nvp, const uint32_t *cidx,
-                                                      const unsigned long long *slots, const uint32_t *hslot,
-                                                      uint32_t *flag) {
-    constexpr uint32_t kV = 4;
-    const uint32_t nv = *nvp;
-    const uint32_t j0 = (blockIdx.x * kBlock * kV) + threadIdx.x;
-    uint32_t hs[kV], pk[kV], ld[kV];
-#pragma unroll
-    for (uint32_t q = 0; q < kV; ++q) {
-        const uint32_t j = j0 + q * kBlock;
-        hs[q] = j < nv ? hslot[j] : kNone;
-        pk[q] = j < nv ? cidx[j] : kNone;
-    }
-#pragma unroll
-    for (uint32_t q = 0; q < kV; ++q)
-        ld[q] = (hs[q] == kNone || (hs[q] & kLeadTag)) ? kNone : (uint32_t)slots[hs[q]];
-    bool bad = false;
-#pragma unroll
-    for (uint32_t q = 0; q < kV; ++q) {
-        if (ld[q] == kNone || ld[q] == pk[q]) continue;
-        const Key x = load_key(a, pk[q], a.pep ? a.pep[pk[q]] : 0u);
-        const Key y = load_key(a, ld[q], a.pep ? a.pep[ld[q]] : 0u);
-        bad |= !key_eq(x, y);
-    }
-    if (__ballot(bad) && (threadIdx.x & 63u) == 0u)
-        __hip_atomic_fetch_or(flag, kDmMismatch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---- stable LSD radix sort by segment id ------------------------------------------------------
@@ -903,7 +818,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_onesweep(uint32_t pass, const uin
 __global__ __launch_bounds__(kBlock) void k_dm_final(const uint32_t *nvp, const uint32_t *nsegp, const uint32_t *kA,
                                                      const uint32_t *vA, const uint32_t *kB, const uint32_t *vB,
                                                      const uint32_t *seg_first, uint32_t *perm, uint32_t *seg_off,
-                                                     uint32_t *n_seg, uint32_t *n_valid, uint32_t *stat) {
+                                                     uint32_t *n_seg, uint32_t *n_valid) {
     const uint32_t nv = *nvp, ns = *nsegp, nf = nv - ns;
     const uint32_t passes = n_passes(ns);  // effective passes; pass p writes B when p is even
     const bool inB = nf > kSmallF && ((passes - 1u) & 1u) == 0u;  // small: sorted in place in A
@@ -914,7 +829,6 @@ __global__ __launch_bounds__(kBlock) void k_dm_final(const uint32_t *nvp, const 
         *n_seg = ns;
         *n_valid = nv;
         seg_off[ns] = nv;
-        if (stat) *stat = 0x80000000u | ns;  // the next call sizes its table by it (host-mapped)
     }
     if (k < ns) {
         uint32_t lo = 0, hi = nf;  // followers with segment id < k
@@ -934,10 +848,9 @@ struct DmWs {
     uint32_t *cidx, *hslot, *rank_at, *pep, *cpos;
     uint32_t *kA, *vA, *kB, *vB;
     uint32_t *ghist;
-    unsigned long long *st_v, *st_c, *st_l, *st_r;  // look-back states | flag | slots: one 0xff fill per
-    uint32_t *flag;                                 // call over the states and the slots this call
-    unsigned long long *slots;                      // uses (the flag is then zeroed)
-    size_t fill_bytes;  // bytes from st_v to the first slot
+    unsigned long long *slots;  // slots | look-back states: one 0xff fill per call
+    unsigned long long *st_v, *st_c, *st_l, *st_r;
+    size_t fill_bytes;
     uint32_t *nv, *nseg;
     uint32_t nb, nt, tsize;
 };
@@ -970,13 +883,12 @@ size_t dm_layout(uint32_t n, uint8_t *base, DmWs *w) {
     d.nv = (uint32_t *)take(8);
     d.nseg = (uint32_t *)take(8);
     const size_t fill0 = off;
+    d.slots = (unsigned long long *)take(8ull * T);
     d.st_v = (unsigned long long *)take(8ull * nt);
     d.st_c = (unsigned long long *)take(8ull * nt);
     d.st_l = (unsigned long long *)take(8ull * nt);
     d.st_r = (unsigned long long *)take(8ull * 4 * 256 * nt);
-    d.flag = (uint32_t *)take(8);
     d.fill_bytes = off - fill0;
-    d.slots = (unsigned long long *)take(8ull * T);
     d.nb = nb;
     d.nt = nt;
     d.tsize = T;
@@ -1021,45 +933,16 @@ extern "C" int rsk_demux_batch(rsk_ctx *c, uint32_t n, const rsk_demux_in *in, u
     a.dst = in->dst;
     a.n = n;
     a.fields = fields;
-    a.fp_mask = c->dm_fp_mask;
     a.pep = (fields & RSK_DEMUX_CMD_BARRIER) ? w.pep : nullptr;
     a.cpos = (fields & RSK_DEMUX_CMD_BARRIER) ? w.cpos : nullptr;
-    // The key table of this call: 4x the previous call's segment count (a host-mapped word k_dm_final
-    // stores; read without synchronisation, as the encode statistic), at least 2^15 slots, at most the
-    // full table (2n: every packet its own key).  A first call, or one whose keys outgrow the estimate,
-    // runs in the full table -- the latter through the flagged redo (round 6: a 4M-packet batch of 28 K
-    // keys probes a 1-MB table that stays in the XCD L2s instead of a 64-MB one).
-    uint32_t ts = w.tsize;
-    const uint32_t last = c->dm_stat_host ? __atomic_load_n(c->dm_stat_host, __ATOMIC_RELAXED) : 0u;
-    if (last & 0x80000000u) {
-        const uint64_t want = 4ull * (last & 0x7fffffffu);
-        uint64_t t = 1ull << 15;
-        while (t < want) t <<= 1;
-        if (t < ts) ts = (uint32_t)t;
-    }
-    if (c->dm_table && c->dm_table < ts) ts = c->dm_table;
-    // one fill: every look-back state word and this call's slots start as all-ones, the flag as zero
-    hipError_t e = hipMemsetAsync(w.st_v, 0xff, w.fill_bytes + 8ull * ts, s);
-    if (e == hipSuccess) e = hipMemsetAsync(w.flag, 0, 4, s);
+    // one fill: the key table and every look-back state word start as all-ones
+    hipError_t e = hipMemsetAsync(w.slots, 0xff, w.fill_bytes, s);
     if (e != hipSuccess) { rsk::set_error("hipMemsetAsync(table)", e); return RSK_EDEVICE; }
     const uint32_t nb = w.nb;
     hipLaunchKernelGGL(k_dm_flags_prep, dim3(w.nt), dim3(kBlock), 0, s, a, w.st_v, w.st_c, w.cidx, w.nv,
                        c->err_dev);
-    const uint32_t ntiles = (n + kInsTile - 1) / kInsTile;
-    const uint32_t limit = ts < w.tsize ? kProbeMax : ~0u;
-    if (c->dm_mode == 1) {  // A/B: fingerprints only, then k_dm_verify
-        hipLaunchKernelGGL(k_dm_insert<false>, dim3(ntiles), dim3(kBlock), 0, s, a, w.nv, w.cidx, w.slots, ts - 1u,
-                           w.hslot, w.flag, limit);
-        hipLaunchKernelGGL(k_dm_verify, dim3((n + 4 * kBlock - 1) / (4 * kBlock)), dim3(kBlock), 0, s, a, w.nv,
-                           w.cidx, w.slots, w.hslot, w.flag);
-    } else {
-        hipLaunchKernelGGL(k_dm_insert<true>, dim3(ntiles), dim3(kBlock), 0, s, a, w.nv, w.cidx, w.slots, ts - 1u,
-                           w.hslot, w.flag, limit);
-    }
-    const uint32_t rg = ntiles < 1024u ? ntiles : 1024u;  // the redo's grid (returns at once unless flagged)
-    hipLaunchKernelGGL(k_dm_refill, dim3(rg), dim3(kBlock), 0, s, w.slots, w.tsize, w.flag);
-    hipLaunchKernelGGL(k_dm_insert_exact, dim3(rg), dim3(kBlock), 0, s, a, w.nv, w.cidx, w.slots, w.tsize - 1u,
-                       w.hslot, w.flag);
+    hipLaunchKernelGGL(k_dm_insert, dim3((n + kInsTile - 1) / kInsTile), dim3(kBlock), 0, s, a, w.nv, w.cidx,
+                       w.slots, w.tsize - 1u, w.hslot);
     hipLaunchKernelGGL(k_dm_leader_rank, dim3(w.nt), dim3(kBlock), 0, s, w.nv, w.hslot, w.slots, w.cidx, w.st_l,
                        w.kA, w.vA, w.rank_at, out->seg_first, w.nseg, w.ghist, c->err_dev);
     hipLaunchKernelGGL(k_dm_segof_hist, dim3(w.nt), dim3(kBlock), 0, s, w.nv, w.nseg, w.rank_at, w.kA, w.vA,
@@ -1077,7 +960,7 @@ extern "C" int rsk_demux_batch(rsk_ctx *c, uint32_t n, const rsk_demux_in *in, u
         if ((r = rsk::launch_check("k_dm_onesweep"))) return r;
     }
     hipLaunchKernelGGL(k_dm_final, dim3(nb), dim3(kBlock), 0, s, w.nv, w.nseg, w.kA, w.vA, w.kB, w.vB,
-                       out->seg_first, out->perm, out->seg_off, out->n_seg, out->n_valid, c->dm_stat_dev);
+                       out->seg_first, out->perm, out->seg_off, out->n_seg, out->n_valid);
     return rsk::launch_check("k_dm_final");
 }
 
@@ -1524,22 +1407,6 @@ extern "C" int rsk_tcp_send_seq_batch(rsk_ctx *c, uint32_t n, const uint32_t *co
                        w.base);
     hipLaunchKernelGGL(k_sq_seq, dim3(nb), dim3(kBlock), 0, s, w.perm, w.nvalid, conn, w.base, w.pre, seq);
     return rsk::launch_check("k_sq_seq");
-}
-
-// internal test knob (not in the public header): the demux's fingerprint table forced to `slots` (a power
-// of two >= 64; 0 = sized per call) and its fingerprints cut to the bits of fp_mask (0xffffffff = all), so
-// tests reach the overflow and mismatch redo paths (k_dm_insert_exact) on purpose
-extern "C" int rsk__set_demux_test(rsk_ctx *c, uint32_t slots, uint32_t fp_mask) {
-    if (!c || (slots && (slots < 64u || (slots & (slots - 1u))))) return RSK_EINVAL;
-    c->dm_table = slots;
-    c->dm_fp_mask = fp_mask;
-    return RSK_OK;
-}
-// internal A/B: 0 the exact insert (default), 1 fingerprints then k_dm_verify
-extern "C" int rsk__set_demux_mode(rsk_ctx *c, int mode) {
-    if (!c || mode < 0 || mode > 1) return RSK_EINVAL;
-    c->dm_mode = mode;
-    return RSK_OK;
 }
 
 // internal A/B + test knob (not in the public header): 1 sends every n_conn through the group-by path,

@@ -2847,18 +2847,13 @@ rsk_ctx *rsk_create(const uint8_t *key, uint32_t key_len, int device) {
     if (e == hipSuccess) e = hipMemset(c->err_dev, 0, sizeof(uint32_t));
     // the encode path statistic's host-mapped word (enc_path); without it every call takes the per-set
     // kernel unless a path is forced -- not an error
-    // (two words: the encode statistic, then the demux's, rsk_ctx.h)
-    if (e == hipSuccess && hipHostMalloc(reinterpret_cast<void **>(&c->enc_stat_host), 2 * sizeof(uint32_t),
+    if (e == hipSuccess && hipHostMalloc(reinterpret_cast<void **>(&c->enc_stat_host), sizeof(uint32_t),
                                          hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
-        c->enc_stat_host[0] = 0u;
-        c->enc_stat_host[1] = 0u;
+        *c->enc_stat_host = 0u;
         if (hipHostGetDevicePointer(reinterpret_cast<void **>(&c->enc_stat_dev), c->enc_stat_host, 0) != hipSuccess) {
             (void)hipHostFree(c->enc_stat_host);
             c->enc_stat_host = nullptr;
             c->enc_stat_dev = nullptr;
-        } else {
-            c->dm_stat_host = c->enc_stat_host + 1;
-            c->dm_stat_dev = c->enc_stat_dev + 1;
         }
     }
     (void)hipGetLastError();  // a failed optional allocation above must not surface as a later launch error

@@ -208,52 +208,3 @@ def test_demux_epoch_edges_same_key(codec, gpu, oracle, fields):
     assert got[1] == exp[1]
     assert got[0] == exp[0]
 
-
-@pytest.mark.parametrize("mode", [0, 1])
-@pytest.mark.parametrize("slots,fp_mask", [(64, 0xFFFFFFFF), (64, 0), (1 << 12, 0x3), (1 << 16, 0), (0, 0x1)])
-@pytest.mark.parametrize("shape", [(4097, 40, 0.01, 0.7), (70000, 300, 0.002, 0.8), (3000, 3000, 0.0, 1.0),
-                                   (20000, 5, 0.3, 1.0)])
-def test_demux_redo_paths(gpu, oracle, mode, slots, fp_mask, shape):
-    """Round 6: the fingerprint insert trusts fingerprints and a table sized from the previous call's
-    key count; k_dm_verify flags a fingerprint clash and a walk past kProbeMax flags a full table, and
-    the exact insert redoes the call in the full table.  Forced here (rsk__set_demux_test): tables of 64
-    slots against thousands of keys (overflow), fingerprints cut to 0-2 bits (every chain clashes); in
-    the exact insert (mode 0) the walk limit flags the small tables, in mode 1 (fingerprints + verify,
-    the A/B form) both flags."""
-    from rsock_amd.codec import Codec
-
-    n, nkeys, p_ctrl, p_valid = shape
-    cx = Codec(b"hello135", 0)
-    try:
-        cx.set_demux_mode(mode)
-        cx.set_demux_test(slots, fp_mask)
-        for fields in (ALL | A.DEMUX_CMD_BARRIER, A.DEMUX_CONN_KEY, A.DEMUX_ID | A.DEMUX_CONV):
-            rng = np.random.default_rng(n + nkeys + fields + slots)
-            case = make_case(rng, n, nkeys, p_ctrl, p_valid)
-            got = run_gpu(cx, gpu, *case[:2], fields, *case[2:])
-            exp = oracle.demux_batch(case[0], case[1], fields, *case[2:])
-            assert got[1] == exp[1]
-            assert got[0] == exp[0]
-    finally:
-        cx.close()
-
-
-def test_demux_table_follows_key_count(gpu, oracle):
-    """The fingerprint table is sized from the previous call's segment count: a batch of few keys, then
-    one of many (the small table overflows: redo), then few again, then every packet its own key, on
-    one context -- every call equal to the oracle."""
-    from rsock_amd.codec import Codec
-
-    cx = Codec(b"hello135", 0)
-    try:
-        for i, (n, nkeys) in enumerate([(50000, 10), (200000, 150000), (50000, 10), (100000, 100000),
-                                        (300000, 64), (300000, 299000)]):
-            rng = np.random.default_rng(i)
-            case = make_case(rng, n, nkeys, 0.0, 1.0)
-            fields = A.DEMUX_CONN_KEY
-            got = run_gpu(cx, gpu, *case[:2], fields, *case[2:])
-            exp = oracle.demux_batch(case[0], case[1], fields, *case[2:])
-            assert got[1] == exp[1]
-            assert got[0] == exp[0], (i, n, nkeys)
-    finally:
-        cx.close()

@@ -23,7 +23,6 @@ def main():
                     help="wire packet pitch alignment (bytes); 0 = the frame slot rule (128 with PAD128 for "
                          "mixed lengths, else 16)")
     ap.add_argument("--only", default="", help="time only these paths (comma list), e.g. demux,demux_64conn")
-    ap.add_argument("--demux-mode", type=int, default=0, help="rsk__set_demux_mode (A/B)")
     ap.add_argument("--encode-path", type=int, default=0,
                     help="rsk_set_encode_path for the encode paths: 0 chosen per call, 1 k_encode, 2 two-pass, 3 short")
     args = ap.parse_args()
@@ -95,8 +94,6 @@ def main():
     # each demux shape on a context of its own: a context sizes its key table from its previous call
     # (steady traffic); one context alternating between shapes is tests/test_gpu_demux.py's business
     cx_dm = {k: rc.Codec(b"hello135", 0) for k in ("demux", "demux_64conn", "demux_server")}
-    for c_ in cx_dm.values():
-        c_.set_demux_mode(args.demux_mode)
     ops["demux"] = lambda: cx_dm["demux"].demux_batch(w.dec.status, w.dec.cmd, dfields, dmx, id=w.dec.id,
                                                       conv=w.dec.conv, conn_key=w.dec.conn_key, stream=s)
     # capture filter (server form) over the Ethernet wire packets: a 4M-packet capture batch
