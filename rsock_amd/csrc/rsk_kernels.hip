@@ -143,7 +143,8 @@ struct Lane1 {
     bool slow;
 };
 
-template <bool TAG = true, bool LANE = false>
+// SADD: added to a framed packet's status (the two-pass wire build: the wire length, HL + 31 + P)
+template <bool TAG = true, bool LANE = false, int SADD = 0>
 __device__ __forceinline__ Lane1 encode_phase1(const EncArgs &a, const KeySched &ks, uint64_t i) {
     Lane1 L;
     L.st = 0;
@@ -170,7 +171,7 @@ __device__ __forceinline__ Lane1 encode_phase1(const EncArgs &a, const KeySched 
             head_words(a.cmd[i], id0, id1, a.conv[i], a.conn_key[i], b0, L.H);
             L.slow = (reinterpret_cast<uintptr_t>(a.frame + L.fo) & 15u) != 0;
         }
-        a.status[i] = L.st;
+        a.status[i] = L.st > 0 ? L.st + SADD : L.st;
     }
     return L;
 }
@@ -799,12 +800,13 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
 // compressions 64 to a wave instead.  rsk_encode_batch takes this form for batches of long frames
 // (enc_path); for short frames one packet per wave idles most lanes and the per-set kernel stays.
 // base: the first packet of this launch (a chunked call runs heads / copy per chunk of packets)
+template <int SADD = 0>
 __global__ __launch_bounds__(kBlock) void k_encode_heads(EncArgs a, KeySched ks, uint4 *heads, uint32_t *stat,
                                                          uint64_t base) {
     stage_tags(ks);
     enc_sample(a.pay_len, a.n, stat);
     const uint64_t i = base + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    const Lane1 L = encode_phase1<true, true>(a, ks, i < a.n ? i : a.n);
+    const Lane1 L = encode_phase1<true, true, SADD>(a, ks, i < a.n ? i : a.n);
     if (i < a.n && L.st > 0) {
         heads[2 * i] = make_uint4(L.H[0], L.H[1], L.H[2], L.H[3]);
         heads[2 * i + 1] = make_uint4(L.H[4], L.H[5], L.H[6], L.H[7]);
@@ -1898,6 +1900,204 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
     EncArgs a, WireArgs wa, KeySched ks) {
     stage_tags(ks);
     encode_wire_set<E, MODE, PU, U, GI>(a, wa, ks);
+}
+
+// ---- the two-pass wire build (round 6): a header pass, one lane per packet (MD5
+// tags 64 to a wave), writes each packet's whole header image -- link, IPv4 with its checksum, TCP,
+// the 31 frame-head bytes: wire bytes [0, HB), HB = 71 RAW4 / 85 Ethernet -- as Q + 1 = 5 / 6 16-B
+// chunks of a record, with the TCP checksum's share of the pseudo-header and the image (from the TCP
+// header on) in the last chunk's bytes 12..15, which the payload overwrites; the status is the wire
+// length.  Then copy waves of K packets as k_encode_copy's: lane k takes IMAGE chunk k -- wire bytes
+// [16k, 16k + 16): the record's chunk (one 16-B load by lanes 0..Q) for k < Q, record and payload for
+// k = Q, payload beyond (one aligned load per chunk and the DPP funnel) -- sums the payload halfwords
+// on the way into the TCP checksum (a wave reduction), which the lane of the checksum chunk ORs in
+// before the stores.  A packet whose first byte is not 16-B aligned (r = dst mod 16) stores
+// destination chunk j = image chunks j - 1 and j funnelled by 16 - r (wave_shr:1), so the checksum is
+// summed in image coordinates at any alignment.
+template <int E>
+struct WireRec {
+    static constexpr int HB = WireGeom<E>::HB, Q = HB / 16, R = HB % 16;  // RAW4 71 = 4 x 16 + 7; Eth 85 = 5 x 16 + 5
+    static constexpr int NC = Q + 1;                                       // record chunks (80 / 96 B)
+    static_assert(R != 0 && R <= 12 && WireGeom<E>::CK / 16 < Q, "record layout");
+};
+
+template <int E>
+__global__ __launch_bounds__(kBlock) void k_wire_heads(EncArgs a, WireArgs wa, KeySched ks, uint4 *rec,
+                                                       uint32_t *stat) {
+    using G = WireGeom<E>;
+    using W = WireRec<E>;
+    constexpr int NIW = 4 * W::NC;
+    stage_tags(ks);
+    enc_sample(a.pay_len, a.n, stat);
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const Lane1 L = encode_phase1<true, true, G::HL>(a, ks, i < a.n ? i : a.n);
+    if (i >= a.n || L.st <= 0) return;
+    const uint32_t flen = (uint32_t)L.st;
+    uint32_t PW[NIW];
+#pragma unroll
+    for (int q = 0; q < NIW; ++q) PW[q] = 0u;
+    const uint32_t src = wa.src[i], dst = wa.dst[i], sp = wa.sp[i], dp = wa.dp[i];
+    const uint32_t seq = wa.seq[i], ack = wa.ack[i], fl = wa.flag[i], id = wa.ip_id[i];
+    if constexpr (E > 0) {
+#pragma unroll
+        for (int b = 0; b < E; b += 4) put_bytes(PW, b, wa.eth[b >> 2], E - b < 4 ? E - b : 4);
+    }
+    // IPv4 header (libnet_build_ipv4): 45 00 | len | id | 40 00 | 40 06 | csum | src | dst
+    const uint32_t tot = 40u + flen;
+    const uint32_t ip0 = 0x45u | (rsk::bswap16(tot) << 16), ip1 = rsk::bswap16(id) | (0x0040u << 16);
+    put_bytes(PW, E + 0, ip0, 4);
+    put_bytes(PW, E + 4, ip1, 4);
+    put_bytes(PW, E + 8, 64u | (6u << 8), 2);
+    put_bytes(PW, E + 12, src, 4);
+    put_bytes(PW, E + 16, dst, 4);
+    const uint32_t ips = hsum(ip0) + hsum(ip1) + hsum(64u | (6u << 8)) + hsum(src) + hsum(dst);
+    put_bytes(PW, G::IPC, ~fold16(ips) & 0xffffu, 2);
+    // TCP header (libnet_build_tcp): sp dp seq ack | 50 flags | ffff | csum (0 here) | 0000
+    put_bytes(PW, E + 20, rsk::bswap16(sp) | (rsk::bswap16(dp) << 16), 4);
+    put_bytes(PW, E + 24, rsk::bswap32(seq), 4);
+    put_bytes(PW, E + 28, rsk::bswap32(ack), 4);
+    put_bytes(PW, E + 32, 0x50u | (fl << 8) | (0xffffu << 16), 4);
+    // frame bytes [0, 31) = tag + EncHead (payload[0], H[7]'s top byte, comes with the payload)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) put_bytes(PW, G::HL + 4 * q, L.H[q], q == 7 ? 3 : 4);
+    // the checksum's share: pseudo-header (src, dst, 0, 6, tcp_len) + the image from the TCP header on
+    uint32_t s = hsum(src) + hsum(dst) + (6u << 8) + rsk::bswap16(20u + flen);
+#pragma unroll
+    for (int q = (E + 20) / 4; q < NIW; ++q) s += ((E + 20) % 4 && q == (E + 20) / 4) ? (PW[q] >> 16) : hsum(PW[q]);
+    PW[NIW - 1] = s;  // bytes 12..15 of chunk Q: payload positions, overwritten by the copy
+    uint4 *o = rec + (uint64_t)W::NC * i;
+#pragma unroll
+    for (int c = 0; c < W::NC; ++c) o[c] = make_uint4(PW[4 * c], PW[4 * c + 1], PW[4 * c + 2], PW[4 * c + 3]);
+}
+
+template <int E, int NT, int K>
+__global__ __launch_bounds__(kBlock) void k_wire_copy(EncArgs a, const uint4 *rec, uint64_t base) {
+    using G = WireGeom<E>;
+    using W = WireRec<E>;
+    constexpr int HB = W::HB, Q = W::Q, R = W::R;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint64_t i0 = base + ((uint64_t)blockIdx.x * kWavesPerBlock + w) * K;
+    if (i0 >= a.n) return;
+    // descriptors, lanes 0..K-1 (one round trip)
+    uint32_t dP = 0;
+    uint64_t dpo = 0, dfo = 0;
+    {
+        const uint64_t il = i0 + lane;
+        if (lane < (uint32_t)K && il < a.n) {
+            dP = a.pay_len[il];
+            dpo = a.pay_off[il];
+            dfo = a.frame_off[il];
+        }
+    }
+    uint4 A[K][2], H[K];
+    uint32_t Pp[K], shp[K];
+#pragma unroll
+    for (int p = 0; p < K; ++p) {
+        const uint32_t P = rdl(dP, (uint32_t)p);
+        const bool on = i0 + p < a.n && P != 0u && P <= (uint32_t)RSK_MAX_PAYLOAD;  // uniform
+        Pp[p] = on ? P : 0u;
+        // the record chunk of lane k <= Q
+        H[p] = on && lane <= (uint32_t)Q ? rec[(uint64_t)W::NC * (i0 + p) + lane] : make_uint4(0u, 0u, 0u, 0u);
+        const uint8_t *src = a.payload + rdl64(dpo, (uint32_t)p);
+        shp[p] = (uint32_t)((reinterpret_cast<uintptr_t>(src) - (uint32_t)R) & 15u);
+        const uint8_t *srcp = src - R - shp[p];  // aligned: image chunk k <- source chunks k - Q, k - Q + 1
+        const int32_t first_rel = R + (int32_t)shp[p], last_rel = first_rel + (int32_t)P - 1;
+        const int32_t m_lo = first_rel >> 4, m_hi = last_rel >> 4;
+        const uint32_t nch = (HB + P + 15u) >> 4;  // image chunks
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            A[p][q] = make_uint4(0u, 0u, 0u, 0u);
+            if (!on || (q == 1 && nch < 64u)) continue;  // uniform
+            const int32_t m = (int32_t)(lane + 64u * q) - Q;
+            const int32_t mc = m < m_lo ? m_lo : m > m_hi ? m_hi : m;  // dead lanes re-read a live chunk
+            A[p][q] = ld16<NT>(srcp + 16 * mc);
+        }
+    }
+    // Three phases over the K packets, so the packets' dependency chains overlap (round 6: one packet at a
+    // time, the wave waited on each packet's funnel -> sum -> reduction chain in turn): (1) each lane's
+    // image chunks and payload halfword sums, (2) the K checksums (wave reductions), (3) the stores.
+    // Header mask of lane k <= Q (the record's bytes: all of chunk k < Q, the first R of chunk Q).
+    const uint4 mh = lane <= (uint32_t)Q ? rsk::keep_bytes16(make_uint4(~0u, ~0u, ~0u, ~0u), lane < (uint32_t)Q ? 16 : R)
+                                         : make_uint4(0u, 0u, 0u, 0u);
+    uint4 VI[K][2];
+    uint32_t part[K];
+#pragma unroll
+    for (int p = 0; p < K; ++p) {
+        VI[p][0] = VI[p][1] = make_uint4(0u, 0u, 0u, 0u);
+        part[p] = 0u;
+        const uint32_t P = Pp[p];
+        if (!P) continue;  // uniform
+        const uint32_t wlen = HB + P, nch = (wlen + 15u) >> 4;
+        uint4 B[2];
+        B[0] = make_uint4(wave_shl1(A[p][0].x), wave_shl1(A[p][0].y), wave_shl1(A[p][0].z), wave_shl1(A[p][0].w));
+        B[1] = make_uint4(0u, 0u, 0u, 0u);
+        if (nch >= 64u) {  // uniform
+            const uint4 l0 = rdl4(A[p][1], 0);
+            if (lane == 63u) B[0] = l0;
+            B[1] = make_uint4(wave_shl1(A[p][1].x), wave_shl1(A[p][1].y), wave_shl1(A[p][1].z), wave_shl1(A[p][1].w));
+        }
+        // lane k's image chunk: the record's bytes under mh, the payload's elsewhere (zero past the
+        // packet); summed: the payload bytes only (the record's are in its checksum share)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            if (q == 1 && nch <= 64u) continue;  // uniform
+            const uint32_t k = lane + 64u * q;
+            uint4 v = rsk::funnel16(A[p][q], B[q], shp[p]);
+            const int lim = (int)wlen - 16 * (int)k;
+            v = lim >= 16 ? v : lim > 0 ? rsk::keep_bytes16(v, lim) : make_uint4(0u, 0u, 0u, 0u);
+            if (q == 0) {
+                v = make_uint4(v.x & ~mh.x, v.y & ~mh.y, v.z & ~mh.z, v.w & ~mh.w);
+                part[p] = hsum4(v, part[p]);
+                const uint4 h = H[p];
+                v = make_uint4(v.x | (h.x & mh.x), v.y | (h.y & mh.y), v.z | (h.z & mh.z), v.w | (h.w & mh.w));
+            } else {
+                part[p] = hsum4(v, part[p]);
+            }
+            VI[p][q] = v;
+        }
+    }
+    uint32_t ck[K];
+#pragma unroll
+    for (int p = 0; p < K; ++p) ck[p] = ~fold16(wave_sum(part[p]) + rdl(H[p].w, (uint32_t)Q)) & 0xffffu;
+#pragma unroll
+    for (int p = 0; p < K; ++p) {
+        const uint32_t P = Pp[p];
+        if (!P) continue;  // uniform
+        const uint32_t wlen = HB + P;
+        uint8_t *dst = a.frame + rdl64(dfo, (uint32_t)p);
+        if (lane == (uint32_t)(G::CK / 16)) {
+            constexpr uint32_t kw = (G::CK & 15) >> 2, kb = 8 * (G::CK & 3);
+            if (kw == 0) VI[p][0].x |= ck[p] << kb; else if (kw == 1) VI[p][0].y |= ck[p] << kb;
+            else if (kw == 2) VI[p][0].z |= ck[p] << kb; else VI[p][0].w |= ck[p] << kb;
+        }
+        const uint32_t r = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15u);  // uniform
+        uint8_t *d0 = dst - r;
+        const uint32_t nst = (r + padded_len(dst, wlen, a.pad) + 15u) >> 4;
+        const bool pad = a.pad != 0u;
+        if (r == 0u) {
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const uint32_t k = lane + 64u * q;
+                if (q == 1 && nst <= 64u) continue;  // uniform
+                if (k < nst) store_last16<NT>(d0 + 16u * k, VI[p][q], (int)wlen - 16 * (int)k, pad);
+            }
+        } else {
+            const uint4 l63 = rdl4(VI[p][0], 63);
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                if (q == 1 && nst <= 64u) continue;  // uniform
+                uint4 prev = make_uint4(wave_shr1(VI[p][q].x), wave_shr1(VI[p][q].y), wave_shr1(VI[p][q].z),
+                                        wave_shr1(VI[p][q].w));
+                if (lane == 0u) prev = q == 0 ? make_uint4(0u, 0u, 0u, 0u) : l63;
+                const uint4 d = rsk::funnel16(prev, VI[p][q], 16u - r);
+                const uint32_t j = lane + 64u * q;
+                if (j >= nst) continue;
+                if (j == 0u) rsk::store_range16(d0, d, r, 16u);
+                else store_last16<NT>(d0 + 16u * j, d, (int)(r + wlen) - 16 * (int)j, pad);
+            }
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -3084,7 +3284,7 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
             for (uint64_t c0 = 0; c0 < n; c0 += chunk) {
                 EncArgs ac = a;
                 ac.n = (uint32_t)std::min<uint64_t>(n, c0 + chunk);
-                hipLaunchKernelGGL(k_encode_heads, dim3(grid_for(ac.n - c0)), bd, 0, st, ac, c->ks,
+                hipLaunchKernelGGL(k_encode_heads<0>, dim3(grid_for(ac.n - c0)), bd, 0, st, ac, c->ks,
                                    static_cast<uint4 *>(hp), c0 == 0 ? c->enc_stat_dev : nullptr, c0);
                 for (uint64_t b0 = c0; b0 < ac.n; b0 += kCopyMaxPackets) {  // one launch up to 2^25 packets
                     const uint64_t m = ac.n - b0 < kCopyMaxPackets ? ac.n - b0 : kCopyMaxPackets;
@@ -3151,14 +3351,50 @@ int rsk_encode_wire_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const
     std::memcpy(w.eth, eth, 16);
     const unsigned grid = enc_grid(n, 8, 1024);
     const hipStream_t st = (hipStream_t)stream;
+    const bool eth14 = wire->with_eth != 0;
+    // the encode's path choice (rsk_set_encode_path, or AUTO by the sampled mean payload): the two-pass
+    // form -- k_wire_heads (header images, 80 / 96-B records in the stream's scratch) + k_wire_copy with
+    // 1, 2 or 4 packets per copy wave (round 6) -- for batches of long frames, else the per-set kernels
+    const int path = enc_path(c, n, in->pay_len, st);
+    if (path < 0) return path;
+    if (path == RSK_ENC_PATH_TWO_PASS) {
+        void *hp = nullptr;
+        const uint64_t recb = 16ull * (eth14 ? WireRec<14>::NC : WireRec<0>::NC);  // 96 / 80 B per packet
+        if (rsk::stream_ws_if(c, st, rsk::WS_ENC, recb * n, &hp) == RSK_OK) {
+            const int ck = copy_k(c);
+            const dim3 bd(kBlock);
+            uint4 *rec = static_cast<uint4 *>(hp);
+            if (eth14) hipLaunchKernelGGL(k_wire_heads<14>, dim3(grid_for(n)), bd, 0, st, a, w, c->ks, rec, c->enc_stat_dev);
+            else hipLaunchKernelGGL(k_wire_heads<0>, dim3(grid_for(n)), bd, 0, st, a, w, c->ks, rec, c->enc_stat_dev);
+            for (uint64_t b0 = 0; b0 < n; b0 += kCopyMaxPackets) {  // one launch up to 2^25 packets
+                const uint64_t m = n - b0 < kCopyMaxPackets ? n - b0 : kCopyMaxPackets;
+                const dim3 cg((unsigned)((m + 4ull * ck - 1ull) / (4ull * ck)));
+#define RSK_WCOPY(E, K) hipLaunchKernelGGL((k_wire_copy<E, 3, K>), cg, bd, 0, st, a, rec, b0)
+                if (eth14) {
+                    if (ck == 2) RSK_WCOPY(14, 2); else if (ck == 4) RSK_WCOPY(14, 4); else RSK_WCOPY(14, 1);
+                } else {
+                    if (ck == 2) RSK_WCOPY(0, 2); else if (ck == 4) RSK_WCOPY(0, 4); else RSK_WCOPY(0, 1);
+                }
+#undef RSK_WCOPY
+            }
+            c->enc_last_path.store(RSK_ENC_PATH_TWO_PASS, std::memory_order_relaxed);
+            c->enc_last_k.store(ck, std::memory_order_relaxed);
+            return launch_check("k_wire_heads / k_wire_copy");
+        }
+        g_last_error[0] = 0;  // no records (a capture that would grow them, or no memory): one pass
+    }
 #define RSK_WIRE(E, M, PU, U) hipLaunchKernelGGL((k_encode_wire<E, M, PU, U>), dim3(grid), dim3(kBlock), 0, st, a, w, c->ks)
 #define RSK_WIRE4(E, M, PU, U) hipLaunchKernelGGL((k_encode_wire_w4<E, M, PU, U>), dim3(grid), dim3(kBlock), 0, st, a, w, c->ks)
-    // the shipped kernels: per-packet half (DPP copy, 8 packets per iteration, tag + payload prefix in
+    // the per-set kernels: per-packet half (DPP copy, 8 packets per iteration, tag + payload prefix in
     // the copy loop for long-frame sets, 4 waves/SIMD) then the flat half
-    if (wire->with_eth) { RSK_WIRE4(14, 5, 108, 2); RSK_WIRE(14, 4, 2, 2); }
+    if (eth14) { RSK_WIRE4(14, 5, 108, 2); RSK_WIRE(14, 4, 2, 2); }
     else { RSK_WIRE4(0, 5, 108, 2); RSK_WIRE(0, 4, 2, 2); }
 #undef RSK_WIRE
 #undef RSK_WIRE4
+    c->enc_last_path.store(RSK_ENC_PATH_PER_SET, std::memory_order_relaxed);
+    // the statistic for the next call's choice (as rsk_encode_batch)
+    if (c->enc_path == 0 && c->enc_stat_dev && n >= kTwoPassMinPackets && !rsk::capturing(st))
+        hipLaunchKernelGGL(k_enc_sample, dim3(1), dim3(64), 0, st, in->pay_len, n, c->enc_stat_dev);
     return launch_check("k_encode_wire");
 }
 

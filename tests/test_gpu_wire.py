@@ -4,8 +4,6 @@ offsets (every offset r in a 16-B chunk, and packets back to back at byte granul
 zero-pad modes; every packet's IPv4 and TCP checksums re-verified."""
 from __future__ import annotations
 
-import os
-
 import struct
 
 import numpy as np
@@ -23,9 +21,11 @@ KEY = b"hello135"
 @pytest.mark.parametrize("layout", ["aligned", "odd_payload", "odd_wire", "any_wire", "packed_wire"])
 @pytest.mark.parametrize("pad", [0, 16, 128])
 @pytest.mark.parametrize("mix", ["mixed", "short", "bimodal", "long"])
-# shipped kernel only; RSK_LIB=librsk_ab.so RSK_WIRE_VARIANTS=0,1,...,9 covers the A/B build
-@pytest.mark.parametrize("variant", [int(v) for v in os.environ.get("RSK_WIRE_VARIANTS", "0").split(",")])
-def test_wire_batch(codec, gpu, oracle, eth, layout, pad, mix, variant):
+# the wire build's paths, each held (rsk_set_encode_path) and asserted after the call: the per-set wire
+# kernels, and the two-pass form (round 6) with 1, 2 and 4 packets per copy wave
+@pytest.mark.parametrize("wpath", [(1, 0), (2, 1), (2, 2), (2, 4)], ids=["perset", "two_pass_k1", "two_pass_k2",
+                                                                          "two_pass_k4"])
+def test_wire_batch(codec, gpu, oracle, eth, layout, pad, mix, wpath):
     import torch
 
     if layout == "packed_wire" and pad:
@@ -63,16 +63,18 @@ def test_wire_batch(codec, gpu, oracle, eth, layout, pad, mix, variant):
     fill = rng.integers(0, 256, n * pitch_w + 64, dtype=np.uint8)
     wire = dev(fill, gpu)
     status = torch.empty(n, dtype=torch.int32, device=gpu)
-    if variant:
-        codec.set_wire_variant(variant)
+    codec.set_encode_path(wpath[0])
+    codec.set_copy_k(wpath[1])
     codec.output_wire_batch(dev(payload, gpu), dev(pay_off, gpu, np.int64), dev(plen, gpu, np.int16), dev(cmd, gpu),
                             dev(conv, gpu, np.int32), dev(ckey, gpu, np.int64), dev(src, gpu, np.int32),
                             dev(dst, gpu, np.int32), dev(sp, gpu, np.int16), dev(dp, gpu, np.int16),
                             dev(seq, gpu, np.int32), dev(ack, gpu, np.int32), dev(flag, gpu), dev(ipid, gpu, np.int16),
                             wire, dev(wire_off, gpu, np.int64), status, eth=ethb, id_uniform=workload.ID_UNIFORM,
                             pad16=pad == 16, pad128=pad == 128)
-    if variant:
-        codec.set_wire_variant(0)
+    took = (codec.last_encode_path, codec.last_copy_k if wpath[0] == 2 else 0)
+    codec.set_encode_path(0)
+    codec.set_copy_k(0)
+    assert took == wpath, f"wire build held to {wpath} ran {took}"
     torch.cuda.synchronize()
     got, st = wire.cpu().numpy(), status.cpu().numpy()
     exp = fill.copy()

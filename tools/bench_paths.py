@@ -68,6 +68,13 @@ def main():
         "encode_wire_eth": lambda: cx.output_wire_batch(*common, src, dst, sp, dp, seq, ack, flag, ipid, wiree, offe,
                                                         ste, eth=eth, id_uniform=workload.ID_UNIFORM, stream=s,
                                                         **wpad),
+        # the per-set wire kernels held (round 6: AUTO takes the two-pass wire build for long frames)
+        "encode_wire_raw4_perset": lambda: (cx.set_encode_path(1), cx.output_wire_batch(
+            *common, src, dst, sp, dp, seq, ack, flag, ipid, wire4, off4, st4, id_uniform=workload.ID_UNIFORM,
+            stream=s, **wpad), cx.set_encode_path(0)),
+        "encode_wire_eth_perset": lambda: (cx.set_encode_path(1), cx.output_wire_batch(
+            *common, src, dst, sp, dp, seq, ack, flag, ipid, wiree, offe, ste, eth=eth, id_uniform=workload.ID_UNIFORM,
+            stream=s, **wpad), cx.set_encode_path(0)),
         "decode": lambda: cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, w.dec, stream=s),
         "parse_decode": lambda: cx.rawinput_batch(wiree, offe, ste, ste, 1, 0, tcp, pdec, stream=s),
     }
