@@ -800,16 +800,19 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
 // compressions 64 to a wave instead.  rsk_encode_batch takes this form for batches of long frames
 // (enc_path); for short frames one packet per wave idles most lanes and the per-set kernel stays.
 // base: the first packet of this launch (a chunked call runs heads / copy per chunk of packets)
+// Records chunk-major (round 6): chunk 0 of packet i at heads[i], chunk 1 at heads[nr + i] (nr = the
+// records' capacity in packets), so each store instruction of a wave writes 1 KB contiguous instead of
+// 16-B pieces at a 32-B stride.
 template <int SADD = 0>
 __global__ __launch_bounds__(kBlock) void k_encode_heads(EncArgs a, KeySched ks, uint4 *heads, uint32_t *stat,
-                                                         uint64_t base) {
+                                                         uint64_t base, uint64_t nr) {
     stage_tags(ks);
     enc_sample(a.pay_len, a.n, stat);
     const uint64_t i = base + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     const Lane1 L = encode_phase1<true, true, SADD>(a, ks, i < a.n ? i : a.n);
     if (i < a.n && L.st > 0) {
-        heads[2 * i] = make_uint4(L.H[0], L.H[1], L.H[2], L.H[3]);
-        heads[2 * i + 1] = make_uint4(L.H[4], L.H[5], L.H[6], L.H[7]);
+        heads[i] = make_uint4(L.H[0], L.H[1], L.H[2], L.H[3]);
+        heads[nr + i] = make_uint4(L.H[4], L.H[5], L.H[6], L.H[7]);
     }
 }
 
@@ -917,7 +920,7 @@ __device__ __forceinline__ void copyk_store(const EncArgs &a, const CopyK<K> &c,
 // base: the launch's first packet (a grid is limited to 2^32 - 1 work-items, i.e. 2^26 packets at 64
 // per packet: larger batches take several launches, kCopyMaxPackets each).
 template <int NT, int K = 1>
-__global__ __launch_bounds__(kBlock) void k_encode_copy(EncArgs a, const uint32_t *heads, uint64_t base = 0) {
+__global__ __launch_bounds__(kBlock) void k_encode_copy(EncArgs a, const uint32_t *heads, uint64_t base, uint64_t nr) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const uint64_t i0 = base + ((uint64_t)blockIdx.x * kWavesPerBlock + w) * K;
@@ -929,7 +932,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_copy(EncArgs a, const uint32_
         if (!c.flen[p]) continue;  // uniform
         uint32_t Hj[8];
 #pragma unroll
-        for (int t = 0; t < 8; ++t) Hj[t] = heads[8 * (i0 + p) + t];  // uniform address: scalar loads
+        for (int t = 0; t < 8; ++t) Hj[t] = heads[4 * ((t < 4 ? 0 : nr) + i0 + p) + (t & 3)];  // uniform: scalar loads
         copyk_store<K, NT>(a, c, p, lane, Hj);
     }
 }
@@ -1965,9 +1968,11 @@ __global__ __launch_bounds__(kBlock) void k_wire_heads(EncArgs a, WireArgs wa, K
 #pragma unroll
     for (int q = (E + 20) / 4; q < NIW; ++q) s += ((E + 20) % 4 && q == (E + 20) / 4) ? (PW[q] >> 16) : hsum(PW[q]);
     PW[NIW - 1] = s;  // bytes 12..15 of chunk Q: payload positions, overwritten by the copy
-    uint4 *o = rec + (uint64_t)W::NC * i;
+    // chunk-major records (chunk c of packet i at rec[c * n + i]): each store instruction of the wave
+    // writes 1 KB contiguous
 #pragma unroll
-    for (int c = 0; c < W::NC; ++c) o[c] = make_uint4(PW[4 * c], PW[4 * c + 1], PW[4 * c + 2], PW[4 * c + 3]);
+    for (int c = 0; c < W::NC; ++c)
+        rec[(uint64_t)c * a.n + i] = make_uint4(PW[4 * c], PW[4 * c + 1], PW[4 * c + 2], PW[4 * c + 3]);
 }
 
 template <int E, int NT, int K>
@@ -1998,7 +2003,7 @@ __global__ __launch_bounds__(kBlock) void k_wire_copy(EncArgs a, const uint4 *re
         const bool on = i0 + p < a.n && P != 0u && P <= (uint32_t)RSK_MAX_PAYLOAD;  // uniform
         Pp[p] = on ? P : 0u;
         // the record chunk of lane k <= Q
-        H[p] = on && lane <= (uint32_t)Q ? rec[(uint64_t)W::NC * (i0 + p) + lane] : make_uint4(0u, 0u, 0u, 0u);
+        H[p] = on && lane <= (uint32_t)Q ? rec[(uint64_t)lane * a.n + (i0 + p)] : make_uint4(0u, 0u, 0u, 0u);
         const uint8_t *src = a.payload + rdl64(dpo, (uint32_t)p);
         shp[p] = (uint32_t)((reinterpret_cast<uintptr_t>(src) - (uint32_t)R) & 15u);
         const uint8_t *srcp = src - R - shp[p];  // aligned: image chunk k <- source chunks k - Q, k - Q + 1
@@ -3285,14 +3290,15 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
                 EncArgs ac = a;
                 ac.n = (uint32_t)std::min<uint64_t>(n, c0 + chunk);
                 hipLaunchKernelGGL(k_encode_heads<0>, dim3(grid_for(ac.n - c0)), bd, 0, st, ac, c->ks,
-                                   static_cast<uint4 *>(hp), c0 == 0 ? c->enc_stat_dev : nullptr, c0);
+                                   static_cast<uint4 *>(hp), c0 == 0 ? c->enc_stat_dev : nullptr, c0, (uint64_t)n);
                 for (uint64_t b0 = c0; b0 < ac.n; b0 += kCopyMaxPackets) {  // one launch up to 2^25 packets
                     const uint64_t m = ac.n - b0 < kCopyMaxPackets ? ac.n - b0 : kCopyMaxPackets;
                     const dim3 cg((unsigned)((m + 4ull * ck - 1ull) / (4ull * ck)));
                     const uint32_t *hr = static_cast<const uint32_t *>(hp);
-                    if (ck == 2) hipLaunchKernelGGL((k_encode_copy<3, 2>), cg, bd, 0, st, ac, hr, b0);
-                    else if (ck == 4) hipLaunchKernelGGL((k_encode_copy<3, 4>), cg, bd, 0, st, ac, hr, b0);
-                    else hipLaunchKernelGGL((k_encode_copy<3, 1>), cg, bd, 0, st, ac, hr, b0);
+                    const uint64_t nr = n;
+                    if (ck == 2) hipLaunchKernelGGL((k_encode_copy<3, 2>), cg, bd, 0, st, ac, hr, b0, nr);
+                    else if (ck == 4) hipLaunchKernelGGL((k_encode_copy<3, 4>), cg, bd, 0, st, ac, hr, b0, nr);
+                    else hipLaunchKernelGGL((k_encode_copy<3, 1>), cg, bd, 0, st, ac, hr, b0, nr);
                 }
             }
             c->enc_last_path.store(2, std::memory_order_relaxed);

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--variants", default="1,3,2:1,2:2,2:4")
     ap.add_argument("--cases", default="", help="subset of CASES as pmin_pmax,... (default: all)")
+    ap.add_argument("--wire", default="", choices=["", "raw4", "eth"],
+                    help="time rsk_encode_wire_batch (RAW4 / Ethernet wire packets) instead of rsk_encode_batch")
     args = ap.parse_args()
     variants = [tuple(int(x) for x in v.split(":")) for v in args.variants.split(",")]
     vname = lambda v: ":".join(map(str, v))  # noqa: E731
@@ -47,8 +49,28 @@ def main():
         workload.CONFIGS[name] = (20 + k, args.packets, pmin, pmax, 1, False, 0)
         d = workload.describe(name, 0, args.packets, n=args.packets)
         w = workload.DeviceWorkload(d, dev)
+        if args.wire:
+            # wire packets in slots of the frame slot rule over the wire length (link + IPv4 + TCP + frame)
+            L = (14 if args.wire == "eth" else 0) + 40
+            al = 128 if d.pad == 128 else 16
+            wp = (L + 31 + pmax + al - 1) // al * al
+            g = torch.Generator(device=dev)
+            g.manual_seed(k)
+            n_ = args.packets
+            ri = lambda hi, dt: torch.randint(0, hi, (n_,), device=dev, generator=g, dtype=torch.int64).to(dt)  # noqa
+            wf = [ri(2**31, torch.int32), ri(2**31, torch.int32), ri(2**15, torch.int16) + 1, ri(2**15, torch.int16) + 1,
+                  ri(2**31, torch.int32), ri(2**31, torch.int32), torch.full((n_,), 0x18, dtype=torch.uint8, device=dev),
+                  ri(2**15, torch.int16)]
+            w.frame = torch.empty(n_ * wp, dtype=torch.uint8, device=dev)
+            w.frame_off = torch.arange(n_, device=dev, dtype=torch.int64) * wp
+            eth = bytes(range(14)) if args.wire == "eth" else None
 
         def enc():
+            if args.wire:
+                cx.output_wire_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, *wf, w.frame,
+                                     w.frame_off, w.status, eth=eth, id_uniform=workload.ID_UNIFORM,
+                                     pad16=d.pad == 16, pad128=d.pad == 128, stream=s)
+                return
             cx.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
                             w.status, id_uniform=workload.ID_UNIFORM, pad16=d.pad == 16, pad128=d.pad == 128,
                             stream=s)
@@ -83,6 +105,8 @@ def main():
                 torch.cuda.synchronize()
                 t[v].append(e0.elapsed_time(e1) / args.reps)
         byts = int(enc_bytes_per_pkt(d.pay_len.astype(np.int64)).sum())
+        if args.wire:  # + the IPv4/TCP (+ link) header and the 23 B of wire fields per packet
+            byts += args.packets * ((14 if args.wire == "eth" else 0) + 40 + 23)
         out[name] = {"mean_payload": round(float(d.pay_len.mean()), 1), "frame_pitch": d.frame_pitch,
                      "ms": {vname(v): round(float(np.median(t[v])), 4) for v in variants}}
         out[name]["frac_8TBs"] = {k: round(byts / (ms * 1e-3) / 8e12, 4) for k, ms in out[name]["ms"].items()}
