@@ -1924,15 +1924,16 @@ struct WireRec {
     static_assert(R != 0 && R <= 12 && WireGeom<E>::CK / 16 < Q, "record layout");
 };
 
+// base: the chunk's first packet (a.n = its end); chunk c of packet i at rec[c * stride + i - base]
 template <int E>
 __global__ __launch_bounds__(kBlock) void k_wire_heads(EncArgs a, WireArgs wa, KeySched ks, uint4 *rec,
-                                                       uint32_t *stat) {
+                                                       uint32_t *stat, uint64_t base, uint64_t stride) {
     using G = WireGeom<E>;
     using W = WireRec<E>;
     constexpr int NIW = 4 * W::NC;
     stage_tags(ks);
     enc_sample(a.pay_len, a.n, stat);
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t i = base + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     const Lane1 L = encode_phase1<true, true, G::HL>(a, ks, i < a.n ? i : a.n);
     if (i >= a.n || L.st <= 0) return;
     const uint32_t flen = (uint32_t)L.st;
@@ -1968,15 +1969,16 @@ __global__ __launch_bounds__(kBlock) void k_wire_heads(EncArgs a, WireArgs wa, K
 #pragma unroll
     for (int q = (E + 20) / 4; q < NIW; ++q) s += ((E + 20) % 4 && q == (E + 20) / 4) ? (PW[q] >> 16) : hsum(PW[q]);
     PW[NIW - 1] = s;  // bytes 12..15 of chunk Q: payload positions, overwritten by the copy
-    // chunk-major records (chunk c of packet i at rec[c * n + i]): each store instruction of the wave
-    // writes 1 KB contiguous
+    // chunk-major records: each store instruction of the wave writes 1 KB contiguous
 #pragma unroll
     for (int c = 0; c < W::NC; ++c)
-        rec[(uint64_t)c * a.n + i] = make_uint4(PW[4 * c], PW[4 * c + 1], PW[4 * c + 2], PW[4 * c + 3]);
+        rec[(uint64_t)c * stride + (i - base)] = make_uint4(PW[4 * c], PW[4 * c + 1], PW[4 * c + 2], PW[4 * c + 3]);
 }
 
+// base: the launch's first packet; rbase / stride: the record chunk's (k_wire_heads)
 template <int E, int NT, int K>
-__global__ __launch_bounds__(kBlock) void k_wire_copy(EncArgs a, const uint4 *rec, uint64_t base) {
+__global__ __launch_bounds__(kBlock) void k_wire_copy(EncArgs a, const uint4 *rec, uint64_t base, uint64_t rbase,
+                                                      uint64_t stride) {
     using G = WireGeom<E>;
     using W = WireRec<E>;
     constexpr int HB = W::HB, Q = W::Q, R = W::R;
@@ -2003,7 +2005,7 @@ __global__ __launch_bounds__(kBlock) void k_wire_copy(EncArgs a, const uint4 *re
         const bool on = i0 + p < a.n && P != 0u && P <= (uint32_t)RSK_MAX_PAYLOAD;  // uniform
         Pp[p] = on ? P : 0u;
         // the record chunk of lane k <= Q
-        H[p] = on && lane <= (uint32_t)Q ? rec[(uint64_t)lane * a.n + (i0 + p)] : make_uint4(0u, 0u, 0u, 0u);
+        H[p] = on && lane <= (uint32_t)Q ? rec[(uint64_t)lane * stride + (i0 + p - rbase)] : make_uint4(0u, 0u, 0u, 0u);
         const uint8_t *src = a.payload + rdl64(dpo, (uint32_t)p);
         shp[p] = (uint32_t)((reinterpret_cast<uintptr_t>(src) - (uint32_t)R) & 15u);
         const uint8_t *srcp = src - R - shp[p];  // aligned: image chunk k <- source chunks k - Q, k - Q + 1
@@ -3329,6 +3331,32 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
     return launch_check("k_encode");
 }
 
+// The wire build's choice (round 6; tools/path_threshold.py --wire raw4 / eth, profiles/r06_wire_paths.json):
+// under AUTO the per-set wire kernels below a mean payload of kWireTwoPassFrom, and for Ethernet packets
+// from kWireEthPerSetFrom (4M x 1400 B: per-set 2.285, two-pass 2.296-2.373 ms); the two-pass form
+// otherwise, with 4 packets per copy wave, RAW4 from kWireK2From 2 (4M x 1400 B: 2.200 vs 2.230 for 1,
+// 2.288 per-set).
+constexpr uint32_t kWireTwoPassFrom = 160;
+constexpr uint32_t kWireEthPerSetFrom = 1300;
+constexpr uint32_t kWireK2From = 1080;
+constexpr uint64_t kWireChunk = 1ull << 20;
+static int wire_path(rsk_ctx *c, uint32_t n, const uint16_t *pay_len, hipStream_t st, bool eth) {
+    if (c->enc_path) return c->enc_path == RSK_ENC_PATH_TWO_PASS ? RSK_ENC_PATH_TWO_PASS : RSK_ENC_PATH_PER_SET;
+    const int ep = enc_path(c, n, pay_len, st);  // the first-call sample, and the statistic
+    if (ep < 0) return ep;
+    const uint32_t s = sampled_mean(c);
+    if (n < kTwoPassMinPackets || !(s & kStatValid)) return RSK_ENC_PATH_PER_SET;
+    const uint32_t mean = s & ~kStatValid;
+    return mean < kWireTwoPassFrom || (eth && mean >= kWireEthPerSetFrom) ? RSK_ENC_PATH_PER_SET
+                                                                          : RSK_ENC_PATH_TWO_PASS;
+}
+static int wire_k(rsk_ctx *c, bool eth) {
+    if (c->copy_k) return c->copy_k;
+    const uint32_t s = sampled_mean(c);
+    const uint32_t mean = (s & kStatValid) ? s & ~kStatValid : 1400u;
+    return eth || mean < kWireK2From ? 4 : 2;
+}
+
 int rsk_encode_wire_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_wire_in *wire,
                           const rsk_encode_out *out, void *stream) {
     if (!c || !in || !wire || !out) return RSK_EINVAL;
@@ -3358,24 +3386,31 @@ int rsk_encode_wire_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const
     const unsigned grid = enc_grid(n, 8, 1024);
     const hipStream_t st = (hipStream_t)stream;
     const bool eth14 = wire->with_eth != 0;
-    // the encode's path choice (rsk_set_encode_path, or AUTO by the sampled mean payload): the two-pass
-    // form -- k_wire_heads (header images, 80 / 96-B records in the stream's scratch) + k_wire_copy with
-    // 1, 2 or 4 packets per copy wave (round 6) -- for batches of long frames, else the per-set kernels
-    const int path = enc_path(c, n, in->pay_len, st);
+    // the encode path the context is held to (rsk_set_encode_path: two-pass, or else the per-set wire
+    // kernels), or AUTO's wire table (wire_path): the two-pass form -- k_wire_heads (header images,
+    // 80 / 96-B records in the stream's scratch) + k_wire_copy with 1, 2 or 4 packets per copy wave
+    // (round 6) -- from a mean payload of 160 B (Ethernet: up to 1300 B), the per-set kernels otherwise
+    const int path = wire_path(c, n, in->pay_len, st, eth14);
     if (path < 0) return path;
     if (path == RSK_ENC_PATH_TWO_PASS) {
         void *hp = nullptr;
         const uint64_t recb = 16ull * (eth14 ? WireRec<14>::NC : WireRec<0>::NC);  // 96 / 80 B per packet
-        if (rsk::stream_ws_if(c, st, rsk::WS_ENC, recb * n, &hp) == RSK_OK) {
-            const int ck = copy_k(c);
+        // header pass then copy per chunk of kWireChunk packets: one chunk's records (80 / 96 MB at 1M)
+        // stay in the Infinity Cache until its copy reads them (a whole C3 batch's, 320 MB, do not)
+        const uint64_t chunk = n < kWireChunk ? (uint64_t)n : kWireChunk;
+        if (rsk::stream_ws_if(c, st, rsk::WS_ENC, recb * chunk, &hp) == RSK_OK) {
+            const int ck = wire_k(c, eth14);
             const dim3 bd(kBlock);
             uint4 *rec = static_cast<uint4 *>(hp);
-            if (eth14) hipLaunchKernelGGL(k_wire_heads<14>, dim3(grid_for(n)), bd, 0, st, a, w, c->ks, rec, c->enc_stat_dev);
-            else hipLaunchKernelGGL(k_wire_heads<0>, dim3(grid_for(n)), bd, 0, st, a, w, c->ks, rec, c->enc_stat_dev);
-            for (uint64_t b0 = 0; b0 < n; b0 += kCopyMaxPackets) {  // one launch up to 2^25 packets
-                const uint64_t m = n - b0 < kCopyMaxPackets ? n - b0 : kCopyMaxPackets;
-                const dim3 cg((unsigned)((m + 4ull * ck - 1ull) / (4ull * ck)));
-#define RSK_WCOPY(E, K) hipLaunchKernelGGL((k_wire_copy<E, 3, K>), cg, bd, 0, st, a, rec, b0)
+            for (uint64_t c0 = 0; c0 < n; c0 += chunk) {
+                EncArgs ac = a;
+                ac.n = (uint32_t)std::min<uint64_t>(n, c0 + chunk);
+                const uint64_t m = ac.n - c0;
+                uint32_t *stat = c0 == 0 ? c->enc_stat_dev : nullptr;
+                if (eth14) hipLaunchKernelGGL(k_wire_heads<14>, dim3(grid_for(m)), bd, 0, st, ac, w, c->ks, rec, stat, c0, chunk);
+                else hipLaunchKernelGGL(k_wire_heads<0>, dim3(grid_for(m)), bd, 0, st, ac, w, c->ks, rec, stat, c0, chunk);
+                const dim3 cg((unsigned)((m + 4ull * ck - 1ull) / (4ull * ck)));  // m <= kWireChunk: one launch
+#define RSK_WCOPY(E, K) hipLaunchKernelGGL((k_wire_copy<E, 3, K>), cg, bd, 0, st, ac, rec, c0, c0, chunk)
                 if (eth14) {
                     if (ck == 2) RSK_WCOPY(14, 2); else if (ck == 4) RSK_WCOPY(14, 4); else RSK_WCOPY(14, 1);
                 } else {

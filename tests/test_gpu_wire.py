@@ -138,3 +138,80 @@ def test_wire_to_parse_loop(codec, gpu):
     assert torch.equal(tcp.cap_pay_off.to(torch.int64), torch.full_like(plen, 54))
     assert torch.equal(out.conv, w.conv) and torch.equal(out.conn_key, w.conn_key) and torch.equal(out.cmd, w.cmd)
     assert torch.equal(out.pay_len.to(torch.int64) & 0xFFFF, plen - 31)
+
+
+@pytest.mark.parametrize("eth", [False, True])
+def test_wire_two_pass_chunks_equal_per_set(codec, gpu, eth):
+    """The two-pass wire build runs its header pass and copy per chunk of 2^20 packets (records stay in
+    the Infinity Cache): a batch of 2^20 + 4097 C4 packets (two chunks, the second ragged) built on the
+    two-pass path with 1, 2 and 4 packets per copy wave equals the per-set kernels' packets byte for
+    byte, and every status is the wire length."""
+    import torch
+
+    n = (1 << 20) + 4097
+    d = workload.describe("c4", 0, n, n=n)
+    w = workload.DeviceWorkload(d, gpu)
+    g = torch.Generator(device=gpu)
+    g.manual_seed(9)
+    ri = lambda hi, dt: torch.randint(0, hi, (n,), device=gpu, generator=g, dtype=torch.int64).to(dt)  # noqa: E731
+    fields = [ri(2**31, torch.int32), ri(2**31, torch.int32), ri(2**15, torch.int16) + 1, ri(2**15, torch.int16) + 1,
+              ri(2**31, torch.int32), ri(2**31, torch.int32), ri(256, torch.uint8), ri(2**15, torch.int16)]
+    pitch = 1536
+    woff = torch.arange(n, device=gpu, dtype=torch.int64) * pitch
+    ethb = bytes(range(14)) if eth else None
+    outs = {}
+    try:
+        for path, k in [(1, 0), (2, 1), (2, 2), (2, 4)]:
+            codec.set_encode_path(path)
+            codec.set_copy_k(k)
+            wire = torch.zeros(n * pitch, dtype=torch.uint8, device=gpu)
+            st = torch.empty(n, dtype=torch.int32, device=gpu)
+            codec.output_wire_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, *fields, wire, woff, st,
+                                    eth=ethb, id_uniform=workload.ID_UNIFORM, pad128=True)
+            assert codec.last_encode_path == path
+            torch.cuda.synchronize()
+            outs[(path, k)] = (wire, st)
+            if path == 2:
+                ref_w, ref_s = outs[(1, 0)]
+                assert torch.equal(st, ref_s), (path, k)
+                assert torch.equal(wire, ref_w), (path, k)
+                del outs[(path, k)]
+        plen = w.pay_len.to(torch.int64) & 0xFFFF
+        exp = torch.where((plen >= 1) & (plen <= 1469), plen + 31 + 40 + (14 if eth else 0), outs[(1, 0)][1].to(torch.int64))
+        assert torch.equal(outs[(1, 0)][1].to(torch.int64), exp)
+    finally:
+        codec.set_encode_path(0)
+        codec.set_copy_k(0)
+
+
+@pytest.mark.parametrize("cfg,eth,exp", [("c4", False, (2, 4)), ("c4", True, (2, 4)), ("c3", False, (2, 2)),
+                                          ("c3", True, (1, 0)), ("c2", False, (1, 0)), ("c2", True, (1, 0))])
+def test_wire_auto_path(gpu, cfg, eth, exp):
+    """AUTO's wire table (rsk_kernels.hip wire_path / wire_k, profiles/r06_wire_paths.json): the per-set
+    wire kernels for short frames (C2) and for Ethernet packets of 1400-B payloads (C3), the two-pass
+    form with 4 packets per copy wave for mid-length frames (C4) and 2 for RAW4 packets of 1400 B --
+    from a fresh context's first call (it samples its own batch) on."""
+    import torch
+
+    from rsock_amd.codec import Codec
+
+    n = 40_000
+    d = workload.describe(cfg, 0, n, n=n)
+    w = workload.DeviceWorkload(d, gpu)
+    z = lambda dt: torch.ones(n, dtype=dt, device=gpu)  # noqa: E731
+    pitch = 1536
+    wire = torch.zeros(n * pitch, dtype=torch.uint8, device=gpu)
+    woff = torch.arange(n, device=gpu, dtype=torch.int64) * pitch
+    st = torch.empty(n, dtype=torch.int32, device=gpu)
+    cx = Codec(KEY, 0)
+    try:
+        for _ in range(2):
+            cx.output_wire_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, z(torch.int32),
+                                 z(torch.int32), z(torch.int16), z(torch.int16), z(torch.int32), z(torch.int32),
+                                 z(torch.uint8), z(torch.int16), wire, woff, st, eth=bytes(14) if eth else None,
+                                 id_uniform=workload.ID_UNIFORM, pad128=True)
+            got = (cx.last_encode_path, cx.last_copy_k if cx.last_encode_path == 2 else 0)
+            assert got == exp, (cfg, eth, got)
+        torch.cuda.synchronize()
+    finally:
+        cx.close()
