@@ -288,13 +288,6 @@ class Codec:
         fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
         _check(fn(self._ctx, k), "rsk__set_copy_k")
 
-    def set_two_pass_overlap(self, packets: int = 0) -> None:
-        """Internal knob (rsk__set_two_pass_overlap): the two-pass encode in chunks of `packets`, each
-        chunk's copy overlapping the next chunk's header pass on a second stream (0 = off)."""
-        fn = lib().rsk__set_two_pass_overlap
-        fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
-        _check(fn(self._ctx, packets), "rsk__set_two_pass_overlap")
-
     def set_two_pass_chunk(self, packets: int = 0) -> None:
         """Internal knob of the two-pass encode (rsk__set_two_pass_chunk): header pass then copy per chunk
         of `packets` (0 = the whole batch)."""

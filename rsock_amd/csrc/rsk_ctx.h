@@ -50,14 +50,6 @@ struct rsk_ctx {
     // different streams never share scratch, calls on one stream are ordered by it (rsk_codec.h).
     std::mutex ws_mu;
     std::unordered_map<hipStream_t, std::array<rsk::WsBuf, rsk::WS_KINDS>> ws;
-    // per caller stream: the second stream the two-pass encode runs its header passes on while the
-    // copy of the previous chunk runs on the caller's (rsk_encode_batch, overlapped form), and its events
-    struct Aux {
-        hipStream_t s2 = nullptr;
-        hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // start, heads ready x2, region free x2
-    };
-    std::unordered_map<hipStream_t, Aux> aux;
-    uint32_t tp_overlap = 0;  // overlapped two-pass chunk (packets; 0: off), rsk__set_two_pass_overlap
     bool sq_force_groupby = false;  // see rsk__set_send_seq_groupby
     int sq_scan_variant = 0;
     // single-packet shim buffers
@@ -226,32 +218,6 @@ inline hipError_t sync_ctx_streams(rsk_ctx *c) {
     return stale ? hipDeviceSynchronize() : hipSuccess;
 }
 
-// The aux stream + events of caller stream s (created on first use; never while s is being captured:
-// nullptr then, and the caller takes the one-stream form).  Caller holds no lock.
-inline rsk_ctx::Aux *aux_for(rsk_ctx *c, hipStream_t s) {
-    std::lock_guard<std::mutex> lk(c->ws_mu);
-    auto it = c->aux.find(s);
-    if (it != c->aux.end()) return &it->second;
-    if (capturing(s)) return nullptr;
-    rsk_ctx::Aux a;
-    hipError_t e = hipStreamCreateWithFlags(&a.s2, hipStreamNonBlocking);
-    for (int q = 0; q < 5 && e == hipSuccess; ++q) e = hipEventCreateWithFlags(&a.ev[q], hipEventDisableTiming);
-    if (e != hipSuccess) {
-        for (hipEvent_t ev : a.ev)
-            if (ev) (void)hipEventDestroy(ev);
-        if (a.s2) (void)hipStreamDestroy(a.s2);
-        (void)hipGetLastError();
-        return nullptr;
-    }
-    return &(c->aux[s] = a);
-}
-inline void aux_free(rsk_ctx::Aux &a) {
-    if (a.s2) (void)hipStreamSynchronize(a.s2);
-    for (hipEvent_t ev : a.ev)
-        if (ev) (void)hipEventDestroy(ev);
-    if (a.s2) (void)hipStreamDestroy(a.s2);
-}
-
 // Sync s, then free its scratch (rsk_release_stream).  Graphs captured on s point at that scratch:
 // they must be destroyed first (rsk_codec.h, rsk_release_stream).
 inline int release_ws(rsk_ctx *c, hipStream_t s) {
@@ -263,11 +229,6 @@ inline int release_ws(rsk_ctx *c, hipStream_t s) {
     for (WsBuf &b : it->second)
         if (b.p) (void)hipFree(b.p);
     c->ws.erase(it);
-    auto ia = c->aux.find(s);
-    if (ia != c->aux.end()) {
-        aux_free(ia->second);
-        c->aux.erase(ia);
-    }
     return RSK_OK;
 }
 
@@ -277,8 +238,6 @@ inline void free_ws(rsk_ctx *c) {
         for (WsBuf &b : kv.second)
             if (b.p) (void)hipFree(b.p);
     c->ws.clear();
-    for (auto &kv : c->aux) aux_free(kv.second);
-    c->aux.clear();
 }
 
 }  // namespace rsk

@@ -805,14 +805,14 @@ __device__ __forceinline__ void encode_set(const EncArgs &a, const KeySched &ks,
 // 16-B pieces at a 32-B stride.
 template <int SADD = 0>
 __global__ __launch_bounds__(kBlock) void k_encode_heads(EncArgs a, KeySched ks, uint4 *heads, uint32_t *stat,
-                                                         uint64_t base, uint64_t nr, uint64_t rbase) {
+                                                         uint64_t base, uint64_t nr) {
     stage_tags(ks);
     enc_sample(a.pay_len, a.n, stat);
     const uint64_t i = base + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     const Lane1 L = encode_phase1<true, true, SADD>(a, ks, i < a.n ? i : a.n);
     if (i < a.n && L.st > 0) {
-        heads[i - rbase] = make_uint4(L.H[0], L.H[1], L.H[2], L.H[3]);
-        heads[nr + i - rbase] = make_uint4(L.H[4], L.H[5], L.H[6], L.H[7]);
+        heads[i] = make_uint4(L.H[0], L.H[1], L.H[2], L.H[3]);
+        heads[nr + i] = make_uint4(L.H[4], L.H[5], L.H[6], L.H[7]);
     }
 }
 
@@ -920,8 +920,7 @@ __device__ __forceinline__ void copyk_store(const EncArgs &a, const CopyK<K> &c,
 // base: the launch's first packet (a grid is limited to 2^32 - 1 work-items, i.e. 2^26 packets at 64
 // per packet: larger batches take several launches, kCopyMaxPackets each).
 template <int NT, int K = 1>
-__global__ __launch_bounds__(kBlock) void k_encode_copy(EncArgs a, const uint32_t *heads, uint64_t base, uint64_t nr,
-                                                        uint64_t rbase) {
+__global__ __launch_bounds__(kBlock) void k_encode_copy(EncArgs a, const uint32_t *heads, uint64_t base, uint64_t nr) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const uint64_t i0 = base + ((uint64_t)blockIdx.x * kWavesPerBlock + w) * K;
@@ -933,7 +932,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_copy(EncArgs a, const uint32_
         if (!c.flen[p]) continue;  // uniform
         uint32_t Hj[8];
 #pragma unroll
-        for (int t = 0; t < 8; ++t) Hj[t] = heads[4 * ((t < 4 ? 0 : nr) + i0 + p - rbase) + (t & 3)];  // uniform: scalar loads
+        for (int t = 0; t < 8; ++t) Hj[t] = heads[4 * ((t < 4 ? 0 : nr) + i0 + p) + (t & 3)];  // uniform: scalar loads
         copyk_store<K, NT>(a, c, p, lane, Hj);
     }
 }
@@ -3135,13 +3134,6 @@ int rsk__set_copy_k(rsk_ctx *c, int k) {
 int rsk__last_copy_k(const rsk_ctx *c) { return c ? c->enc_last_k.load(std::memory_order_relaxed) : RSK_EINVAL; }
 
 // Internal (tests, tools): the two-pass form in chunks of `packets` (0: the whole batch in one pass each)
-// internal A/B knob: the overlapped two-pass form's chunk (packets, <= 2^25; 0 = off)
-int rsk__set_two_pass_overlap(rsk_ctx *c, uint32_t packets) {
-    if (!c || packets > kCopyMaxPackets) return RSK_EINVAL;
-    c->tp_overlap = packets;
-    return RSK_OK;
-}
-
 int rsk__set_two_pass_chunk(rsk_ctx *c, uint32_t packets) {
     if (!c) return RSK_EINVAL;
     c->tp_chunk = packets;
@@ -3293,49 +3285,6 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
         void *hp = nullptr;
         if (rsk::stream_ws_if(c, st, rsk::WS_ENC, 32ull * n, &hp) == RSK_OK) {
             const int ck = copy_k(c);
-            // overlapped (rsk__set_two_pass_overlap): chunk j's copy on the caller's stream while chunk j + 1's
-            // header pass runs on the context's second stream for it, records double-buffered
-            const uint64_t och = c->tp_overlap;
-            rsk_ctx::Aux *ax = och && n > och ? rsk::aux_for(c, st) : nullptr;
-            void *hp2 = nullptr;
-            if (ax && rsk::stream_ws_if(c, st, rsk::WS_ENC, 64ull * och, &hp2) == RSK_OK) {
-                const int ck = copy_k(c);
-                uint4 *reg[2] = {static_cast<uint4 *>(hp2), static_cast<uint4 *>(hp2) + 2ull * och};
-                hipEvent_t ev_start = ax->ev[0], ev_h[2] = {ax->ev[1], ax->ev[2]}, ev_c[2] = {ax->ev[3], ax->ev[4]};
-                hipStream_t s2 = ax->s2;
-                const uint64_t J = (n + och - 1) / och;
-                auto heads = [&](uint64_t j) {
-                    EncArgs ac = a;
-                    const uint64_t c0 = j * och;
-                    ac.n = (uint32_t)std::min<uint64_t>(n, c0 + och);
-                    hipLaunchKernelGGL(k_encode_heads<0>, dim3(grid_for(ac.n - c0)), bd, 0, s2, ac, c->ks, reg[j & 1],
-                                       j == 0 ? c->enc_stat_dev : nullptr, c0, och, c0);
-                    (void)hipEventRecord(ev_h[j & 1], s2);
-                };
-                (void)hipEventRecord(ev_start, st);  // the second stream starts behind the caller's work
-                (void)hipStreamWaitEvent(s2, ev_start, 0);
-                heads(0);
-                for (uint64_t j = 0; j < J; ++j) {
-                    (void)hipStreamWaitEvent(st, ev_h[j & 1], 0);
-                    EncArgs ac = a;
-                    const uint64_t c0 = j * och;
-                    ac.n = (uint32_t)std::min<uint64_t>(n, c0 + och);
-                    const uint64_t m = ac.n - c0;  // <= och <= kCopyMaxPackets
-                    const dim3 cg((unsigned)((m + 4ull * ck - 1ull) / (4ull * ck)));
-                    const uint32_t *hr = reinterpret_cast<const uint32_t *>(reg[j & 1]);
-                    if (ck == 2) hipLaunchKernelGGL((k_encode_copy<3, 2>), cg, bd, 0, st, ac, hr, c0, och, c0);
-                    else if (ck == 4) hipLaunchKernelGGL((k_encode_copy<3, 4>), cg, bd, 0, st, ac, hr, c0, och, c0);
-                    else hipLaunchKernelGGL((k_encode_copy<3, 1>), cg, bd, 0, st, ac, hr, c0, och, c0);
-                    (void)hipEventRecord(ev_c[j & 1], st);
-                    if (j + 1 < J) {
-                        if (j >= 1) (void)hipStreamWaitEvent(s2, ev_c[(j + 1) & 1], 0);  // region free: copy j - 1 done
-                        heads(j + 1);
-                    }
-                }
-                c->enc_last_path.store(2, std::memory_order_relaxed);
-                c->enc_last_k.store(ck, std::memory_order_relaxed);
-                return launch_check("k_encode_heads / k_encode_copy (overlapped)");
-            }
             // chunked (rsk__set_two_pass_chunk): heads then copy per chunk, so a chunk's records and
             // first payload lines may still be in the Infinity Cache when its copy reads them
             const uint64_t chunk = c->tp_chunk ? c->tp_chunk : (uint64_t)n;
@@ -3343,15 +3292,15 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
                 EncArgs ac = a;
                 ac.n = (uint32_t)std::min<uint64_t>(n, c0 + chunk);
                 hipLaunchKernelGGL(k_encode_heads<0>, dim3(grid_for(ac.n - c0)), bd, 0, st, ac, c->ks,
-                                   static_cast<uint4 *>(hp), c0 == 0 ? c->enc_stat_dev : nullptr, c0, (uint64_t)n, 0ull);
+                                   static_cast<uint4 *>(hp), c0 == 0 ? c->enc_stat_dev : nullptr, c0, (uint64_t)n);
                 for (uint64_t b0 = c0; b0 < ac.n; b0 += kCopyMaxPackets) {  // one launch up to 2^25 packets
                     const uint64_t m = ac.n - b0 < kCopyMaxPackets ? ac.n - b0 : kCopyMaxPackets;
                     const dim3 cg((unsigned)((m + 4ull * ck - 1ull) / (4ull * ck)));
                     const uint32_t *hr = static_cast<const uint32_t *>(hp);
                     const uint64_t nr = n;
-                    if (ck == 2) hipLaunchKernelGGL((k_encode_copy<3, 2>), cg, bd, 0, st, ac, hr, b0, nr, 0ull);
-                    else if (ck == 4) hipLaunchKernelGGL((k_encode_copy<3, 4>), cg, bd, 0, st, ac, hr, b0, nr, 0ull);
-                    else hipLaunchKernelGGL((k_encode_copy<3, 1>), cg, bd, 0, st, ac, hr, b0, nr, 0ull);
+                    if (ck == 2) hipLaunchKernelGGL((k_encode_copy<3, 2>), cg, bd, 0, st, ac, hr, b0, nr);
+                    else if (ck == 4) hipLaunchKernelGGL((k_encode_copy<3, 4>), cg, bd, 0, st, ac, hr, b0, nr);
+                    else hipLaunchKernelGGL((k_encode_copy<3, 1>), cg, bd, 0, st, ac, hr, b0, nr);
                 }
             }
             c->enc_last_path.store(2, std::memory_order_relaxed);

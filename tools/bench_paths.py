@@ -68,15 +68,6 @@ def main():
         "encode_wire_eth": lambda: cx.output_wire_batch(*common, src, dst, sp, dp, seq, ack, flag, ipid, wiree, offe,
                                                         ste, eth=eth, id_uniform=workload.ID_UNIFORM, stream=s,
                                                         **wpad),
-        # the two-pass encode with each chunk's copy overlapping the next chunk's header pass (round 6)
-        "encode_overlap": lambda: (cx.set_two_pass_overlap(1 << 20), cx.output_batch(
-            w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off, w.status,
-            id_uniform=workload.ID_UNIFORM, pad16=d.pad == 16, pad128=d.pad == 128, stream=s),
-            cx.set_two_pass_overlap(0)),
-        "encode_overlap512k": lambda: (cx.set_two_pass_overlap(1 << 19), cx.output_batch(
-            w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off, w.status,
-            id_uniform=workload.ID_UNIFORM, pad16=d.pad == 16, pad128=d.pad == 128, stream=s),
-            cx.set_two_pass_overlap(0)),
         # the per-set wire kernels held (round 6: AUTO takes the two-pass wire build for long frames)
         "encode_wire_raw4_perset": lambda: (cx.set_encode_path(1), cx.output_wire_batch(
             *common, src, dst, sp, dp, seq, ack, flag, ipid, wire4, off4, st4, id_uniform=workload.ID_UNIFORM,
@@ -189,8 +180,6 @@ def main():
     p = float(d.pay_len.astype(np.float64).mean())
     alg = {  # algorithmic bytes per packet
         "encode": 2 * p + 66,
-        "encode_overlap": 2 * p + 66,
-        "encode_overlap512k": 2 * p + 66,
         "encode_wire_raw4": 2 * p + 66 + 40 + 23,
         "encode_wire_eth": 2 * p + 66 + 54 + 23,
         "encode_wire_raw4_pkt": 2 * p + 66 + 40 + 23,
