@@ -135,7 +135,7 @@ __device__ __forceinline__ void head_words(uint32_t cmd, uint32_t id0, uint32_t 
 // ---- phase 1: one lane per packet ---------------------------------------------------------------
 // status (RConn.cpp:88-98), tag (rhash.cpp:20-41 via md5_tag), frame words 0..7 (tag + EncHead +
 // payload[0]); `slow` marks a framed packet whose frame is not 16-B aligned (k_encode_wire: the
-// shifted copies; the byte path of the A/B modes).
+// shifted copies).
 struct Lane1 {
     int32_t st;
     uint64_t po, fo;
@@ -1099,77 +1099,6 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     return rdl(v, 15) + rdl(v, 31) + rdl(v, 47) + rdl(v, 63);
 }
 
-// ---- per-packet copy, PU packets per iteration: lane l takes payload chunks NPRE + l and
-// NPRE + 64 + l (a packet has at most 88 past the prefix); the halfword sums of those chunks are
-// reduced over the wave into the TCP checksum, which lane CK/16 patches into its prefix chunk (read
-// from the wave's LDS stage of the 64 lanes' prefix images) before the stores.
-template <int E, int PU>
-__device__ __forceinline__ void copy_wire_pkt(const EncArgs &a, const Lane1 &L, const uint32_t *stage,
-                                              uint32_t sum_pre, int32_t wst, uint32_t lane, uint64_t vm) {
-    using G = WireGeom<E>;
-    while (vm) {
-        uint32_t js[PU];
-        bool on[PU];
-#pragma unroll
-        for (int p = 0; p < PU; ++p) {
-            on[p] = vm != 0ull;
-            js[p] = on[p] ? (uint32_t)__builtin_ctzll(vm) : 0u;
-            if (on[p]) vm &= vm - 1ull;
-        }
-        uint4 v[PU][2];
-        uint32_t ck[PU], wlen[PU];
-        uint8_t *dstp[PU];
-#pragma unroll
-        for (int p = 0; p < PU; ++p) {
-            wlen[p] = on[p] ? (uint32_t)rdl((uint32_t)wst, js[p]) : 0u;
-            const uint32_t P = wlen[p] - G::HB;
-            const uint8_t *pay = a.payload + rdl64(L.po, js[p]);
-            dstp[p] = a.frame + rdl64(L.fo, js[p]);
-            const uint32_t sh = (uint32_t)((reinterpret_cast<uintptr_t>(pay) + G::D0) & 15u);
-            const uint8_t *src_al = pay + G::D0 - sh;
-            const int32_t last_rel = (int32_t)P - 1 - G::D0 + (int32_t)sh;
-            const uint32_t nch = (wlen[p] + 15u) >> 4;
-            uint32_t part = 0;
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const uint32_t k = G::NPRE + lane + 64u * q;
-                uint4 A = make_uint4(0u, 0u, 0u, 0u), B = make_uint4(0u, 0u, 0u, 0u);
-                if (k < nch) {
-                    const uint32_t ro = 16u * (k - G::NPRE);
-                    A = ld16<0>(src_al + ro);
-                    if (sh != 0u && (int32_t)(ro + 16u) <= last_rel) B = ld16<0>(src_al + ro + 16u);
-                }
-                v[p][q] = rsk::funnel16(A, B, sh);
-                const int lim = (int)wlen[p] - 16 * (int)k;
-                if (k < nch) {
-                    if (lim < 16) v[p][q] = rsk::keep_bytes16(v[p][q], lim);
-                    part = hsum4(v[p][q], part);
-                }
-            }
-            ck[p] = part;
-        }
-#pragma unroll
-        for (int p = 0; p < PU; ++p) ck[p] = ~fold16(wave_sum(ck[p]) + rdl(sum_pre, js[p])) & 0xffffu;
-#pragma unroll
-        for (int p = 0; p < PU; ++p) {
-            if (!on[p]) continue;
-            const uint32_t nst = (padded_len(dstp[p], wlen[p], a.pad) + 15u) >> 4;
-            if (lane < (uint32_t)G::NPRE && lane < nst) {
-                const uint4 sv = *reinterpret_cast<const uint4 *>(stage + js[p] * G::NPW + 4u * lane);
-                uint32_t w4[4] = {sv.x, sv.y, sv.z, sv.w};
-                if (lane == (uint32_t)(G::CK / 16)) w4[(G::CK & 15) >> 2] |= ck[p] << (8 * (G::CK & 3));
-                store_last16<0>(dstp[p] + 16u * lane, make_uint4(w4[0], w4[1], w4[2], w4[3]),
-                                (int)wlen[p] - 16 * (int)lane, a.pad != 0u);
-            }
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const uint32_t k = G::NPRE + lane + 64u * q;
-                if (k < nst) store_last16<0>(dstp[p] + 16u * k, v[p][q], (int)wlen[p] - 16 * (int)k, a.pad != 0u);
-            }
-        }
-    }
-}
-
 // A wire packet whose first byte sits r = dst mod 16 (1..15) bytes into a chunk: destination chunk j
 // (aligned base d0 = dst - r) holds wire-image bytes [16j - r, 16j - r + 16), i.e. the 16 bytes at
 // offset 16 - r of image chunks j - 1 and j.  Image chunks c < NPRE are the prefix image in LDS (the
@@ -1358,157 +1287,6 @@ __device__ __forceinline__ void copy_wire_pkt_dpp(const EncArgs &a, const KeySch
                 wire_store_shifted<E, NT>(a, stage + js[p] * G::NPW, ck[p], dstp[p], r, wlen[p], v[p], lane);
             }
         }
-    }
-}
-
-// ---- software-pipelined form of copy_wire_pkt_dpp (as copy_pkt_pipe for k_encode): the loads of
-// the next PU packets (TAG: the payload prefix of lane p's packet, two aligned 16-B chunks, then the
-// payload chunks) are issued before the current PU packets are summed and stored.  Every load runs
-// with all lanes (dead lanes re-read a mapped chunk), so a batch's load count is static and the wait
-// for the older batch leaves the newer one in flight.  Payload chunks are stored as soon as they are
-// summed; only the prefix chunks wait for the packet's checksum.
-template <int E, int PU, bool TAG>
-__device__ __forceinline__ void wire_issue(const EncArgs &a, const Lane1 &L, int32_t wst, uint32_t lane,
-                                           uint64_t bm, uint4 (&A)[PU][2], uint4 (&pc)[2]) {
-    using G = WireGeom<E>;
-    uint32_t js[PU], myj;
-    bool on[PU], mine;
-    batch_slots<PU>(bm, lane, js, on, myj, mine);
-    if constexpr (TAG) {  // lane p: the first 16 payload bytes of packet p
-        const uint64_t po = shfl64(L.po, myj);
-        const uint32_t wl = (uint32_t)__shfl((int)wst, (int)myj);  // with every lane active (bpermute)
-        const uint32_t P = mine ? wl - G::HB : 0u;
-        const uint8_t *pay = a.payload + (mine ? po : 0u);
-        const uint8_t *al = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(pay) & ~(uintptr_t)15);
-        const uint32_t r = (uint32_t)(reinterpret_cast<uintptr_t>(pay) & 15u);
-        pc[0] = ld16<0>(al);
-        pc[1] = ld16<0>(16u - r < P ? al + 16 : al);
-    }
-#pragma unroll
-    for (int p = 0; p < PU; ++p) {
-        const uint32_t wlen = on[p] ? (uint32_t)rdl((uint32_t)wst, js[p]) : 0u;
-        const uint32_t P = wlen - G::HB;
-        const uint8_t *pay = a.payload + rdl64(L.po, js[p]);
-        const uint32_t shp = (uint32_t)((reinterpret_cast<uintptr_t>(pay) + G::D0) & 15u);
-        const uint8_t *src_al = pay + G::D0 - shp;
-        const int32_t last_rel = (int32_t)P - 1 - G::D0 + (int32_t)shp;
-        const uint8_t *dummy = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(pay) & ~(uintptr_t)15);
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const uint32_t m = lane + 64u * q;  // source chunk of frame chunk NPRE + m
-            const bool live = on[p] && (int32_t)(16u * m) <= last_rel;
-            A[p][q] = ld16<0>(live ? src_al + 16u * m : dummy);  // dead lanes zeroed in wire_store (as pkt_issue)
-        }
-    }
-}
-
-template <int E, int PU, int NT, bool TAG>
-__device__ __forceinline__ void wire_store(const EncArgs &a, const KeySched &ks, const Lane1 &L, uint32_t *stage,
-                                           uint32_t sum_pre, int32_t wst, uint32_t lane, uint64_t bm,
-                                           const uint4 (&A)[PU][2], const uint4 (&pc)[2]) {
-    using G = WireGeom<E>;
-    uint32_t js[PU], myj;
-    bool on[PU], mine;
-    batch_slots<PU>(bm, lane, js, on, myj, mine);
-    uint32_t dsum = 0;  // TAG: lane p, checksum share of the bytes it adds to packet p's prefix image
-    if constexpr (TAG) {
-        const uint64_t po = shfl64(L.po, myj);
-        const uint32_t wl = (uint32_t)__shfl((int)wst, (int)myj);  // with every lane active (bpermute)
-        const uint32_t P = mine ? wl - G::HB : 0u;
-        const uint32_t r = (uint32_t)((reinterpret_cast<uintptr_t>(a.payload) + po) & 15u);
-        const uint4 f = rsk::funnel16(pc[0], pc[1], r);
-        uint32_t pw[4] = {f.x, f.y, f.z, f.w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int k = (int)P - 4 * q;
-            pw[q] &= k >= 4 ? 0xffffffffu : (k <= 0 ? 0u : ((1u << (8 * k)) - 1u));
-        }
-        uint32_t t0, t1;
-        tag_of(ks, pw[0] & 0xffu, t0, t1);
-        uint32_t D[G::NPW];
-#pragma unroll
-        for (int q = 0; q < G::NPW; ++q) D[q] = 0;
-        put_bytes(D, G::HL, t0, 4);
-        put_bytes(D, G::HL + 4, t1, 4);
-        wire_put_prefix<E>(D, pw);  // payload bytes from wire offset HB (frame byte 31 = payload[0])
-        if (mine && P) {
-#pragma unroll
-            for (int q = G::HL / 4; q < G::NPW; ++q) {
-                stage[myj * G::NPW + q] |= D[q];
-                dsum += hsum(D[q]);
-            }
-        }
-        wave_lds_sync();
-    }
-    uint32_t ck[PU];
-#pragma unroll
-    for (int p = 0; p < PU; ++p) {
-        const uint32_t wlen = on[p] ? (uint32_t)rdl((uint32_t)wst, js[p]) : 0u;
-        uint8_t *dst = a.frame + rdl64(L.fo, js[p]);
-        const uint32_t shp = (uint32_t)((reinterpret_cast<uintptr_t>(a.payload + rdl64(L.po, js[p])) + G::D0) & 15u);
-        const int32_t last_rel = (int32_t)(wlen - G::HB) - 1 - G::D0 + (int32_t)shp;
-        uint4 Ap[2];  // the issued loads, dead lanes zeroed (after the wait: see pkt_issue)
-#pragma unroll
-        for (int q = 0; q < 2; ++q)
-            Ap[q] = on[p] && (int32_t)(16u * (lane + 64u * q)) <= last_rel ? A[p][q] : make_uint4(0u, 0u, 0u, 0u);
-        uint4 B[2];
-        B[0] = make_uint4(wave_shl1(Ap[0].x), wave_shl1(Ap[0].y), wave_shl1(Ap[0].z), wave_shl1(Ap[0].w));
-        B[1] = make_uint4(wave_shl1(Ap[1].x), wave_shl1(Ap[1].y), wave_shl1(Ap[1].z), wave_shl1(Ap[1].w));
-        const uint4 l0 = make_uint4(rdl(Ap[1].x, 0), rdl(Ap[1].y, 0), rdl(Ap[1].z, 0),
-                                    rdl(Ap[1].w, 0));  // read in uniform flow (see k_encode)
-        if (lane == 63u) B[0] = l0;
-        const uint32_t nch = (wlen + 15u) >> 4;
-        const uint32_t nst = on[p] ? (padded_len(dst, wlen, a.pad) + 15u) >> 4 : 0u;
-        uint32_t part = 0;
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const uint32_t k = G::NPRE + lane + 64u * q;
-            uint4 v = rsk::funnel16(Ap[q], B[q], shp);
-            const int lim = (int)wlen - 16 * (int)k;
-            if (k < nch) {
-                if (lim < 16) v = rsk::keep_bytes16(v, lim);
-                part = hsum4(v, part);
-            }
-            if (k < nst) store_last16<NT>(dst + 16u * k, v, lim, a.pad != 0u);
-        }
-        ck[p] = part;
-    }
-#pragma unroll
-    for (int p = 0; p < PU; ++p)
-        ck[p] = ~fold16(wave_sum(ck[p]) + rdl(sum_pre, js[p]) + (TAG ? rdl(dsum, (uint32_t)p) : 0u)) & 0xffffu;
-#pragma unroll
-    for (int p = 0; p < PU; ++p) {
-        if (!on[p]) continue;
-        const uint32_t wlen = (uint32_t)rdl((uint32_t)wst, js[p]);
-        uint8_t *dst = a.frame + rdl64(L.fo, js[p]);
-        const uint32_t nst = (padded_len(dst, wlen, a.pad) + 15u) >> 4;
-        if (lane < (uint32_t)G::NPRE && lane < nst) {
-            const uint4 sv = *reinterpret_cast<const uint4 *>(stage + js[p] * G::NPW + 4u * lane);
-            uint32_t w4[4] = {sv.x, sv.y, sv.z, sv.w};
-            if (lane == (uint32_t)(G::CK / 16)) w4[(G::CK & 15) >> 2] |= ck[p] << (8 * (G::CK & 3));
-            store_last16<NT>(dst + 16u * lane, make_uint4(w4[0], w4[1], w4[2], w4[3]), (int)wlen - 16 * (int)lane,
-                             a.pad != 0u);
-        }
-    }
-}
-
-template <int E, int PU, int NT, bool TAG>
-__device__ __forceinline__ void copy_wire_pkt_pipe(const EncArgs &a, const KeySched &ks, const Lane1 &L,
-                                                   uint32_t *stage, uint32_t sum_pre, int32_t wst, uint32_t lane,
-                                                   uint64_t vm) {
-    uint4 A0[PU][2], A1[PU][2], p0[2], p1[2];
-    uint64_t cur = take_batch<PU>(vm);
-    if (!cur) return;
-    wire_issue<E, PU, TAG>(a, L, wst, lane, cur, A0, p0);
-    while (true) {
-        const uint64_t nxt = take_batch<PU>(vm);
-        if (nxt) wire_issue<E, PU, TAG>(a, L, wst, lane, nxt, A1, p1);
-        wire_store<E, PU, NT, TAG>(a, ks, L, stage, sum_pre, wst, lane, cur, A0, p0);
-        if (!nxt) break;
-        cur = take_batch<PU>(vm);
-        if (cur) wire_issue<E, PU, TAG>(a, L, wst, lane, cur, A0, p0);
-        wire_store<E, PU, NT, TAG>(a, ks, L, stage, sum_pre, wst, lane, nxt, A1, p1);
-        if (!cur) break;
     }
 }
 
@@ -1718,65 +1496,21 @@ __device__ __forceinline__ void copy_wire_flat_any(const EncArgs &a, const Lane1
     }
 }
 
-// ---- wire packets that are not 16-B aligned, A/B modes 0-3 only: byte path (prefix bytes from the
-// lane image)
-template <int E>
-__device__ __forceinline__ void copy_wire_bytes(const EncArgs &a, const Lane1 &L, const uint32_t *stage,
-                                                uint32_t sum_pre, int32_t wst, uint32_t lane, uint64_t sm) {
-    using G = WireGeom<E>;
-    while (sm) {
-        const uint32_t j = (uint32_t)__builtin_ctzll(sm);
-        sm &= sm - 1ull;
-        const uint32_t wl = rdl((uint32_t)wst, j);
-        const uint8_t *pay = a.payload + rdl64(L.po, j);
-        uint8_t *dst = a.frame + rdl64(L.fo, j);
-        uint32_t Wj[G::NPW];
-#pragma unroll
-        for (int t = 0; t < G::NPW; ++t) Wj[t] = stage[j * G::NPW + t];  // uniform LDS reads
-        // checksum: prefix part from the packet lane, payload bytes past the prefix summed here
-        uint32_t s = 0;
-        for (uint32_t f = 16u * G::NPRE + lane; f < wl; f += 64u) {
-            const uint32_t byte = rsk::gptr(pay)[f - G::HB];
-            s += byte << (8u * ((f - (E + 20)) & 1u));
-        }
-        s = fold16(s);
-#pragma unroll
-        for (int off = 32; off; off >>= 1) s += __shfl_xor(s, off);
-        const uint32_t ck = ~fold16(s + rdl(sum_pre, j)) & 0xffffu;
-        const uint32_t fend = padded_len(dst, wl, a.pad);
-        for (uint32_t f = lane; f < fend; f += 64u) {
-            uint32_t byte = 0;
-            if (f >= wl) {
-                byte = 0;
-            } else if (f < 16u * G::NPRE) {
-                uint32_t wv = 0;
-#pragma unroll
-                for (int q = 0; q < G::NPW; ++q)
-                    if ((f >> 2) == (uint32_t)q) wv = Wj[q];
-                byte = (wv >> (8u * (f & 3u))) & 0xffu;
-                if (f == (uint32_t)G::CK) byte = ck & 0xffu;
-                if (f == (uint32_t)G::CK + 1u) byte = ck >> 8;
-            } else {
-                byte = rsk::gptr(pay)[f - G::HB];
-            }
-            rsk::gptr(dst)[f] = (uint8_t)byte;
-        }
-    }
-}
-
-// MODE: 0 per-packet, 1 flat, 2 hybrid (per-wave choice on the set's mean wire length, one launch),
-// 3 / 4 = the per-packet / flat halves of the two-launch hybrid: each wave re-derives the same
-// choice from pay_len and frame_off alone and returns unless it is its launch's path, so every set
-// is handled exactly once and each launch sizes LDS (hence occupancy) for its own path only;
-// 5 = 3 with the tag and payload prefix deferred into the copy loop for sets of long frames.
+// The per-set wire build: two launches over the same grid (k_encode's grouped-interleave mapping:
+// 8-packet groups across 1024-wave super-blocks, grid by enc_grid).  Each wave derives the set's copy
+// path from pay_len alone -- the flat chunk list below a set-mean wire length of kFlatBelowMeanBytes,
+// else the per-packet DPP copy -- and returns unless it is its launch's path, so every set is handled
+// exactly once and each launch sizes LDS (hence occupancy) for its own path only (one launch holding
+// both: C3 2.75 vs 2.52 ms).  MODE 5: the per-packet half (PU packets per iteration), with the tag and
+// payload prefix deferred into the copy loop for sets of long frames; MODE 4: the flat half.
 template <int E, int MODE>
 struct WireLds {
     static constexpr int kStage = 64 * WireGeom<E>::NPW * 4;  // prefix images (both paths)
-    static constexpr bool kFlat = MODE == 1 || MODE == 2 || MODE == 4;
+    static constexpr bool kFlat = MODE == 4;
     static constexpr int kBytes = kStage + (kFlat ? 64 * (int)sizeof(CopyRec) + 2 * 64 * 4 : 0);
 };
 
-// Per-wave copy-path choice (identical in both launches of the split hybrid).
+// Per-wave copy-path choice (identical in both launches).
 template <int E>
 __device__ __forceinline__ bool wire_flat_choice(bool vec, uint32_t wlen) {
     uint32_t fl = vec ? wlen : 0u;
@@ -1785,33 +1519,32 @@ __device__ __forceinline__ bool wire_flat_choice(bool vec, uint32_t wlen) {
     return fl < kFlatBelowMeanBytes * (uint32_t)__popcll(__ballot(vec));
 }
 
-// GI: k_encode's grouped-interleave mapping (8-packet groups across 1024-wave super-blocks, grid by
-// enc_grid); otherwise the tiled mapping (A/B build: wire variant 10).
-template <int E, int MODE, int PU, int U, bool GI>
+template <int E, int MODE, int PU, int U>
 __device__ __forceinline__ void encode_wire_set(const EncArgs &a, const WireArgs &wa, const KeySched &ks) {
+    static_assert(MODE == 4 || MODE == 5, "the flat half and the per-packet half");
     using G = WireGeom<E>;
     __shared__ uint4 lds[kWavesPerBlock][WireLds<E, MODE>::kBytes / 16];
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     const uint64_t wg = (uint64_t)blockIdx.x * kWavesPerBlock + w;
-    constexpr uint32_t kGrp = GI ? 8u : 64u;
+    constexpr uint32_t kGrp = 8u;
     const uint64_t sb = wg / 1024u, wl = wg % 1024u;
-    const uint64_t first = GI ? sb * 65536u + wl * 8u : wg * 64u;
+    const uint64_t first = sb * 65536u + wl * 8u;
     if (first >= a.n) return;  // wave-uniform; no block barriers below
-    const uint64_t gi = GI ? sb * 65536u + ((uint64_t)(lane / 8u) * 1024u + wl) * 8u + lane % 8u : first + lane;
+    const uint64_t gi = sb * 65536u + ((uint64_t)(lane / 8u) * 1024u + wl) * 8u + lane % 8u;
     const uint64_t i = gi < a.n ? gi : a.n;
-    if constexpr (MODE >= 3) {  // split hybrid: is this set ours?
+    {  // is this set ours?
         bool v0 = false;
-        uint32_t wl = 0;
+        uint32_t wlen = 0;
         if (i < a.n) {
             const uint32_t P = a.pay_len[i];
-            v0 = P != 0u && P <= (uint32_t)RSK_MAX_PAYLOAD;  // any alignment (round 2: the DPP copy takes all)
-            wl = G::HL + RSK_HEAD_SIZE + P;
+            v0 = P != 0u && P <= (uint32_t)RSK_MAX_PAYLOAD;  // any alignment: both copies take all
+            wlen = G::HL + RSK_HEAD_SIZE + P;
         }
-        if (wire_flat_choice<E>(v0, wl) != (MODE == 4)) return;
+        if (wire_flat_choice<E>(v0, wlen) != (MODE == 4)) return;
     }
     Lane1 L = encode_phase1<MODE != 5>(a, ks, i);
     bool defer = false;
-    if constexpr (MODE == 5) {  // as k_encode MODE 6: set mean frame length decides
+    if constexpr (MODE == 5) {  // the set mean frame length decides (as k_encode)
         const bool v = L.st > 0;
         uint32_t fl = v ? (uint32_t)L.st : 0u;
 #pragma unroll
@@ -1822,87 +1555,56 @@ __device__ __forceinline__ void encode_wire_set(const EncArgs &a, const WireArgs
     uint32_t PW[G::NPW];
     uint32_t sum_pre;
     int32_t wst;
-    // the DPP per-packet copy (PU 100..199) writes wire packets at any alignment, and so does the
-    // flat half (MODE 4, copy_wire_flat_any); the A/B modes leave unaligned ones to the byte path
-    constexpr bool kAnyAlign = PU >= 100 && PU < 200;
-    wire_phase1<E>(a, wa, L, i, PW, sum_pre, wst, !defer || (L.slow && !kAnyAlign));
-    const bool vec = L.st > 0 && (kAnyAlign || !L.slow);
+    wire_phase1<E>(a, wa, L, i, PW, sum_pre, wst, !defer);
+    const bool vec = L.st > 0;  // every framed packet takes a vector path, at any alignment
     const uint64_t vm = __ballot(vec);
-    bool flat = MODE == 1 || MODE == 4;
-    if constexpr (MODE == 2) flat = wire_flat_choice<E>(vec, (uint32_t)wst);
     uint8_t *slice = reinterpret_cast<uint8_t *>(lds[w]);
     uint32_t *stage = reinterpret_cast<uint32_t *>(slice);
-    if (L.st > 0) {  // every framed packet's prefix image (vector and byte paths read it from here)
+    if (L.st > 0) {  // every framed packet's prefix image
 #pragma unroll
         for (int c = 0; c < G::NPRE; ++c)
             *reinterpret_cast<uint4 *>(stage + lane * G::NPW + 4 * c) =
                 make_uint4(PW[4 * c], PW[4 * c + 1], PW[4 * c + 2], PW[4 * c + 3]);
     }
-    if constexpr (WireLds<E, MODE>::kFlat) {
-        if (flat) {
-            CopyRec *recs = reinterpret_cast<CopyRec *>(slice + WireLds<E, MODE>::kStage);
-            uint32_t *cend = reinterpret_cast<uint32_t *>(slice + WireLds<E, MODE>::kStage + 64 * sizeof(CopyRec));
-            if (MODE == 4 && __ballot(L.st > 0 && L.slow) != 0ull)  // an unaligned packet: any-alignment list
-                copy_wire_flat_any<E, U>(a, L, stage, sum_pre, wst, lane, L.st > 0, recs, cend, cend + 64);
-            else
-                copy_wire_flat<E, U>(a, L, stage, sum_pre, wst, lane, vec, recs, cend, cend + 64);
-        }
-    }
-    if (!flat) {
+    if constexpr (MODE == 4) {
+        CopyRec *recs = reinterpret_cast<CopyRec *>(slice + WireLds<E, MODE>::kStage);
+        uint32_t *cend = reinterpret_cast<uint32_t *>(slice + WireLds<E, MODE>::kStage + 64 * sizeof(CopyRec));
+        if (__ballot(L.st > 0 && L.slow) != 0ull)  // an unaligned packet: the any-alignment list
+            copy_wire_flat_any<E, U>(a, L, stage, sum_pre, wst, lane, L.st > 0, recs, cend, cend + 64);
+        else
+            copy_wire_flat<E, U>(a, L, stage, sum_pre, wst, lane, vec, recs, cend, cend + 64);
+    } else {
         wave_lds_sync();
-        if constexpr (PU >= 200) {  // software-pipelined DPP copy, PU - 200 packets per batch
-            const uint32_t wend = vec ? padded_len(a.frame + L.fo, (uint32_t)wst, a.pad) : 0u;
-            const uint64_t end = L.fo + wend;
-            const uint64_t nfo = (uint64_t)(uint32_t)__shfl_down((int)(uint32_t)L.fo, 1) |
-                                 ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(L.fo >> 32), 1) << 32);
-            const bool nvec = __shfl_down((int)vec, 1) != 0;
-            const bool gaps = __ballot(vec && nvec && lane % kGrp != kGrp - 1u && end != nfo) != 0ull;
-            if (MODE == 5 && defer) {
-                if (gaps) copy_wire_pkt_pipe<E, PU - 200, 2, true>(a, ks, L, stage, sum_pre, wst, lane, vm);
-                else copy_wire_pkt_pipe<E, PU - 200, 0, true>(a, ks, L, stage, sum_pre, wst, lane, vm);
-            } else {
-                if (gaps) copy_wire_pkt_pipe<E, PU - 200, 2, false>(a, ks, L, stage, sum_pre, wst, lane, vm);
-                else copy_wire_pkt_pipe<E, PU - 200, 0, false>(a, ks, L, stage, sum_pre, wst, lane, vm);
-            }
-        } else if constexpr (PU >= 100) {
-            // store policy per set, as k_encode: stream the stores when the wire packets leave gaps
-            const uint32_t wend = vec ? padded_len(a.frame + L.fo, (uint32_t)wst, a.pad) : 0u;
-            const uint64_t end = L.fo + wend;
-            const uint64_t nfo = (uint64_t)(uint32_t)__shfl_down((int)(uint32_t)L.fo, 1) |
-                                 ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(L.fo >> 32), 1) << 32);
-            const bool nvec = __shfl_down((int)vec, 1) != 0;
-            const bool gaps = __ballot(vec && nvec && lane % kGrp != kGrp - 1u && end != nfo) != 0ull;
-            if (MODE == 5 && defer) {
-                if (gaps) copy_wire_pkt_dpp<E, PU - 100, 2, true>(a, ks, L, stage, sum_pre, wst, lane, vm);
-                else copy_wire_pkt_dpp<E, PU - 100, 0, true>(a, ks, L, stage, sum_pre, wst, lane, vm);
-            } else {
-                if (gaps) copy_wire_pkt_dpp<E, PU - 100, 2>(a, ks, L, stage, sum_pre, wst, lane, vm);
-                else copy_wire_pkt_dpp<E, PU - 100, 0>(a, ks, L, stage, sum_pre, wst, lane, vm);
-            }
+        // store policy per set, as k_encode: stream the stores when the wire packets leave gaps
+        const uint32_t wend = vec ? padded_len(a.frame + L.fo, (uint32_t)wst, a.pad) : 0u;
+        const uint64_t end = L.fo + wend;
+        const uint64_t nfo = (uint64_t)(uint32_t)__shfl_down((int)(uint32_t)L.fo, 1) |
+                             ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(L.fo >> 32), 1) << 32);
+        const bool nvec = __shfl_down((int)vec, 1) != 0;
+        const bool gaps = __ballot(vec && nvec && lane % kGrp != kGrp - 1u && end != nfo) != 0ull;
+        if (defer) {
+            if (gaps) copy_wire_pkt_dpp<E, PU, 2, true>(a, ks, L, stage, sum_pre, wst, lane, vm);
+            else copy_wire_pkt_dpp<E, PU, 0, true>(a, ks, L, stage, sum_pre, wst, lane, vm);
+        } else {
+            if (gaps) copy_wire_pkt_dpp<E, PU, 2>(a, ks, L, stage, sum_pre, wst, lane, vm);
+            else copy_wire_pkt_dpp<E, PU, 0>(a, ks, L, stage, sum_pre, wst, lane, vm);
         }
-        else copy_wire_pkt<E, PU>(a, L, stage, sum_pre, wst, lane, vm);
-    }
-    // (the flat half sends a set with an unaligned packet through copy_wire_flat_any)
-    const uint64_t sm = __ballot(L.st > 0 && L.slow && !kAnyAlign && !(MODE == 4 && flat));
-    if (sm) {
-        wave_lds_sync();
-        copy_wire_bytes<E>(a, L, stage, sum_pre, wst, lane, sm);
     }
 }
 
-template <int E, int MODE, int PU, int U, bool GI = true>
+template <int E, int MODE, int PU, int U>
 __global__ __launch_bounds__(kBlock) void k_encode_wire(EncArgs a, WireArgs wa, KeySched ks) {
     stage_tags(ks);
-    encode_wire_set<E, MODE, PU, U, GI>(a, wa, ks);
+    encode_wire_set<E, MODE, PU, U>(a, wa, ks);
 }
 
 // The same held to 4 waves per SIMD (<= 128 VGPRs): the deferred-tag build (MODE 5) needs 131 and
 // would otherwise drop to 3, which costs the sets that keep the tag in phase 1 (C4 +9 %).
-template <int E, int MODE, int PU, int U, bool GI = true>
+template <int E, int MODE, int PU, int U>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_encode_wire_w4(
     EncArgs a, WireArgs wa, KeySched ks) {
     stage_tags(ks);
-    encode_wire_set<E, MODE, PU, U, GI>(a, wa, ks);
+    encode_wire_set<E, MODE, PU, U>(a, wa, ks);
 }
 
 // ---- the two-pass wire build (round 6): a header pass, one lane per packet (MD5
@@ -3428,8 +3130,8 @@ int rsk_encode_wire_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const
 #define RSK_WIRE4(E, M, PU, U) hipLaunchKernelGGL((k_encode_wire_w4<E, M, PU, U>), dim3(grid), dim3(kBlock), 0, st, a, w, c->ks)
     // the per-set kernels: per-packet half (DPP copy, 8 packets per iteration, tag + payload prefix in
     // the copy loop for long-frame sets, 4 waves/SIMD) then the flat half
-    if (eth14) { RSK_WIRE4(14, 5, 108, 2); RSK_WIRE(14, 4, 2, 2); }
-    else { RSK_WIRE4(0, 5, 108, 2); RSK_WIRE(0, 4, 2, 2); }
+    if (eth14) { RSK_WIRE4(14, 5, 8, 2); RSK_WIRE(14, 4, 2, 2); }
+    else { RSK_WIRE4(0, 5, 8, 2); RSK_WIRE(0, 4, 2, 2); }
 #undef RSK_WIRE
 #undef RSK_WIRE4
     c->enc_last_path.store(RSK_ENC_PATH_PER_SET, std::memory_order_relaxed);
