@@ -159,8 +159,8 @@ int rsk_set_encode_path(rsk_ctx *ctx, int path);
  * kernels read is the immutable key schedule and tag table (and the tag mode, passed by value).
  *
  * Pre-size the scratch of `stream` (rsk_reserve: the legacy default stream, NULL) for batches of up
- * to n packets: the compaction state and, for n >= 16384, the 32-B-per-packet header records of the
- * two-pass encode -- only for a context that encodes: one held to RSK_ENC_PATH_TWO_PASS, or an AUTO
+ * to n packets: the compaction state and, for n >= 16384, the header records of the two-pass encode
+ * and wire build (max(32 n, 96 min(n, 2^20)) bytes) -- only for a context that encodes: one held to RSK_ENC_PATH_TWO_PASS, or an AUTO
  * context that has already run an rsk_encode_batch call (so a decode- or demux-only context pays
  * nothing for them; a failed records allocation is not an error: eager calls allocate them on demand,
  * a captured call then takes the per-set kernel).  Batch calls grow the scratch on demand, which waits
@@ -265,7 +265,14 @@ int rsk_encode_batch(rsk_ctx *ctx, uint32_t n, const rsk_encode_in *in, const rs
  * frame length status[i] - 40 - (with_eth ? 14 : 0).  seq and ip_id are the caller's per-packet
  * values: the reference advances them per send (FakeTcp::Output: seq += 31 + nread, FakeTcp.cpp:43-49;
  * RawTcp::Output: mIpId++, RawTcp.cpp:118-120), so one connection's batch carries
- * seq[i] = seq0 + sum_{k<i} (31 + P_k) and ip_id[i] = id0 + i. */
+ * seq[i] = seq0 + sum_{k<i} (31 + P_k) and ip_id[i] = id0 + i.
+ * Two device paths, identical bytes: the per-set wire kernels (a flat half and a per-packet half),
+ * and (round 6) the two-pass form -- a header pass writing each packet's header image (80 / 96 B,
+ * RAW4 / Ethernet) into the stream's scratch, then copy waves of 4 / 2 / 1 packets that sum the
+ * payload into the TCP checksum -- run per chunk of 2^20 packets.  The path follows the context's
+ * rsk_set_encode_path (TWO_PASS: the two-pass form; any other forced path: the per-set kernels) or,
+ * under AUTO, the sampled mean payload: per-set below 160 B and for Ethernet packets from 1300 B, the
+ * two-pass form otherwise, 4 packets per copy wave, RAW4 from 1080 B 2. */
 typedef struct rsk_wire_in {
     const uint32_t *src, *dst; /* [n] TcpInfo::src / dst: IPv4 addresses as stored (network order) */
     const uint16_t *sp, *dp;   /* [n] ports, host order                                           */

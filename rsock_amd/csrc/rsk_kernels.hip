@@ -2905,7 +2905,9 @@ int rsk_reserve_stream(rsk_ctx *c, uint32_t n_max, void *stream) {
     // A failed allocation is not an error: eager calls allocate on demand, a captured call
     // takes the per-set kernel.
     void *p = nullptr;
-    if (rsk::stream_ws(c, (hipStream_t)stream, rsk::WS_ENC, 32ull * n_max, &p) != RSK_OK) {
+    // (and the two-pass wire build's: 96 B per packet of one 2^20-packet chunk, k_wire_heads)
+    const uint64_t wire_rec = 96ull * std::min<uint64_t>(n_max, 1ull << 20);
+    if (rsk::stream_ws(c, (hipStream_t)stream, rsk::WS_ENC, std::max<uint64_t>(32ull * n_max, wire_rec), &p) != RSK_OK) {
         (void)hipGetLastError();
         g_last_error[0] = 0;
     }
