@@ -427,14 +427,23 @@ int rsk_tcp_recv_ack_batch(rsk_ctx *ctx, uint32_t n, const uint32_t *conn, const
  *   - with RSK_DEMUX_CMD_BARRIER, a packet whose cmd != RSK_CMD_DATA (RST / keepalive, handled by
  *     IAppGroup outside the conn maps) is a segment of its own and an ordering barrier: DATA
  *     packets on either side of it never share a segment;
+ *   - with RSK_DEMUX_GROUP_BARRIER instead (requires RSK_DEMUX_ID, excludes CMD_BARRIER), a control
+ *     packet is a segment of its own and a barrier for the packets of its own IdBuf only: DATA
+ *     packets of one IdBuf on either side of it never share a segment, packets of other IdBufs
+ *     are not split by it.  That is the server's routing: ServerGroup::OnRecv (server/
+ *     ServerGroup.cpp:44-60) hands each packet to its IdBuf's SubGroup, whose conns and control
+ *     handling never see another IdBuf's packets, so only the order inside one IdBuf is
+ *     observable.  A server batch then has about one segment per conn and epoch of its own group
+ *     instead of one per conn and epoch of the whole batch;
  *   - segments are ordered by their first packet, packets inside a segment by arrival.
  * Delivering segment by segment therefore hands every conn the same packet sequence as the
  * reference's per-packet loop, and creates new conns in the same order (first occurrence). */
-#define RSK_DEMUX_ID          0x01u /* EncHead IdBuf (8 B)                                        */
-#define RSK_DEMUX_CONN_KEY    0x02u /* EncHead connKey                                            */
-#define RSK_DEMUX_CONV        0x04u /* EncHead conv                                               */
-#define RSK_DEMUX_DST         0x08u /* TcpInfo dst (SubGroup keys on BuildConvKey(dst, conv))     */
-#define RSK_DEMUX_CMD_BARRIER 0x10u
+#define RSK_DEMUX_ID            0x01u /* EncHead IdBuf (8 B)                                      */
+#define RSK_DEMUX_CONN_KEY      0x02u /* EncHead connKey                                          */
+#define RSK_DEMUX_CONV          0x04u /* EncHead conv                                             */
+#define RSK_DEMUX_DST           0x08u /* TcpInfo dst (SubGroup keys on BuildConvKey(dst, conv))   */
+#define RSK_DEMUX_CMD_BARRIER   0x10u
+#define RSK_DEMUX_GROUP_BARRIER 0x20u
 typedef struct rsk_demux_in {
     const int8_t *status;      /* [n] packet i takes part iff status[i] == RSK_RECV_VALID       */
     const uint8_t *cmd;        /* [n]                                                           */
@@ -450,7 +459,9 @@ typedef struct rsk_demux_out {
     uint32_t *n_seg;     /* [1]                                                                   */
     uint32_t *n_valid;   /* [1]                                                                   */
 } rsk_demux_out;
-/* n <= 2^30.  Workspace (per context, grown on demand): about 70 B per packet. */
+/* n <= 2^30.  Workspace (per context, grown on demand): about 70 B per packet.  GROUP_BARRIER runs
+ * two group-bys (by IdBuf, then by the key with each DATA packet's epoch inside its IdBuf), writing
+ * the first one's result to `out` before the second overwrites it. */
 int rsk_demux_batch(rsk_ctx *ctx, uint32_t n, const rsk_demux_in *in, uint32_t fields,
                     const rsk_demux_out *out, void *stream);
 

@@ -664,19 +664,41 @@ int orc_demux_batch(uint32_t n, const int8_t *status, const uint8_t *cmd, const 
         return -12;
     }
     const int barrier = (fields & RSK_DEMUX_CMD_BARRIER) != 0;
+    const int gbarrier = (fields & RSK_DEMUX_GROUP_BARRIER) != 0;
+    /* GROUP_BARRIER: the epoch of a DATA packet counts the control packets of its own IdBuf before
+       it (per-IdBuf counters in a second table, `epoch` = the count, `key` = the IdBuf) */
+    orc_dkey *gtab = gbarrier ? (orc_dkey *)calloc(cap, sizeof(orc_dkey)) : NULL;
+    if (gbarrier && !gtab) {
+        free(tab); free(seg_of); free(cnt);
+        return -12;
+    }
     uint32_t epoch = 0, S = 0, nv = 0;
     for (uint32_t i = 0; i < n; i++) {
         if (status[i] != RSK_RECV_VALID) continue;
         nv++;
-        if (barrier && cmd[i] != RSK_CMD_DATA) {  /* singleton segment, then a new epoch */
+        orc_dkey *grp = NULL;
+        if (gbarrier) {
+            uint64_t gid;
+            memcpy(&gid, id + 8ull * i, 8);
+            orc_dkey gk;
+            memset(&gk, 0, sizeof gk);
+            gk.id = gid;
+            uint64_t h = orc_dkey_hash(&gk) & (cap - 1);
+            while (gtab[h].used && gtab[h].id != gid) h = (h + 1) & (cap - 1);
+            grp = &gtab[h];
+            grp->used = 1;
+            grp->id = gid;
+        }
+        if ((barrier || gbarrier) && cmd[i] != RSK_CMD_DATA) {  /* singleton segment, then a new epoch */
             seg_first[S] = i;
             seg_of[i] = S++;
-            epoch++;
+            if (grp) grp->epoch++;
+            else epoch++;
             continue;
         }
         orc_dkey k;
         memset(&k, 0, sizeof k);
-        k.epoch = epoch;
+        k.epoch = grp ? grp->epoch : epoch;
         if (fields & RSK_DEMUX_ID) memcpy(&k.id, id + 8ull * i, 8);
         if (fields & RSK_DEMUX_CONN_KEY) k.key = conn_key[i];
         if (fields & RSK_DEMUX_CONV) k.conv = conv[i];
@@ -711,7 +733,7 @@ int orc_demux_batch(uint32_t n, const int8_t *status, const uint8_t *cmd, const 
         if (status[i] == RSK_RECV_VALID) perm[cnt[seg_of[i]]++] = i;
     *n_seg = S;
     *n_valid = nv;
-    free(tab); free(seg_of); free(cnt);
+    free(tab); free(gtab); free(seg_of); free(cnt);
     return 0;
 }
 

@@ -97,8 +97,10 @@ uint16_t orc_inet_csum(const uint8_t *p, size_t n, uint32_t init);
  * per-packet conn lookups (INetGroup.cpp:57-83 by connKey, IAppGroup.cpp:76-96 by cmd,
  * ServerGroup.cpp:44-60 by IdBuf, SubGroup.cpp:31-50 by (dst, conv), ClientGroup.cpp:66-80 by conv)
  * restated as a sequential walk: each VALID packet looks its key up in a map (new key -> next
- * segment id), control packets (cmd != 0) under RSK_DEMUX_CMD_BARRIER open a new epoch.  Pointers
- * for unselected fields may be NULL.  Returns 0, or -12 on allocation failure. */
+ * segment id), control packets (cmd != 0) under RSK_DEMUX_CMD_BARRIER open a new epoch, under
+ * RSK_DEMUX_GROUP_BARRIER a new epoch of their own IdBuf only (ServerGroup.cpp:44-60 hands a packet
+ * to its IdBuf's SubGroup alone).  Pointers for unselected fields may be NULL.  Returns 0, or -12 on
+ * allocation failure. */
 int orc_demux_batch(uint32_t n, const int8_t *status, const uint8_t *cmd, const uint8_t *id,
                     const uint32_t *conv, const uint64_t *conn_key, const uint32_t *dst,
                     uint32_t fields, uint32_t *perm, uint32_t *seg_off, uint32_t *seg_first,

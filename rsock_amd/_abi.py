@@ -38,6 +38,7 @@ FILTER_MAX_PORTS = 64
 TAG_MD5, TAG_TABLE = 0, 1
 DEVERR_LOOKBACK = 0x1
 DEMUX_ID, DEMUX_CONN_KEY, DEMUX_CONV, DEMUX_DST, DEMUX_CMD_BARRIER = 0x01, 0x02, 0x04, 0x08, 0x10
+DEMUX_GROUP_BARRIER = 0x20
 
 _vp = ctypes.c_void_p
 _u8p = ctypes.c_void_p  # all arrays passed as raw addresses

@@ -143,6 +143,7 @@ struct DmIn {
     const uint32_t *dst;
     uint32_t *pep;   // with CMD_BARRIER: epoch of each VALID data packet, by packet index (else null: 0)
     uint32_t *cpos;  // with CMD_BARRIER: packet index of the c-th VALID control packet; cpos[n_ctrl] = n
+    const uint32_t *xep;  // second pass of GROUP_BARRIER: a key word per packet (else null: 0)
     uint32_t n, fields;
 };
 
@@ -239,7 +240,7 @@ __device__ uint32_t dlb_digit(unsigned long long *st, uint32_t t, uint32_t d, ui
 }
 
 struct Key {
-    uint32_t ep, conv, dst;
+    uint32_t ep, conv, dst, xf;
     uint64_t id, ck;
 };
 
@@ -250,13 +251,14 @@ __device__ __forceinline__ Key load_key(const DmIn &a, uint32_t i, uint32_t ep) 
     k.ck = (a.fields & RSK_DEMUX_CONN_KEY) ? a.key[i] : 0ull;
     k.conv = (a.fields & RSK_DEMUX_CONV) ? a.conv[i] : 0u;
     k.dst = (a.fields & RSK_DEMUX_DST) ? a.dst[i] : 0u;
+    k.xf = a.xep ? a.xep[i] : 0u;
     return k;
 }
 __device__ __forceinline__ bool key_eq(const Key &x, const Key &y) {
-    return x.ep == y.ep && x.id == y.id && x.ck == y.ck && x.conv == y.conv && x.dst == y.dst;
+    return x.ep == y.ep && x.xf == y.xf && x.id == y.id && x.ck == y.ck && x.conv == y.conv && x.dst == y.dst;
 }
 __device__ __forceinline__ uint64_t key_hash(const Key &k) {
-    uint64_t h = (uint64_t)k.ep * 0x9E3779B97F4A7C15ull ^ k.id * 0xC2B2AE3D27D4EB4Full ^
+    uint64_t h = ((uint64_t)k.ep | (uint64_t)k.xf << 32) * 0x9E3779B97F4A7C15ull ^ k.id * 0xC2B2AE3D27D4EB4Full ^
                  k.ck * 0x165667B19E3779F9ull ^ ((uint64_t)k.conv | (uint64_t)k.dst << 32) * 0xD6E8FEB86659FD93ull;
     h ^= h >> 31;
     h *= 0xBF58476D1CE4E5B9ull;
@@ -347,7 +349,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_insert(DmIn a, const uint32_t *nv
     }
 #pragma unroll
     for (uint32_t it = 0; it < kInsItems; ++it)
-        kr[it] = pkr[it] == kNone ? Key{kCtrl, 0, 0, 0, 0} : load_key(a, pkr[it], a.pep ? a.pep[pkr[it]] : 0u);
+        kr[it] = pkr[it] == kNone ? Key{kCtrl, 0, 0, 0, 0, 0} : load_key(a, pkr[it], a.pep ? a.pep[pkr[it]] : 0u);
 #pragma unroll
     for (uint32_t it = 0; it < kInsItems; ++it) {
         const uint32_t li = it * kBlock + t, j = base + li;
@@ -818,7 +820,8 @@ __global__ __launch_bounds__(kBlock) void k_dm_onesweep(uint32_t pass, const uin
 __global__ __launch_bounds__(kBlock) void k_dm_final(const uint32_t *nvp, const uint32_t *nsegp, const uint32_t *kA,
                                                      const uint32_t *vA, const uint32_t *kB, const uint32_t *vB,
                                                      const uint32_t *seg_first, uint32_t *perm, uint32_t *seg_off,
-                                                     uint32_t *n_seg, uint32_t *n_valid) {
+                                                     uint32_t *n_seg, uint32_t *n_valid, const uint8_t *gcmd,
+                                                     uint32_t *gflag, uint32_t *gseg) {
     const uint32_t nv = *nvp, ns = *nsegp, nf = nv - ns;
     const uint32_t passes = n_passes(ns);  // effective passes; pass p writes B when p is even
     const bool inB = nf > kSmallF && ((passes - 1u) & 1u) == 0u;  // small: sorted in place in A
@@ -839,8 +842,18 @@ __global__ __launch_bounds__(kBlock) void k_dm_final(const uint32_t *nvp, const 
         }
         seg_off[k] = k + lo;
         perm[k + lo] = seg_first[k];
+        if (gflag) {  // GROUP_BARRIER's first pass: per position, control flag and segment id
+            gflag[k + lo] = gcmd[seg_first[k]] != RSK_CMD_DATA ? 1u : 0u;
+            gseg[k + lo] = k;
+        }
     }
-    if (k < nf) perm[keys[k] + 1u + k] = vals[k];
+    if (k < nf) {
+        perm[keys[k] + 1u + k] = vals[k];
+        if (gflag) {
+            gflag[keys[k] + 1u + k] = gcmd[vals[k]] != RSK_CMD_DATA ? 1u : 0u;
+            gseg[keys[k] + 1u + k] = keys[k];
+        }
+    }
 }
 
 // ---- workspace ------------------------------------------------------------------------------
@@ -896,13 +909,65 @@ size_t dm_layout(uint32_t n, uint8_t *base, DmWs *w) {
     return off;
 }
 
+// ---- GROUP_BARRIER: each DATA packet's epoch inside its IdBuf -------------------------------
+// After the first pass (key = IdBuf alone, no barrier) perm lists every IdBuf's packets in arrival
+// order, segment by segment, and k_dm_final wrote gflag[j] = perm[j] is a control packet and gseg[j]
+// = its segment.  An exclusive scan of gflag over perm order minus its value at the segment's start
+// counts the control packets of the same IdBuf before each packet: that count is a DATA packet's key
+// word in the second pass, and a control packet gets kLeadTag | its own index, a key no other packet
+// has (a singleton segment).
+__global__ __launch_bounds__(kBlock) void k_dm_gep(const uint32_t *nvp, const uint32_t *perm, const uint32_t *seg_off,
+                                                   const uint32_t *gflag, const uint32_t *gseg, const uint32_t *pre,
+                                                   uint32_t *xep) {
+    const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
+    if (j >= *nvp) return;
+    const uint32_t p = perm[j];
+    xep[p] = gflag[j] ? (kLeadTag | p) : pre[j] - pre[seg_off[gseg[j]]];
+}
+
+// One group-by pass over the batch (the whole rsk_demux_batch without GROUP_BARRIER); with gflag,
+// k_dm_final also writes each position's control flag and segment id (GROUP_BARRIER's first pass).
+int demux_pass(rsk_ctx *c, const DmIn &a, const DmWs &w, const rsk_demux_out *out, hipStream_t s,
+               uint32_t *gflag = nullptr, uint32_t *gseg = nullptr) {
+    const uint32_t n = a.n;
+    // one fill: the key table and every look-back state word start as all-ones
+    hipError_t e = hipMemsetAsync(w.slots, 0xff, w.fill_bytes, s);
+    if (e != hipSuccess) { rsk::set_error("hipMemsetAsync(table)", e); return RSK_EDEVICE; }
+    int r;
+    hipLaunchKernelGGL(k_dm_flags_prep, dim3(w.nt), dim3(kBlock), 0, s, a, w.st_v, w.st_c, w.cidx, w.nv,
+                       c->err_dev);
+    hipLaunchKernelGGL(k_dm_insert, dim3((n + kInsTile - 1) / kInsTile), dim3(kBlock), 0, s, a, w.nv, w.cidx,
+                       w.slots, w.tsize - 1u, w.hslot);
+    hipLaunchKernelGGL(k_dm_leader_rank, dim3(w.nt), dim3(kBlock), 0, s, w.nv, w.hslot, w.slots, w.cidx, w.st_l,
+                       w.kA, w.vA, w.rank_at, out->seg_first, w.nseg, w.ghist, c->err_dev);
+    hipLaunchKernelGGL(k_dm_segof_hist, dim3(w.nt), dim3(kBlock), 0, s, w.nv, w.nseg, w.rank_at, w.kA, w.vA,
+                       w.ghist);
+    if ((r = rsk::launch_check("k_dm_segof_hist"))) return r;
+    // passes for the largest possible segment count (n); surplus passes return at once
+    uint32_t maxbits = 1;
+    while (maxbits < 32 && (1ull << maxbits) < n) ++maxbits;
+    const uint32_t passes = (maxbits + 7) / 8;
+    for (uint32_t p = 0; p < passes; ++p) {
+        const uint32_t *kin = (p & 1u) ? w.kB : w.kA, *vin = (p & 1u) ? w.vB : w.vA;
+        uint32_t *kout = (p & 1u) ? w.kA : w.kB, *vout = (p & 1u) ? w.vA : w.vB;
+        hipLaunchKernelGGL(k_dm_onesweep, dim3(w.nt), dim3(kBlock), 0, s, p, w.nv, w.nseg, kin, vin, w.ghist, w.st_r,
+                           kout, vout, c->err_dev);
+        if ((r = rsk::launch_check("k_dm_onesweep"))) return r;
+    }
+    hipLaunchKernelGGL(k_dm_final, dim3(w.nb), dim3(kBlock), 0, s, w.nv, w.nseg, w.kA, w.vA, w.kB, w.vB,
+                       out->seg_first, out->perm, out->seg_off, out->n_seg, out->n_valid, a.cmd, gflag, gseg);
+    return rsk::launch_check("k_dm_final");
+}
+
 }  // namespace
 
 extern "C" int rsk_demux_batch(rsk_ctx *c, uint32_t n, const rsk_demux_in *in, uint32_t fields,
                                const rsk_demux_out *out, void *stream) {
     if (!c || !in || !out || !out->perm || !out->seg_off || !out->seg_first || !out->n_seg || !out->n_valid)
         return RSK_EINVAL;
-    if (fields & ~0x1fu) return RSK_EINVAL;
+    if (fields & ~0x3fu) return RSK_EINVAL;
+    const bool group = (fields & RSK_DEMUX_GROUP_BARRIER) != 0u;
+    if (group && ((fields & RSK_DEMUX_CMD_BARRIER) || !(fields & RSK_DEMUX_ID))) return RSK_EINVAL;
     if (n && (!in->status || !in->cmd)) return RSK_EINVAL;
     if (n && (fields & RSK_DEMUX_ID) && (!in->id || (reinterpret_cast<uintptr_t>(in->id) & 7u))) return RSK_EINVAL;
     if (n && (fields & RSK_DEMUX_CONN_KEY) && !in->conn_key) return RSK_EINVAL;
@@ -932,36 +997,28 @@ extern "C" int rsk_demux_batch(rsk_ctx *c, uint32_t n, const rsk_demux_in *in, u
     a.key = in->conn_key;
     a.dst = in->dst;
     a.n = n;
-    a.fields = fields;
+    a.fields = fields & ~RSK_DEMUX_GROUP_BARRIER;
     a.pep = (fields & RSK_DEMUX_CMD_BARRIER) ? w.pep : nullptr;
     a.cpos = (fields & RSK_DEMUX_CMD_BARRIER) ? w.cpos : nullptr;
-    // one fill: the key table and every look-back state word start as all-ones
-    hipError_t e = hipMemsetAsync(w.slots, 0xff, w.fill_bytes, s);
-    if (e != hipSuccess) { rsk::set_error("hipMemsetAsync(table)", e); return RSK_EDEVICE; }
-    const uint32_t nb = w.nb;
-    hipLaunchKernelGGL(k_dm_flags_prep, dim3(w.nt), dim3(kBlock), 0, s, a, w.st_v, w.st_c, w.cidx, w.nv,
-                       c->err_dev);
-    hipLaunchKernelGGL(k_dm_insert, dim3((n + kInsTile - 1) / kInsTile), dim3(kBlock), 0, s, a, w.nv, w.cidx,
-                       w.slots, w.tsize - 1u, w.hslot);
-    hipLaunchKernelGGL(k_dm_leader_rank, dim3(w.nt), dim3(kBlock), 0, s, w.nv, w.hslot, w.slots, w.cidx, w.st_l,
-                       w.kA, w.vA, w.rank_at, out->seg_first, w.nseg, w.ghist, c->err_dev);
-    hipLaunchKernelGGL(k_dm_segof_hist, dim3(w.nt), dim3(kBlock), 0, s, w.nv, w.nseg, w.rank_at, w.kA, w.vA,
-                       w.ghist);
-    if ((r = rsk::launch_check("k_dm_segof_hist"))) return r;
-    // passes for the largest possible segment count (n); surplus passes return at once
-    uint32_t maxbits = 1;
-    while (maxbits < 32 && (1ull << maxbits) < n) ++maxbits;
-    const uint32_t passes = (maxbits + 7) / 8;
-    for (uint32_t p = 0; p < passes; ++p) {
-        const uint32_t *kin = (p & 1u) ? w.kB : w.kA, *vin = (p & 1u) ? w.vB : w.vA;
-        uint32_t *kout = (p & 1u) ? w.kA : w.kB, *vout = (p & 1u) ? w.vA : w.vB;
-        hipLaunchKernelGGL(k_dm_onesweep, dim3(w.nt), dim3(kBlock), 0, s, p, w.nv, w.nseg, kin, vin, w.ghist, w.st_r,
-                           kout, vout, c->err_dev);
-        if ((r = rsk::launch_check("k_dm_onesweep"))) return r;
-    }
-    hipLaunchKernelGGL(k_dm_final, dim3(nb), dim3(kBlock), 0, s, w.nv, w.nseg, w.kA, w.vA, w.kB, w.vB,
-                       out->seg_first, out->perm, out->seg_off, out->n_seg, out->n_valid);
-    return rsk::launch_check("k_dm_final");
+    a.xep = nullptr;
+    if (!group) return demux_pass(c, a, w, out, s);
+    // GROUP_BARRIER: by IdBuf first (into out), the epochs inside each IdBuf into pep (unused by
+    // either pass: neither has CMD_BARRIER), then the key with that epoch (over out again).  Between
+    // the passes every per-packet scratch array is free: k_dm_final of the first pass writes each
+    // position's control flag and segment id into rank_at / hslot, the scan goes to cidx and its
+    // chunk sums to cpos (positions past n_valid hold stale words; no kept value depends on them).
+    DmIn ga = a;
+    ga.fields = RSK_DEMUX_ID;
+    if ((r = demux_pass(c, ga, w, out, s, w.rank_at, w.hslot))) return r;
+    ScanWs sw;
+    sw.sums = w.cpos;
+    sw.sum_off = w.cpos + (n + kScanChunk - 1) / kScanChunk;
+    if ((r = scan_u32(w.rank_at, w.cidx, n, nullptr, sw, s))) return r;
+    hipLaunchKernelGGL(k_dm_gep, dim3(w.nb), dim3(kBlock), 0, s, out->n_valid, out->perm, out->seg_off, w.rank_at,
+                       w.hslot, w.cidx, w.pep);
+    if ((r = rsk::launch_check("k_dm_gep"))) return r;
+    a.xep = w.pep;
+    return demux_pass(c, a, w, out, s);
 }
 
 // =============================================================================================

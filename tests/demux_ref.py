@@ -14,7 +14,9 @@ packets travel over every fake-TCP conn of its group (INetGroup::doSend picks on
 packet, conn/INetGroup.cpp:111-127), so the demux key has to be the leaf's key, not the connKey:
   server  RSK_DEMUX_ID | RSK_DEMUX_DST | RSK_DEMUX_CONV | RSK_DEMUX_CMD_BARRIER
   client  RSK_DEMUX_CONV | RSK_DEMUX_CMD_BARRIER
-Control packets (cmd != DATA: IReset / keep-alive input, or "unrecognized") are barriers.
+Control packets (cmd != DATA: IReset / keep-alive input, or "unrecognized") are barriers.  On the
+server a control packet only reaches its own IdBuf's SubGroup, so RSK_DEMUX_GROUP_BARRIER (a barrier
+for its IdBuf's packets alone) is enough there: SERVER_GROUP_FIELDS.
 """
 from __future__ import annotations
 
@@ -23,6 +25,7 @@ import numpy as np
 from rsock_amd import _abi as A
 
 SERVER_FIELDS = A.DEMUX_ID | A.DEMUX_DST | A.DEMUX_CONV | A.DEMUX_CMD_BARRIER
+SERVER_GROUP_FIELDS = A.DEMUX_ID | A.DEMUX_DST | A.DEMUX_CONV | A.DEMUX_GROUP_BARRIER
 CLIENT_FIELDS = A.DEMUX_CONV | A.DEMUX_CMD_BARRIER
 SERVER, CLIENT = 0, 1
 
@@ -86,10 +89,11 @@ def outcomes(ref_cls, log, n):
     return {"leaf": leaf, "group": group, "ctrl": ctrl, "rst_conv": rst_conv, "ret": log["ret"].copy()}
 
 
-def check_segments(segs, status, cmd, out, server: bool):
+def check_segments(segs, status, cmd, out, server: bool, id=None):
     """Delivering `segs` (list of (first, [packets])) segment by segment hands every leaf the same
     packet sequence the reference gave it, creates leaves and groups in the same order, keeps every
-    control packet exactly where it was relative to the rest, and needs one conn lookup per
+    control packet exactly where it was relative to the rest (with `id`, the IdBuf bytes: relative
+    to the rest of its own IdBuf, the group barrier's promise), and needs one conn lookup per
     segment.  `out` = outcomes() of the reference run."""
     valid = np.nonzero(status == A.RECV_VALID)[0]
     perm = np.array([p for _f, pk in segs for p in pk], np.int64)
@@ -103,9 +107,18 @@ def check_segments(segs, status, cmd, out, server: bool):
     is_ctrl = (status == A.RECV_VALID) & (cmd != A.CMD_DATA)
     assert np.array_equal(is_ctrl, (status == A.RECV_VALID) & ((out["ctrl"] == 1) | (cmd > 4))), \
         "the reference's control packets are the cmd != DATA ones"
-    rank = np.cumsum(status == A.RECV_VALID) - 1
-    for i in np.nonzero(is_ctrl)[0]:
-        assert pos[i] == rank[i], f"control packet {i} moved"
+    if id is None:
+        rank = np.cumsum(status == A.RECV_VALID) - 1
+        for i in np.nonzero(is_ctrl)[0]:
+            assert pos[i] == rank[i], f"control packet {i} moved"
+    else:
+        gid = np.asarray(id, np.uint8).reshape(-1, 8).view(np.uint64).ravel()
+        for g in np.unique(gid[valid]):
+            mine = valid[gid[valid] == g]  # this IdBuf's VALID packets in arrival order
+            pm = pos[mine]
+            for k in np.nonzero(is_ctrl[mine])[0]:
+                assert (pm[:k] < pm[k]).all() and (pm[k + 1:] > pm[k]).all(), \
+                    f"control packet {mine[k]} moved inside its IdBuf"
     for f, pk in segs:
         if is_ctrl[f]:
             assert pk == [f]

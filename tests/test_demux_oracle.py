@@ -13,6 +13,7 @@ import pytest
 from rsock_amd import _abi as A
 
 ALL = A.DEMUX_ID | A.DEMUX_CONN_KEY | A.DEMUX_CONV | A.DEMUX_DST
+BARRIERS = A.DEMUX_CMD_BARRIER | A.DEMUX_GROUP_BARRIER
 
 
 def key_of(i, fields, id, conv, ckey, dst):
@@ -22,17 +23,24 @@ def key_of(i, fields, id, conv, ckey, dst):
             int(dst[i]) if fields & A.DEMUX_DST else None)
 
 
+def group_of(i, fields, id):
+    """The scope a control packet is a barrier for: the whole batch (CMD_BARRIER) or its IdBuf."""
+    return bytes(id[8 * i: 8 * i + 8]) if fields & A.DEMUX_GROUP_BARRIER else None
+
+
 def py_demux(status, cmd, fields, id, conv, ckey, dst):
-    """Restatement: walk VALID packets; a control packet (barrier) is alone and closes the epoch."""
-    segs, where, epoch = [], {}, 0
+    """Restatement: walk VALID packets; a control packet (barrier) is alone and closes the epoch of
+    its scope (group_of)."""
+    segs, where, epoch = [], {}, {}
     for i in range(len(status)):
         if status[i] != A.RECV_VALID:
             continue
-        if fields & A.DEMUX_CMD_BARRIER and cmd[i] != A.CMD_DATA:
+        g = group_of(i, fields, id)
+        if fields & BARRIERS and cmd[i] != A.CMD_DATA:
             segs.append((i, [i]))
-            epoch += 1
+            epoch[g] = epoch.get(g, 0) + 1
             continue
-        k = (epoch,) + key_of(i, fields, id, conv, ckey, dst)
+        k = (epoch.get(g, 0),) + key_of(i, fields, id, conv, ckey, dst)
         if k not in where:
             where[k] = len(segs)
             segs.append((i, []))
@@ -42,13 +50,14 @@ def py_demux(status, cmd, fields, id, conv, ckey, dst):
 
 def reference_routing(status, cmd, fields, id, conv, ckey, dst):
     """The reference's observable effect: per-key delivery sequences + conn creation order, with
-    control packets as ordered events."""
+    control packets as ordered events (each seeing the conns of its scope created so far)."""
     conns, created, events = {}, [], []
     for i in range(len(status)):
         if status[i] != A.RECV_VALID:
             continue
-        if fields & A.DEMUX_CMD_BARRIER and cmd[i] != A.CMD_DATA:
-            events.append(("ctrl", i, len(created)))
+        if fields & BARRIERS and cmd[i] != A.CMD_DATA:
+            g = group_of(i, fields, id)
+            events.append(("ctrl", i, sum(1 for k in created if g is None or k[0] == g)))
             continue
         k = key_of(i, fields, id, conv, ckey, dst)
         if k not in conns:
@@ -61,8 +70,9 @@ def reference_routing(status, cmd, fields, id, conv, ckey, dst):
 def segment_routing(segs, cmd, fields, id, conv, ckey, dst):
     conns, created, events = {}, [], []
     for first, pk in segs:
-        if fields & A.DEMUX_CMD_BARRIER and cmd[first] != A.CMD_DATA:
-            events.append(("ctrl", first, len(created)))
+        if fields & BARRIERS and cmd[first] != A.CMD_DATA:
+            g = group_of(first, fields, id)
+            events.append(("ctrl", first, sum(1 for k in created if g is None or k[0] == g)))
             continue
         k = key_of(first, fields, id, conv, ckey, dst)
         assert all(key_of(i, fields, id, conv, ckey, dst) == k for i in pk)
@@ -87,7 +97,8 @@ def make_case(rng, n, nkeys, p_ctrl, p_valid):
 
 @pytest.mark.parametrize("fields", [ALL, A.DEMUX_CONN_KEY, A.DEMUX_ID | A.DEMUX_CONV | A.DEMUX_DST, A.DEMUX_CONV,
                                     0, ALL | A.DEMUX_CMD_BARRIER, A.DEMUX_CONN_KEY | A.DEMUX_CMD_BARRIER,
-                                    A.DEMUX_CMD_BARRIER])
+                                    A.DEMUX_CMD_BARRIER, ALL | A.DEMUX_GROUP_BARRIER,
+                                    A.DEMUX_ID | A.DEMUX_GROUP_BARRIER])
 @pytest.mark.parametrize("shape", [(0, 1, 0.0, 1.0), (1, 1, 0.0, 1.0), (500, 3, 0.05, 0.9), (3000, 40, 0.01, 0.7),
                                    (2000, 2000, 0.0, 1.0), (800, 5, 0.5, 1.0), (300, 4, 0.0, 0.0), (400, 7, 1.0, 1.0)])
 def test_oracle_vs_restatement(oracle, fields, shape):
@@ -108,3 +119,14 @@ def test_oracle_null_unselected_fields(oracle):
     status, cmd, ids, conv, ckey, dst = make_case(rng, 200, 6, 0.1, 0.8)
     got, _ = oracle.demux_batch(status, cmd, A.DEMUX_CONN_KEY | A.DEMUX_CMD_BARRIER, conn_key=ckey)
     assert got == py_demux(status, cmd, A.DEMUX_CONN_KEY | A.DEMUX_CMD_BARRIER, ids, conv, ckey, dst)
+
+
+def test_group_barrier_fewer_segments(oracle):
+    """A control packet splits only its own IdBuf's conns: with many IdBufs the group barrier leaves
+    far fewer segments than the batch-wide barrier, and both satisfy the reference's routing."""
+    rng = np.random.default_rng(5)
+    status, cmd, ids, conv, ckey, dst = make_case(rng, 6000, 60, 0.05, 1.0)
+    nb = len(oracle.demux_batch(status, cmd, ALL | A.DEMUX_CMD_BARRIER, ids, conv, ckey, dst)[0])
+    ng = len(oracle.demux_batch(status, cmd, ALL | A.DEMUX_GROUP_BARRIER, ids, conv, ckey, dst)[0])
+    assert ng < nb // 2, (ng, nb)
+

@@ -75,14 +75,14 @@ SHAPES = [  # n, groups, nets, convs, p_ctrl, p_valid, p_bad_cmd
 
 
 @needs_ref
-@pytest.mark.parametrize("stack", [D.SERVER, D.CLIENT])
+@pytest.mark.parametrize("stack,fields", [(D.SERVER, D.SERVER_FIELDS), (D.SERVER, D.SERVER_GROUP_FIELDS),
+                                          (D.CLIENT, D.CLIENT_FIELDS)])
 @pytest.mark.parametrize("shape", SHAPES)
-def test_reference_unchanged_by_segment_order(refdemux, oracle, stack, shape):
+def test_reference_unchanged_by_segment_order(refdemux, oracle, stack, fields, shape):
     n, ng, nn, nc, pc, pv, pb = shape
     rng = np.random.default_rng(n * 7 + stack * 1000 + ng)
     status, cmd, ids, conv, ckey, dst = D.rsock_case(rng, n, ng, nn, nc, pc, pv, pb)
     kk, kc = _known(rng, ckey, nc) if stack == D.CLIENT else ((), ())
-    fields = D.SERVER_FIELDS if stack == D.SERVER else D.CLIENT_FIELDS
     segs, nv = oracle.demux_batch(status, cmd, fields, ids, conv, ckey, dst)
     assert nv == int((status == A.RECV_VALID).sum())
     perm = [p for _f, pk in segs for p in pk]
@@ -128,6 +128,10 @@ def test_oracle_segments_against_golden(oracle, ci):
     segs, nv = oracle.demux_batch(c["status"], c["cmd"], c["fields"], c["id"], c["conv"], c["conn_key"], c["dst"])
     assert nv == int((c["status"] == A.RECV_VALID).sum())
     D.check_segments(segs, c["status"], c["cmd"], c, c["stack"] == D.SERVER)
+    if c["stack"] == D.SERVER:  # the server's IdBuf-scoped barrier against the same reference outcomes
+        segs, _ = oracle.demux_batch(c["status"], c["cmd"], D.SERVER_GROUP_FIELDS, c["id"], c["conv"],
+                                     c["conn_key"], c["dst"])
+        D.check_segments(segs, c["status"], c["cmd"], c, True, id=c["id"])
 
 
 def test_check_segments_rejects_arrival_order_violations(oracle):
@@ -146,3 +150,29 @@ def test_check_segments_rejects_arrival_order_violations(oracle):
     moved = segs[:s - 1] + [segs[s], segs[s - 1]] + segs[s + 1:]
     with pytest.raises(AssertionError):
         D.check_segments(moved, c["status"], c["cmd"], c, True)
+    # group barrier: the batch-wide segments (a stricter order) pass the IdBuf-scoped check, and a
+    # leaf's first segment after a control packet of its IdBuf, merged into the leaf's segment before
+    # it (leaf order and segment order stay intact), fails it
+    D.check_segments(segs, c["status"], c["cmd"], c, True, id=c["id"])
+    gs, _ = oracle.demux_batch(c["status"], c["cmd"], D.SERVER_GROUP_FIELDS, c["id"], c["conv"], c["conn_key"],
+                               c["dst"])
+    D.check_segments(gs, c["status"], c["cmd"], c, True, id=c["id"])
+    leaf, gid = c["leaf"], c["id"].reshape(-1, 8).view(np.uint64).ravel()
+    bad = None
+    for k, (f, _pk) in enumerate(gs):
+        if c["cmd"][f] == 0:
+            continue
+        lf = [e for e, (f2, _p) in enumerate(gs[:k]) if c["cmd"][f2] == 0 and leaf[f2] >= 0 and gid[f2] == gid[f]]
+        for e in reversed(lf):  # the leaf's next segment lies after the barrier
+            m = next((m for m in range(e + 1, len(gs)) if c["cmd"][gs[m][0]] == 0 and leaf[gs[m][0]] == leaf[gs[e][0]]),
+                     None)
+            if m is not None and m > k:
+                bad = list(gs)
+                bad[e] = (gs[e][0], gs[e][1] + gs[m][1])
+                del bad[m]
+                break
+        if bad:
+            break
+    assert bad is not None
+    with pytest.raises(AssertionError, match="moved inside its IdBuf"):
+        D.check_segments(bad, c["status"], c["cmd"], c, True, id=c["id"])

@@ -29,7 +29,8 @@ def run_gpu(codec, gpu, status, cmd, fields, ids, conv, ckey, dst):
 
 
 FIELDS = [ALL, A.DEMUX_CONN_KEY, A.DEMUX_ID | A.DEMUX_CONV | A.DEMUX_DST, A.DEMUX_CONV, 0,
-          ALL | A.DEMUX_CMD_BARRIER, A.DEMUX_CONN_KEY | A.DEMUX_CMD_BARRIER, A.DEMUX_CMD_BARRIER]
+          ALL | A.DEMUX_CMD_BARRIER, A.DEMUX_CONN_KEY | A.DEMUX_CMD_BARRIER, A.DEMUX_CMD_BARRIER,
+          ALL | A.DEMUX_GROUP_BARRIER, A.DEMUX_ID | A.DEMUX_GROUP_BARRIER]
 SHAPES = [(1, 1, 0.0, 1.0), (63, 3, 0.1, 0.9), (500, 3, 0.05, 0.9), (4097, 40, 0.01, 0.7), (3000, 3000, 0.0, 1.0),
           (800, 5, 0.5, 1.0), (300, 4, 0.0, 0.0), (400, 7, 1.0, 1.0), (70000, 300, 0.002, 0.8)]
 
@@ -47,7 +48,7 @@ def test_demux_random(codec, gpu, oracle, fields, shape):
 
 
 @pytest.mark.parametrize("n,fields", [(300000, ALL), (200000, A.DEMUX_CONN_KEY | A.DEMUX_CMD_BARRIER),
-                                      (65537, A.DEMUX_CONV)])
+                                      (65537, A.DEMUX_CONV), (200000, ALL | A.DEMUX_GROUP_BARRIER)])
 def test_demux_many_segments(codec, gpu, oracle, n, fields):
     """Every packet its own key (segments = n_valid: 3 radix passes at 300K), and dense barriers."""
     rng = np.random.default_rng(n)
@@ -118,6 +119,12 @@ def test_demux_empty_and_errors(codec, gpu):
         codec.demux_batch(st, st.view(torch.uint8), 0x40, DemuxBuffers.alloc(8, gpu))  # unknown field bit
     with pytest.raises(RskError):
         codec.demux_batch(st, st.view(torch.uint8), A.DEMUX_CONN_KEY, DemuxBuffers.alloc(8, gpu))  # key missing
+    ids = torch.zeros(64, dtype=torch.uint8, device=gpu)
+    for bad in (A.DEMUX_CONV | A.DEMUX_GROUP_BARRIER,  # group barrier without the IdBuf
+                A.DEMUX_ID | A.DEMUX_GROUP_BARRIER | A.DEMUX_CMD_BARRIER):  # both barriers
+        with pytest.raises(RskError):
+            codec.demux_batch(st, st.view(torch.uint8), bad, DemuxBuffers.alloc(8, gpu), id=ids,
+                              conv=st.view(torch.uint8).to(torch.int32))
 
 
 def test_demux_decoded_c4(codec, gpu, oracle):
@@ -186,10 +193,16 @@ def test_demux_golden_reference_routing(codec, gpu, oracle, ci):
     D.check_segments(got, c["status"], c["cmd"], c, c["stack"] == D.SERVER)
     exp = oracle.demux_batch(c["status"], c["cmd"], c["fields"], c["id"], c["conv"], c["conn_key"], c["dst"])
     assert got == exp[0]
+    if c["stack"] == D.SERVER:  # the IdBuf-scoped barrier (two passes on the device)
+        f = D.SERVER_GROUP_FIELDS
+        got, nv = run_gpu(codec, gpu, c["status"], c["cmd"], f, c["id"], c["conv"], c["conn_key"], c["dst"])
+        D.check_segments(got, c["status"], c["cmd"], c, True, id=c["id"])
+        assert got == oracle.demux_batch(c["status"], c["cmd"], f, c["id"], c["conv"], c["conn_key"], c["dst"])[0]
 
 
 @pytest.mark.parametrize("fields", [A.DEMUX_ID | A.DEMUX_CONN_KEY | A.DEMUX_CMD_BARRIER,
-                                    A.DEMUX_CONN_KEY | A.DEMUX_CMD_BARRIER, ALL | A.DEMUX_CMD_BARRIER])
+                                    A.DEMUX_CONN_KEY | A.DEMUX_CMD_BARRIER, ALL | A.DEMUX_CMD_BARRIER,
+                                    ALL | A.DEMUX_GROUP_BARRIER])
 def test_demux_epoch_edges_same_key(codec, gpu, oracle, fields):
     """The same (IdBuf, connKey) on both sides of control packets placed at insert / look-back tile
     edges (511/512, 1023/1024, 4095/4096/4097, 8191/8192), one epoch spanning several tiles, and
@@ -208,3 +221,21 @@ def test_demux_epoch_edges_same_key(codec, gpu, oracle, fields):
     assert got[1] == exp[1]
     assert got[0] == exp[0]
 
+
+
+@pytest.mark.parametrize("n,groups,p_ctrl", [(1 << 20, 64, 0.002), (1 << 20, 64, 0.05), (300000, 5000, 0.01),
+                                             (100000, 2, 0.3)])
+def test_demux_group_barrier_server_shapes(codec, gpu, oracle, n, groups, p_ctrl):
+    """Server batches (tests/demux_ref.rsock_case: IdBuf groups, convs over several fake-TCP conns)
+    under the IdBuf-scoped barrier: the device's two passes against the oracle's walk, with far fewer
+    segments than the batch-wide barrier once there are many groups."""
+    from tests import demux_ref as D
+
+    rng = np.random.default_rng(n + groups)
+    status, cmd, ids, conv, ckey, dst = D.rsock_case(rng, n, groups, 4, 8, p_ctrl, 0.95, 0.001)
+    got, nv = run_gpu(codec, gpu, status, cmd, D.SERVER_GROUP_FIELDS, ids, conv, ckey, dst)
+    exp = oracle.demux_batch(status, cmd, D.SERVER_GROUP_FIELDS, ids, conv, ckey, dst)
+    assert nv == exp[1] and len(got) == len(exp[0])
+    assert got == exp[0]
+    if groups >= 64 and p_ctrl >= 0.002:
+        assert len(got) < len(oracle.demux_batch(status, cmd, D.SERVER_FIELDS, ids, conv, ckey, dst)[0]) // 2

@@ -100,7 +100,7 @@ def main():
     dfields = rc._abi.DEMUX_ID | rc._abi.DEMUX_CONN_KEY | rc._abi.DEMUX_CMD_BARRIER
     # each demux shape on a context of its own: a context sizes its key table from its previous call
     # (steady traffic); one context alternating between shapes is tests/test_gpu_demux.py's business
-    cx_dm = {k: rc.Codec(b"hello135", 0) for k in ("demux", "demux_64conn", "demux_server")}
+    cx_dm = {k: rc.Codec(b"hello135", 0) for k in ("demux", "demux_64conn", "demux_server", "demux_server_group")}
     ops["demux"] = lambda: cx_dm["demux"].demux_batch(w.dec.status, w.dec.cmd, dfields, dmx, id=w.dec.id,
                                                       conv=w.dec.conv, conn_key=w.dec.conn_key, stream=s)
     # capture filter (server form) over the Ethernet wire packets: a 4M-packet capture batch
@@ -142,6 +142,12 @@ def main():
     dmxs = rc.DemuxBuffers.alloc(n, dev)
     ops["demux_server"] = lambda: cx_dm["demux_server"].demux_batch(k_st, k_cmd, sfields, dmxs, id=s_id,
                                                                     conv=s_conv, dst=s_dst, stream=s)
+    # the same batch with the IdBuf-scoped barrier (RSK_DEMUX_GROUP_BARRIER: ServerGroup routes a
+    # control packet to its own IdBuf's SubGroup only): two group-by passes, ~1 segment per SConn
+    gfields = A.DEMUX_ID | A.DEMUX_DST | A.DEMUX_CONV | A.DEMUX_GROUP_BARRIER
+    dmxg = rc.DemuxBuffers.alloc(n, dev)
+    ops["demux_server_group"] = lambda: cx_dm["demux_server_group"].demux_batch(k_st, k_cmd, gfields, dmxg, id=s_id,
+                                                                                conv=s_conv, dst=s_dst, stream=s)
     for k, f in ops.items():
         if k == "demux":
             cx.onrecv_batch(w.frame, w.frame_off, w.frame_len, w.dec, stream=s)
@@ -163,7 +169,7 @@ def main():
     hlen = w.frame_len.to(torch.int32) + 21
     tcp3, sdec = rc.TcpInfoBuffers.alloc(n, dev), rc.DecodeBuffers.alloc(n, dev)
     ops["syncinput_decode"] = lambda: cx.syncinput_batch(hand, hoff, hlen, tcp3, sdec, stream=s)
-    nseg = [int(dmx.n_seg.item()), int(dmx64.n_seg.item()), int(dmxs.n_seg.item())]
+    nseg = [int(dmx.n_seg.item()), int(dmx64.n_seg.item()), int(dmxs.n_seg.item()), int(dmxg.n_seg.item())]
     if args.only:
         keep = args.only.split(",")
         ops = {k: f for k, f in ops.items() if k in keep}
@@ -190,6 +196,7 @@ def main():
         "demux": 1 + 1 + 8 + 8 + 4,  # status, cmd, id, conn_key in; perm out (+ per-segment words)
         "demux_64conn": 1 + 1 + 8 + 8 + 4,
         "demux_server": 1 + 1 + 8 + 4 + 4 + 4,  # status, cmd, id, conv, dst in; perm out
+        "demux_server_group": 1 + 1 + 8 + 4 + 4 + 4,
         "capture_filter": 8 + 4 + 64 + 16 + 1 + 4,  # cap_off, cap_len, header windows, match, match_idx
         "filter_parse_decode": 8 + 4 + 64 + 16 + 1 + 54 + 32 + 16 + 21 + 4 + 73 - 42,
         "decode_hdr": 32 + 2 + 27 + 4,
