@@ -276,14 +276,17 @@ class Codec:
 
     @property
     def last_copy_k(self) -> int:
-        """Packets per copy wave of the last two-pass output_batch (1, 2, 4; 0 before any)."""
+        """Packets per copy wave of the last two-pass output_batch (1, 2, 4; -1: the output-stationary copy;
+        0 before any)."""
         fn = lib().rsk__last_copy_k
         fn.argtypes = [ctypes.c_void_p]
         return int(fn(self._ctx))
 
     def set_copy_k(self, k: int = 0) -> None:
-        """Internal knob of the two-pass encode (rsk__set_copy_k): packets per copy wave (1, 2, 4; 0 = chosen
-        from the last sampled mean payload: 4 below 880 B, 2 below 1160 B, 1 above; rsk_kernels.hip kAutoK*)."""
+        """Internal knob of the two-pass encode (rsk__set_copy_k): packets per copy wave (1, 2, 4), or -1 for the
+        output-stationary copy (k_encode_os: waves own 1-KB blocks of the frame arena, for frames laid back to
+        back); 0 = chosen from the last sampled statistic: output-stationary when the sampled frames lie back
+        to back, else 4 below a mean payload of 880 B, 2 below 1160 B, 1 above (rsk_kernels.hip kAutoK*)."""
         fn = lib().rsk__set_copy_k
         fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
         _check(fn(self._ctx, k), "rsk__set_copy_k")

@@ -32,7 +32,8 @@ struct rsk_ctx {
     // encode path (rsk_encode_batch): 0 = chosen per call from the previous batch's statistic, else
     // RSK_ENC_PATH_* (rsk_set_encode_path)
     int enc_path = 0;
-    int copy_k = 0;  // the two-pass copy's packets per wave (0: by the sampled mean payload; rsk__set_copy_k)
+    int copy_k = 0;  // the two-pass copy's packets per wave (-1: output-stationary; 0: by the sampled statistic; rsk__set_copy_k)
+    uint32_t os_epoch = 0;  // per output-stationary call: the value k_encode_heads_os flags a failed layout check with
     uint32_t tp_chunk = 0;  // the two-pass form's chunk of packets (0: whole batch; rsk__set_two_pass_chunk)
     std::atomic<int> enc_last_path{0};  // the path the last rsk_encode_batch took (rsk__last_encode_path)
     std::atomic<int> enc_last_k{0};     // its packets per copy wave, two-pass form (rsk__last_copy_k)

@@ -192,6 +192,8 @@ __device__ __forceinline__ void encode_tag(const EncArgs &a, const KeySched &ks,
 // other paths launch k_enc_sample behind the encode (the per-set kernel itself carries no extra
 // argument: one more pointer in its arguments cost C4 12 % through SGPR spills, gpurun_out/r04o).
 constexpr uint32_t kStatValid = 0x80000000u;
+constexpr uint32_t kStatPacked = 0x40000000u;  // the sampled frames lie back to back (output-stationary copy)
+constexpr uint32_t kStatMean = 0xffffu;        // the sampled mean payload
 // AUTO's choice (rsk_encode_batch, enc_path / copy_k): batches of at least kTwoPassMinPackets by the mean
 // payload of the context's last sampled batch (below that, and in a capture before any sample, the
 // per-set kernel).
@@ -208,15 +210,37 @@ constexpr uint32_t kAutoShortBelow = 400;   // .. below this: the short-frame ke
 constexpr uint32_t kAutoK4Below = 880;      // .. below this: two-pass, 4 packets per copy wave (C4)
 constexpr uint32_t kAutoK2Below = 1160;     // .. below this: two-pass, 2 packets per copy wave; above: 1 (C3)
 constexpr uint64_t kCopyMaxPackets = 1ull << 25;  // per k_encode_copy launch (2^31 work-items)
-__device__ __forceinline__ void enc_sample(const uint16_t *pay_len, uint32_t n, uint32_t *stat) {
+// the output-stationary copy's block map: 2 blocks per packet (frames of <= 1531 B + pad, back to back:
+// <= 2 KB each)
+__host__ __device__ constexpr uint64_t os_bcap(uint64_t n) { return 2ull * n + 2ull; }
+// the two-pass encode's workspace: 32-B records, the block map and its two control words
+__host__ __device__ constexpr uint64_t enc_ws_bytes(uint64_t n) { return 32ull * n + 4ull * os_bcap(n) + 16ull; }
+// With frame_off (round 6) it also checks whether each sampled packet's frame ends where the next
+// packet's begins, inside a 16-B chunk (byte-packed frames without a pad share their boundary
+// chunks): three in four -> kStatPacked, which lets AUTO take the output-stationary copy
+// (k_encode_os).  Frames packed at a 16-B pitch share nothing, and the packet copies are faster
+// there (C4 16-B packed: 0.36 vs 0.435 ms).  A hint only: every copy writes the same bytes.
+__device__ __forceinline__ void enc_sample(const uint16_t *pay_len, uint32_t n, uint32_t *stat,
+                                           const uint64_t *frame_off = nullptr, uint32_t pad = 0u) {
     if (stat == nullptr || blockIdx.x != 0u || threadIdx.x >= 64u) return;  // one wave of block 0
-    uint32_t v = pay_len[((uint64_t)threadIdx.x * n) >> 6];
+    const uint64_t i = ((uint64_t)threadIdx.x * n) >> 6;
+    const uint32_t P = pay_len[i];
+    uint32_t v = P;
+    bool packed = false;
+    if (frame_off && pad == 0u && i + 1u < n && P != 0u && P <= (uint32_t)RSK_MAX_PAYLOAD) {
+        const uint64_t e = frame_off[i] + RSK_HEAD_SIZE + P;
+        packed = frame_off[i + 1] == e && (e & 15u) != 0u;  // the next frame starts inside e's 16-B chunk
+    }
+    const uint32_t np = (uint32_t)__popcll(__ballot(packed));
 #pragma unroll
     for (int off = 32; off; off >>= 1) v += (uint32_t)__shfl_xor((int)v, off);
-    if (threadIdx.x == 0u) __hip_atomic_store(stat, kStatValid | (v >> 6), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 0u)
+        __hip_atomic_store(stat, kStatValid | (np >= 48u ? kStatPacked : 0u) | (v >> 6), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__global__ __launch_bounds__(64) void k_enc_sample(const uint16_t *pay_len, uint32_t n, uint32_t *stat) {
-    enc_sample(pay_len, n, stat);
+__global__ __launch_bounds__(64) void k_enc_sample(const uint16_t *pay_len, uint32_t n, uint32_t *stat,
+                                                   const uint64_t *frame_off, uint32_t pad) {
+    enc_sample(pay_len, n, stat, frame_off, pad);
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -807,7 +831,7 @@ template <int SADD = 0>
 __global__ __launch_bounds__(kBlock) void k_encode_heads(EncArgs a, KeySched ks, uint4 *heads, uint32_t *stat,
                                                          uint64_t base, uint64_t nr) {
     stage_tags(ks);
-    enc_sample(a.pay_len, a.n, stat);
+    enc_sample(a.pay_len, a.n, stat, a.frame_off, a.pad);
     const uint64_t i = base + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     const Lane1 L = encode_phase1<true, true, SADD>(a, ks, i < a.n ? i : a.n);
     if (i < a.n && L.st > 0) {
@@ -934,6 +958,271 @@ __global__ __launch_bounds__(kBlock) void k_encode_copy(EncArgs a, const uint32_
 #pragma unroll
         for (int t = 0; t < 8; ++t) Hj[t] = heads[4 * ((t < 4 ? 0 : nr) + i0 + p) + (t & 3)];  // uniform: scalar loads
         copyk_store<K, NT>(a, c, p, lane, Hj);
+    }
+}
+
+// ---- the output-stationary copy for frames laid back to back (round 6) -------
+// When frames are byte-packed, the 16-B chunk where one frame ends and the next begins is written by
+// two packet-stationary waves, each with byte stores for its part (store_range16: up to five
+// stores), and the write pattern costs what the copy saves: tools/bench_layouts.py --probe writes
+// C4's frames in the encode's access shape at 0.348 ms with whole-chunk stores and 0.572 ms with the
+// byte-exact edges (profiles/r06_layout_probe.json).  Here waves own OUTPUT: block b = kOsBlock bytes
+// of the arena from r0 = (frame + frame_off[0]) rounded down, each lane one 16-B chunk, assembled from
+// at most two frames (frames are >= 32 B: a chunk holds the tail of frame F1 -- header words from its
+// pass-1 record, payload through a per-lane funnel, pad zeros -- and the first header bytes of F2), so
+// every chunk a frame touches is written once, whole, unless it also holds bytes outside every frame.
+// The header pass (k_encode_heads_os) maps each block to the first packet that can reach it and
+// checks that the frames are laid out in packet order without overlap; otherwise (or when the gaps
+// are wide) k_encode_os copies packet by packet as k_encode_copy<NT, 1> does.
+constexpr uint32_t kOsBlock = 2048;  // bytes per wave-iteration: 2 chunks per lane (1 KB: 0.487 ms on C4 byte-packed; 4 KB: 141 VGPRs)
+constexpr uint32_t kOsMaxGapBlocks = 16;  // blocks one packet may map (wider gaps: the fallback)
+struct OsMap {
+    uint32_t *bfirst;  // [bcap] first packet of block b
+    uint32_t *ctl;     // [0] = epoch: the layout failed a check in this call; [1] = block count
+    uint32_t bcap, epoch;
+};
+__device__ __forceinline__ uint32_t os_ext(const EncArgs &a, uint64_t fo, uint32_t P) {
+    return P != 0u && P <= (uint32_t)RSK_MAX_PAYLOAD ? padded_len(a.frame + fo, RSK_HEAD_SIZE + P, a.pad) : 0u;
+}
+
+template <int SADD = 0>
+__global__ __launch_bounds__(kBlock) void k_encode_heads_os(EncArgs a, KeySched ks, uint4 *heads, uint32_t *stat,
+                                                            uint64_t nr, OsMap m) {
+    stage_tags(ks);
+    enc_sample(a.pay_len, a.n, stat, a.frame_off, a.pad);
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const Lane1 L = encode_phase1<true, true, SADD>(a, ks, i < a.n ? i : a.n);
+    bool bad = false;
+    if (i < a.n) {
+        if (L.st > 0) {
+            heads[i] = make_uint4(L.H[0], L.H[1], L.H[2], L.H[3]);
+            heads[nr + i] = make_uint4(L.H[4], L.H[5], L.H[6], L.H[7]);
+        }
+        const uint64_t base = reinterpret_cast<uintptr_t>(a.frame);
+        const uint64_t r0 = (base + a.frame_off[0]) & ~(uint64_t)(kOsBlock - 1u);
+        const uint64_t s = base + L.fo, e = s + (L.st > 0 ? padded_len(a.frame + L.fo, (uint32_t)L.st, a.pad) : 0u);
+        uint64_t ep = r0;  // the previous packet's end
+        if (i > 0) {
+            const uint64_t fp = a.frame_off[i - 1];
+            ep = base + fp + os_ext(a, fp, a.pay_len[i - 1]);
+        }
+        bad = s < ep;
+        if (!bad) {  // blocks starting in [ep, e): this packet is the first that can reach them
+            uint64_t b = (ep - r0 + kOsBlock - 1u) / kOsBlock;
+            const uint64_t bend = e > r0 ? (e - r0 + kOsBlock - 1u) / kOsBlock : 0u;
+            if (bend > b + kOsMaxGapBlocks || bend > m.bcap) bad = true;
+            else
+                for (; b < bend; ++b) m.bfirst[b] = (uint32_t)i;
+        }
+        if (i == a.n - 1u) m.ctl[1] = e > r0 ? (uint32_t)((e - r0 + kOsBlock - 1u) / kOsBlock) : 0u;
+    }
+    if (__ballot(bad) != 0ull && (threadIdx.x & 63u) == 0u)
+        __hip_atomic_store(m.ctl, m.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Lane view of one frame of the window: start address, bytes written (padded), payload geometry.
+struct OsFrame {
+    uint64_t s, e;        // [s, e): the frame's bytes in the arena (absolute addresses)
+    uint64_t po;          // payload offset
+    uint32_t P, p;        // payload length, packet index
+};
+
+// The 16 bytes of frame F's image at image offset t (t >= 0): header words from its record for
+// t < 32, the payload through the per-lane funnel from t + 16 > 32 on (payload byte x at image
+// 31 + x), zero past 31 + P (the pad).  Split in two so that a block issues every load of all its
+// chunks before the first use (a load inside a divergent branch waits for the branch: the first
+// build, with the loads in branches, ran C4's byte-packed frames at 0.66 ms): os_load always loads
+// (addresses clamped into the payload and the records), os_compose only selects.
+struct OsLd {
+    uint4 A, B, H0, H1;
+    uint32_t sh;
+};
+template <int NT>
+__device__ __forceinline__ OsLd os_load(const EncArgs &a, const uint4 *heads, uint64_t nr, const OsFrame &F,
+                                        uint32_t t) {
+    OsLd L;
+    const uint64_t lo = F.po & ~15ull, hi = (F.po + (F.P ? F.P : 1u) - 1u) & ~15ull;
+    const int64_t src = (int64_t)F.po + (int64_t)t - RSK_HEAD_SIZE;  // payload address of chunk byte 0
+    const uint64_t c0 = (uint64_t)(src & ~(int64_t)15);
+    L.sh = (uint32_t)(src & 15);
+    const int64_t c1 = (int64_t)c0 + 16;  // chunks outside the payload: any payload chunk (masked)
+    const uint64_t a0 = (int64_t)c0 < (int64_t)lo ? lo : c0 > hi ? hi : c0;
+    const uint64_t a1 = c1 < (int64_t)lo ? lo : (uint64_t)c1 > hi ? hi : (uint64_t)c1;
+    L.A = ld16<NT & 1>(a.payload + a0);
+    L.B = ld16<NT & 1>(a.payload + a1);
+    L.H0 = heads[F.p];
+    L.H1 = heads[nr + F.p];
+    return L;
+}
+__device__ __forceinline__ uint4 os_compose(const OsFrame &F, const OsLd &L, uint32_t t) {
+    const uint32_t flen = RSK_HEAD_SIZE + F.P;
+    uint4 v = funnel16_lane(L.A, L.B, L.sh);
+    const int lim = (int)flen - (int)t;  // payload bytes end at image flen
+    if (lim < 16) v = lim > 0 ? rsk::keep_bytes16(v, lim) : make_uint4(0u, 0u, 0u, 0u);
+    if (t < 32u) {  // header words (bytes [0, 32) of the record, byte 31 = payload[0])
+        const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+        const uint4 hv = t < 16u ? funnel16_lane(L.H0, L.H1, t) : funnel16_lane(L.H1, z, t - 16u);
+        const int nh = 32 - (int)t;  // chunk bytes [0, nh) are header bytes
+        const uint4 mk = nh >= 16 ? make_uint4(~0u, ~0u, ~0u, ~0u) : rsk::keep_bytes16(make_uint4(~0u, ~0u, ~0u, ~0u), nh);
+        v = make_uint4((hv.x & mk.x) | (v.x & ~mk.x), (hv.y & mk.y) | (v.y & ~mk.y), (hv.z & mk.z) | (v.z & ~mk.z),
+                       (hv.w & mk.w) | (v.w & ~mk.w));
+    }
+    return v;
+}
+
+// A wave's window: descriptors of 64 consecutive packets from p0, one per lane.
+struct OsWin {
+    uint32_t p0;
+    uint64_t s, e, po;  // lane j: packet p0 + j's frame [s, e) (absolute; e = s when not framed), payload offset
+    uint32_t P;
+};
+__device__ __forceinline__ OsWin os_window(const EncArgs &a, uint32_t p0, uint32_t lane) {
+    OsWin W;
+    W.p0 = p0;
+    const uint64_t pj = (uint64_t)p0 + lane;
+    uint64_t fo = 0, po = 0;
+    uint32_t P = 0;
+    if (pj < a.n) {
+        P = a.pay_len[pj];
+        fo = a.frame_off[pj];
+        po = a.pay_off[pj];
+    }
+    W.s = pj < a.n ? reinterpret_cast<uintptr_t>(a.frame) + fo : ~0ull;  // past the batch: starts nowhere
+    W.e = pj < a.n ? W.s + os_ext(a, fo, P) : ~0ull;
+    W.po = po;
+    W.P = P;
+    return W;
+}
+
+// Block [B0, B0 + kOsBlock): every packet overlapping it lies in the window lanes [jlo, jhi] (the
+// caller slides the window).  Chunk u of lane l (q = B0 + 1024 u + 16 l) takes F1 = the last packet
+// starting at or before q (a dropped one has no bytes: with frames in order nothing earlier reaches q
+// then) and F2 = the first framed packet starting inside the chunk; the loop over the block's packets
+// only counts (32-bit starts relative to B0), the frames' fields come from their window lanes by one
+// ds_bpermute each (round 6: selecting whole frame records in the loop cost ~200 VALU per block).
+template <int NT>
+__device__ __forceinline__ void os_block(const EncArgs &a, const uint4 *heads, uint64_t nr, const OsWin &W,
+                                         uint32_t jlo, uint32_t jhi, uint64_t B0, uint32_t lane) {
+    constexpr int U = kOsBlock / 1024;  // chunks per lane, 1 KB apart
+    constexpr int32_t kFar = 1 << 30;
+    // window lane j's start / end relative to B0, clamped to +-2^30 (blocks are 2 KB)
+    const int64_t ds = (int64_t)(W.s - B0), de = (int64_t)(W.e - B0);
+    const int32_t rs = W.s == ~0ull ? kFar : ds < -kFar ? -kFar : ds > kFar ? kFar : (int32_t)ds;
+    const int32_t re = W.e == ~0ull ? kFar : de < -kFar ? -kFar : de > kFar ? kFar : (int32_t)de;
+    uint32_t j1[U], j2[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        j1[u] = 64u;  // none
+        j2[u] = 64u;
+    }
+    for (uint32_t j = jlo; j <= jhi; ++j) {  // uniform
+        const int32_t sj = (int32_t)rdl((uint32_t)rs, j), ej = (int32_t)rdl((uint32_t)re, j);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int32_t q = (int32_t)(1024u * u + 16u * lane);
+            if (sj <= q) j1[u] = j;
+            else if (sj < q + 16 && ej > sj && j2[u] == 64u) j2[u] = j;
+        }
+    }
+    uint32_t c1[U], uu[U], t1[U];
+    OsFrame F1[U];
+    uint32_t p2[U];
+    OsLd L[U];
+    uint4 G[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {  // fields by bpermute, then every load, unconditionally
+        const int32_t q = (int32_t)(1024u * u + 16u * lane);
+        const uint32_t k1 = j1[u] & 63u, k2 = j2[u] & 63u;
+        const int32_t s1 = __shfl(rs, (int)k1), e1 = __shfl(re, (int)k1), s2 = __shfl(rs, (int)k2);
+        const bool h1 = j1[u] < 64u && e1 > q, h2 = j2[u] < 64u;
+        c1[u] = h1 ? (uint32_t)(e1 - q >= 16 ? 16 : e1 - q) : 0u;
+        uu[u] = h2 ? (uint32_t)(s2 - q) : 16u;
+        t1[u] = h1 ? (uint32_t)(q - s1) : 0u;
+        F1[u].po = (uint64_t)(uint32_t)__shfl((int)(uint32_t)W.po, (int)k1) |
+                   ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(W.po >> 32), (int)k1) << 32);
+        F1[u].P = (uint32_t)__shfl((int)W.P, (int)k1);
+        if (!h1) {  // no frame bytes: the loads read payload[0..16) (a dropped packet's offsets may be anything)
+            F1[u].po = 0u;
+            F1[u].P = 1u;
+        }
+        F1[u].p = W.p0 + k1;
+        p2[u] = W.p0 + k2;
+        L[u] = os_load<NT>(a, heads, nr, F1[u], t1[u]);
+        G[u] = heads[p2[u] < a.n ? p2[u] : 0u];
+    }
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        v[u] = os_compose(F1[u], L[u], t1[u]);
+        if (uu[u] < 16u) {  // F2's first 16 - uu header bytes at chunk offset uu
+            const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+            const uint4 hv = funnel16_lane(z, G[u], 16u - uu[u]);
+            const uint4 mk = rsk::keep_bytes16(make_uint4(~0u, ~0u, ~0u, ~0u), (int)uu[u]);
+            v[u] = make_uint4((v[u].x & mk.x) | (hv.x & ~mk.x), (v[u].y & mk.y) | (hv.y & ~mk.y),
+                              (v[u].z & mk.z) | (hv.z & ~mk.z), (v[u].w & mk.w) | (hv.w & ~mk.w));
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        uint8_t *d = reinterpret_cast<uint8_t *>(B0 + 1024u * u + 16u * lane);
+        if (c1[u] == 16u || (uu[u] < 16u && c1[u] == uu[u])) st16<NT>(d, v[u]);  // the whole chunk is frame bytes
+        else {
+            if (c1[u]) rsk::store_range16(d, v[u], 0u, c1[u]);
+            if (uu[u] < 16u) rsk::store_range16(d, v[u], uu[u], 16u);
+        }
+    }
+}
+
+// Persistent waves, each streaming its own contiguous range of blocks with a sliding window of 64
+// packets' descriptors (one block-map load per wave, one descriptor load per 64 packets), or, when the
+// header pass flagged the layout, copying packet by packet.
+template <int NT>
+__global__ __launch_bounds__(kBlock) void k_encode_os(EncArgs a, const uint4 *heads, uint64_t nr, const uint32_t *bfirst,
+                                                      const uint32_t *ctl, uint32_t epoch) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint64_t wid = (uint64_t)blockIdx.x * kWavesPerBlock + w, nw = (uint64_t)gridDim.x * kWavesPerBlock;
+    if (__hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch) {
+        const uint32_t *hr = reinterpret_cast<const uint32_t *>(heads);
+        for (uint64_t i0 = wid; i0 < a.n; i0 += nw) {  // packet by packet (k_encode_copy<NT, 1>)
+            CopyK<1> c;
+            copyk_issue<1, NT>(a, i0, lane, c);
+            if (!c.flen[0]) continue;  // uniform
+            uint32_t Hj[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) Hj[t] = hr[4 * ((t < 4 ? 0 : nr) + i0) + (t & 3)];
+            copyk_store<1, NT>(a, c, 0, lane, Hj);
+        }
+        return;
+    }
+    const uint64_t nb = ctl[1];
+    const uint64_t r0 = (reinterpret_cast<uintptr_t>(a.frame) + a.frame_off[0]) & ~(uint64_t)(kOsBlock - 1u);
+    const uint64_t b0 = nb * wid / nw, b1 = nb * (wid + 1u) / nw;  // this wave's blocks
+    if (b0 >= b1) return;
+    OsWin W = os_window(a, bfirst[b0], lane);
+    for (uint64_t b = b0; b < b1; ++b) {
+        const uint64_t B0 = r0 + b * kOsBlock, B1 = B0 + kOsBlock;
+        // slide: drop the packets that end at or before the block (the window's first packet that
+        // reaches past B0 becomes lane 0) once no packet in the window starts past the block
+        for (;;) {
+            const uint64_t live = __ballot(W.e > B0);  // frames reaching into or past the block (a suffix)
+            const uint64_t past = __ballot(W.s >= B1);  // packets starting past the block
+            if (past != 0ull || (W.p0 + 64ull >= a.n)) {
+                const uint32_t jlo = live ? (uint32_t)__builtin_ctzll(live) : 64u;
+                const uint32_t jhi = past ? (uint32_t)__builtin_ctzll(past) : 64u;  // first starting past
+                if (jlo < jhi) os_block<NT>(a, heads, nr, W, jlo, jhi - 1u, B0, lane);
+                break;
+            }
+            // every packet of the window starts inside or before the block: move on by the packets
+            // that end before it (at least one, else the whole window is inside the block: by 32)
+            const uint32_t adv = live ? (uint32_t)__builtin_ctzll(live) : 64u;
+            if (adv == 0u) {  // a block holding 64 packet starts (tiny or dropped packets): by halves
+                os_block<NT>(a, heads, nr, W, 0u, 31u, B0, lane);  // packets 0..31, then from 32 on
+                W = os_window(a, W.p0 + 32u, lane);
+                continue;
+            }
+            W = os_window(a, W.p0 + adv, lane);
+        }
     }
 }
 
@@ -2824,10 +3113,10 @@ int rsk_set_encode_path(rsk_ctx *c, int path) {
     return RSK_OK;
 }
 
-// Internal (tests, tools): the two-pass copy's packets per wave k (1, 2, 4; 0 = from the sampled mean
-// payload, copy_k below).
+// Internal (tests, tools): the two-pass copy's packets per wave k (1, 2, 4; -1 = the output-stationary
+// copy k_encode_os; 0 = from the sampled statistic, copy_k below).
 int rsk__set_copy_k(rsk_ctx *c, int k) {
-    if (!c || !(k == 0 || k == 1 || k == 2 || k == 4)) return RSK_EINVAL;
+    if (!c || !(k == -1 || k == 0 || k == 1 || k == 2 || k == 4)) return RSK_EINVAL;
     c->copy_k = k;
     return RSK_OK;
 }
@@ -2907,7 +3196,8 @@ int rsk_reserve_stream(rsk_ctx *c, uint32_t n_max, void *stream) {
     void *p = nullptr;
     // (and the two-pass wire build's: 96 B per packet of one 2^20-packet chunk, k_wire_heads)
     const uint64_t wire_rec = 96ull * std::min<uint64_t>(n_max, 1ull << 20);
-    if (rsk::stream_ws(c, (hipStream_t)stream, rsk::WS_ENC, std::max<uint64_t>(32ull * n_max, wire_rec), &p) != RSK_OK) {
+    if (rsk::stream_ws(c, (hipStream_t)stream, rsk::WS_ENC, std::max<uint64_t>(enc_ws_bytes(n_max), wire_rec), &p) !=
+        RSK_OK) {
         (void)hipGetLastError();
         g_last_error[0] = 0;
     }
@@ -2927,7 +3217,8 @@ static uint32_t sampled_mean(const rsk_ctx *c) {
 static int copy_k(rsk_ctx *c) {
     if (c->copy_k) return c->copy_k;
     const uint32_t s = sampled_mean(c);
-    const uint32_t mean = (s & kStatValid) ? s & ~kStatValid : 1400u;
+    if ((s & kStatValid) && (s & kStatPacked) && c->tp_chunk == 0u) return -1;  // frames back to back
+    const uint32_t mean = (s & kStatValid) ? s & kStatMean : 1400u;
     return mean < kAutoK4Below ? 4 : mean < kAutoK2Below ? 2 : 1;
 }
 
@@ -2938,10 +3229,11 @@ static int copy_k(rsk_ctx *c) {
 // calls in gpurun_out/r05f1/c3).  The event, not the stream: nothing queued on the
 // stream after the sample is waited for, and a failed wait is the call's error.  A capture never
 // waits: it takes the per-set kernel when no sample exists.  Returns the path, or RSK_EDEVICE.
-static int enc_path(rsk_ctx *c, uint32_t n, const uint16_t *pay_len, hipStream_t st) {
+static int enc_path(rsk_ctx *c, uint32_t n, const uint16_t *pay_len, hipStream_t st,
+                    const uint64_t *frame_off = nullptr, uint32_t pad = 0u) {
     if (c->enc_path) return c->enc_path;
     if (n >= kTwoPassMinPackets && c->enc_stat_dev && !(sampled_mean(c) & kStatValid) && !rsk::capturing(st)) {
-        hipLaunchKernelGGL(k_enc_sample, dim3(1), dim3(64), 0, st, pay_len, n, c->enc_stat_dev);
+        hipLaunchKernelGGL(k_enc_sample, dim3(1), dim3(64), 0, st, pay_len, n, c->enc_stat_dev, frame_off, pad);
         hipEvent_t ev = nullptr;
         hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventRecord(ev, st);
@@ -2951,11 +3243,28 @@ static int enc_path(rsk_ctx *c, uint32_t n, const uint16_t *pay_len, hipStream_t
     }
     const uint32_t s = sampled_mean(c);
     if (n < kTwoPassMinPackets || !(s & kStatValid)) return RSK_ENC_PATH_PER_SET;
-    const uint32_t mean = s & ~kStatValid;
+    const uint32_t mean = s & kStatMean;
     return mean <= kAutoShortMax      ? RSK_ENC_PATH_SHORT
            : mean < kAutoPerSetBelow  ? RSK_ENC_PATH_PER_SET
            : mean < kAutoShortBelow   ? RSK_ENC_PATH_SHORT
                                       : RSK_ENC_PATH_TWO_PASS;
+}
+
+// k_encode_os's persistent grid: every workgroup resident at once (its waves own static block ranges,
+// so a workgroup that waited for a slot would run its range after the others: a tail)
+static unsigned os_grid(int device) {
+    static std::atomic<unsigned> cached[64];
+    const int d = device >= 0 && device < 64 ? device : 0;
+    unsigned g = cached[d].load(std::memory_order_relaxed);
+    if (g) return g;
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_encode_os<3>, kBlock, 0) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) cus = 256;
+    (void)hipGetLastError();
+    g = (unsigned)(per_cu * cus);
+    cached[d].store(g, std::memory_order_relaxed);
+    return g;
 }
 
 int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_encode_out *out,
@@ -2982,13 +3291,27 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
     hipStream_t st = (hipStream_t)stream;
     const dim3 gd(grid), bd(kBlock);
     (void)gd;
-    const int path = enc_path(c, n, in->pay_len, st);
+    const int path = enc_path(c, n, in->pay_len, st, out->frame_off, a.pad);
     if (path < 0) return path;
     if (path == RSK_ENC_PATH_TWO_PASS) {
         // the two-pass form (batches of long frames): header records, then one wave per packet
         void *hp = nullptr;
-        if (rsk::stream_ws_if(c, st, rsk::WS_ENC, 32ull * n, &hp) == RSK_OK) {
+        if (rsk::stream_ws_if(c, st, rsk::WS_ENC, enc_ws_bytes(n), &hp) == RSK_OK) {
             const int ck = copy_k(c);
+            if (ck < 0) {  // frames back to back: the output-stationary copy (k_encode_os)
+                OsMap m;
+                m.bfirst = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(hp) + 32ull * n);
+                m.ctl = m.bfirst + os_bcap(n);
+                m.bcap = os_bcap(n);
+                m.epoch = ++c->os_epoch;
+                hipLaunchKernelGGL(k_encode_heads_os<0>, dim3(grid_for(n)), bd, 0, st, a, c->ks, static_cast<uint4 *>(hp),
+                                   c->enc_stat_dev, (uint64_t)n, m);
+                hipLaunchKernelGGL(k_encode_os<3>, dim3(os_grid(c->device)), bd, 0, st, a, static_cast<const uint4 *>(hp),
+                                   (uint64_t)n, m.bfirst, m.ctl, m.epoch);
+                c->enc_last_path.store(2, std::memory_order_relaxed);
+                c->enc_last_k.store(-1, std::memory_order_relaxed);
+                return launch_check("k_encode_heads_os / k_encode_os");
+            }
             // chunked (rsk__set_two_pass_chunk): heads then copy per chunk, so a chunk's records and
             // first payload lines may still be in the Infinity Cache when its copy reads them
             const uint64_t chunk = c->tp_chunk ? c->tp_chunk : (uint64_t)n;
@@ -3031,7 +3354,8 @@ int rsk_encode_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const rsk_
     // 64-thread launch behind the encode: the per-set kernel itself carries no pointer for it (one more
     // argument cost C4 12 % through SGPR spills, gpurun_out/r04o).
     if (c->enc_path == 0 && c->enc_stat_dev && n >= kTwoPassMinPackets && !rsk::capturing(st))
-        hipLaunchKernelGGL(k_enc_sample, dim3(1), dim3(64), 0, st, in->pay_len, n, c->enc_stat_dev);
+        hipLaunchKernelGGL(k_enc_sample, dim3(1), dim3(64), 0, st, in->pay_len, n, c->enc_stat_dev, out->frame_off,
+                           a.pad);
     return launch_check("k_encode");
 }
 
@@ -3050,14 +3374,14 @@ static int wire_path(rsk_ctx *c, uint32_t n, const uint16_t *pay_len, hipStream_
     if (ep < 0) return ep;
     const uint32_t s = sampled_mean(c);
     if (n < kTwoPassMinPackets || !(s & kStatValid)) return RSK_ENC_PATH_PER_SET;
-    const uint32_t mean = s & ~kStatValid;
+    const uint32_t mean = s & kStatMean;
     return mean < kWireTwoPassFrom || (eth && mean >= kWireEthPerSetFrom) ? RSK_ENC_PATH_PER_SET
                                                                           : RSK_ENC_PATH_TWO_PASS;
 }
 static int wire_k(rsk_ctx *c, bool eth) {
     if (c->copy_k) return c->copy_k;
     const uint32_t s = sampled_mean(c);
-    const uint32_t mean = (s & kStatValid) ? s & ~kStatValid : 1400u;
+    const uint32_t mean = (s & kStatValid) ? s & kStatMean : 1400u;
     return eth || mean < kWireK2From ? 4 : 2;
 }
 
@@ -3139,7 +3463,8 @@ int rsk_encode_wire_batch(rsk_ctx *c, uint32_t n, const rsk_encode_in *in, const
     c->enc_last_path.store(RSK_ENC_PATH_PER_SET, std::memory_order_relaxed);
     // the statistic for the next call's choice (as rsk_encode_batch)
     if (c->enc_path == 0 && c->enc_stat_dev && n >= kTwoPassMinPackets && !rsk::capturing(st))
-        hipLaunchKernelGGL(k_enc_sample, dim3(1), dim3(64), 0, st, in->pay_len, n, c->enc_stat_dev);
+        hipLaunchKernelGGL(k_enc_sample, dim3(1), dim3(64), 0, st, in->pay_len, n, c->enc_stat_dev,
+                           (const uint64_t *)nullptr, 0u);
     return launch_check("k_encode_wire");
 }
 

@@ -25,6 +25,14 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--pad16", action="store_true", help="RSK_ENC_ZERO_PAD16 (not for the byte-packed layout)")
+    ap.add_argument("--probe", action="store_true",
+                    help="also time tools/libhbm_probe.so probe_frames per layout: the encode's write pattern "
+                         "(one wave per frame, payload chunks to the frame's chunks) with byte-exact edge "
+                         "stores (exact) and with whole-chunk stores (whole)")
+    ap.add_argument("--layouts", default="", help="comma list: time only these layouts (slots is always built)")
+    ap.add_argument("--copy-k", type=int, default=0,
+                    help="rsk__set_copy_k for the two-pass form: 1 / 2 / 4 packets per copy wave, -1 the "
+                         "output-stationary copy, 0 chosen per call")
     ap.add_argument("--encode-path", type=int, default=0,
                     help="rsk_set_encode_path: 0 chosen per call, 1 per-set kernel, 2 two-pass")
     args = ap.parse_args()
@@ -41,6 +49,8 @@ def main():
     cx = rc.Codec(b"hello135", 0)
     if args.encode_path:
         cx.set_encode_path(args.encode_path)
+    if args.copy_k:
+        cx.set_copy_k(args.copy_k)
     s = torch.cuda.current_stream()
     flen = d.frame_len.astype(np.int64)
     r16 = (flen + 15) // 16 * 16
@@ -79,13 +89,30 @@ def main():
             b = ref_fr[(ref_fo[lo:hi].view(-1, 1) + idx.view(1, -1)).clamp(max=ref_fr.numel() - 1)] * m
             if not torch.equal(a, b):
                 raise SystemExit(f"layout {k}: frames differ from the slots layout in [{lo}, {hi})")
-    times = {k: [] for k in arenas}
+    keep = args.layouts.split(",") if args.layouts else list(arenas)
+    runs = {k: (lambda k=k: run(k)) for k in arenas if k in keep}
+    if args.probe:
+        import ctypes
+        L = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhbm_probe.so"))
+        L.probe_frames.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
+        sp = ctypes.c_void_p(s.cuda_stream)
+
+        def probe(k, exact):
+            fr, fo, _ = arenas[k]
+            r = L.probe_frames(w.payload.data_ptr(), fr.data_ptr(), w.pay_off.data_ptr(), fo.data_ptr(),
+                               w.pay_len.data_ptr(), n, exact, sp)
+            assert r == 0
+
+        for k in list(arenas):
+            runs[f"probe_exact:{k}"] = (lambda k=k: probe(k, 1))
+            runs[f"probe_whole:{k}"] = (lambda k=k: probe(k, 0))
+    times = {k: [] for k in runs}
     for _ in range(args.rounds):
-        for k in arenas:
+        for k, f in runs.items():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s)
             for _ in range(args.reps):
-                run(k)
+                f()
             e1.record(s)
             torch.cuda.synchronize()
             times[k].append(e0.elapsed_time(e1) / args.reps)

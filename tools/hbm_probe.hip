@@ -6,9 +6,14 @@
 //   shift2ld    dst chunk k = src bytes [16k+1, 16k+17): two 16-B loads + v_alignbyte
 //   shiftdpp    same, second operand from lane+1 via DPP wave_shl:1 (one load per chunk)
 //   strided     isolated 16- / 32-B reads at a pitch, one lane per item (decode / header-pass ceiling)
+//   frames      one wave per frame: its aligned payload chunks copied to the frame's destination chunks
+//               at any frame_off, first / last chunk stored byte-exact (as the encode) or whole
+//               (unaligned-layout ceiling)
 // Build: hipcc -O3 --offload-arch=gfx950 -shared -fPIC -o tools/libhbm_probe.so tools/hbm_probe.hip
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include "../rsock_amd/csrc/rsk_device.h"
 
 namespace {
 
@@ -110,9 +115,56 @@ __global__ __launch_bounds__(256) void k_strided(const uint8_t *__restrict__ s, 
     else if ((v.x ^ v.y ^ v.z ^ v.w) == 0x12345678u) out[0] = 1u;  // keeps the loads live
 }
 
+// The unaligned-layout ceiling (round 6): the byte ranges the encode writes for
+// frames at any frame_off, with its access shape (one wave per frame, lane k = destination chunk k,
+// the payload's aligned chunk k loaded) and none of its work (no funnel, header or MD5: wrong
+// bytes).  EXACT: the frame's first and last chunks are stored byte-exact (stores of 1-8 B, as the
+// encode's store_range16, so bytes outside the frame are never written); otherwise whole chunks
+// (bytes outside the frame overwritten: the cost of the partial chunks alone).
+template <bool EXACT>
+__global__ __launch_bounds__(256) void k_frames(const uint8_t *__restrict__ s, uint8_t *__restrict__ d,
+                                                const uint64_t *__restrict__ po, const uint64_t *__restrict__ fo,
+                                                const uint16_t *__restrict__ plen, uint64_t n) {
+    const uint64_t i = blockIdx.x * 4ull + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    if (i >= n) return;
+    const uint64_t f = fo[i], p0 = po[i] & ~15ull;
+    const uint32_t fl = 31u + plen[i], r = (uint32_t)(f & 15u);
+    const uint32_t nst = (r + fl + 15u) >> 4, last = (uint32_t)((po[i] + plen[i] - 1u - p0) >> 4);
+    uint8_t *d0 = d + (f - r);
+#pragma unroll
+    for (uint32_t q = 0; q < 2; ++q) {
+        const uint32_t k = lane + 64u * q;
+        if (k >= nst) continue;
+        const uint4 v = reinterpret_cast<const uint4 *>(s + p0)[k < last ? k : last];
+        const uint32_t lo = k == 0u ? r : 0u;
+        const int lim = (int)(r + fl) - 16 * (int)k;
+        const uint32_t hi = lim < 16 ? (uint32_t)lim : 16u;
+        if (!EXACT || (lo == 0u && hi == 16u)) {
+            *reinterpret_cast<uint4 *>(d0 + 16u * k) = v;
+            continue;
+        }
+        rsk::store_range16(d0 + 16u * k, v, lo, hi);  // the encode's edge store
+    }
+}
+
 }  // namespace
 
 extern "C" {
+// the frame-write pattern above over n frames (exact = 1: byte-exact edges)
+int probe_frames(const void *src, void *dst, const void *po, const void *fo, const void *plen, uint64_t n, int exact,
+                 void *stream) {
+    const unsigned grid = (unsigned)((n + 3) / 4);
+    hipStream_t st = (hipStream_t)stream;
+    if (exact)
+        hipLaunchKernelGGL(k_frames<true>, dim3(grid), dim3(256), 0, st, (const uint8_t *)src, (uint8_t *)dst,
+                           (const uint64_t *)po, (const uint64_t *)fo, (const uint16_t *)plen, n);
+    else
+        hipLaunchKernelGGL(k_frames<false>, dim3(grid), dim3(256), 0, st, (const uint8_t *)src, (uint8_t *)dst,
+                           (const uint64_t *)po, (const uint64_t *)fo, (const uint16_t *)plen, n);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 // the isolated-read pattern above: nb 16-B chunks per item (1 or 2), write = 1 adds a dense 16-B
 // record per item; stride in bytes (a multiple of 16)
 int probe_strided(void *src, void *dst, uint64_t n, uint64_t stride, int nb, int write, void *stream) {
