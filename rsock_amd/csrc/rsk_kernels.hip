@@ -3217,8 +3217,10 @@ static uint32_t sampled_mean(const rsk_ctx *c) {
 static int copy_k(rsk_ctx *c) {
     if (c->copy_k) return c->copy_k;
     const uint32_t s = sampled_mean(c);
-    if ((s & kStatValid) && (s & kStatPacked) && c->tp_chunk == 0u) return -1;  // frames back to back
     const uint32_t mean = (s & kStatValid) ? s & kStatMean : 1400u;
+    // byte-packed frames of the four-packet range: the output-stationary copy (C4 0.420 vs 0.429 ms);
+    // long ones keep the one-packet waves (C3 byte-packed 2.59 vs 3.01 ms: profiles/r06_layouts_os.json)
+    if ((s & kStatValid) && (s & kStatPacked) && mean < kAutoK4Below && c->tp_chunk == 0u) return -1;
     return mean < kAutoK4Below ? 4 : mean < kAutoK2Below ? 2 : 1;
 }
 

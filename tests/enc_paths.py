@@ -9,8 +9,9 @@ import contextlib
 # (path, packets per copy wave of the two-pass form; 0 = not the two-pass form)
 #   1 = the per-set kernel k_encode; 2 = the two-pass form (k_encode_heads, then k_encode_copy with k
 #   packets per wave: 1 for long frames, 4 for mid-length ones; k = -1: the output-stationary copy
-#   k_encode_os for frames laid back to back, which copies packet by packet when the header pass finds
-#   the frames out of order or far apart); 3 = the short-frame kernel (every set on the flat chunk list)
+#   k_encode_os AUTO takes for byte-packed frames, which copies packet by packet when the header pass
+#   finds the frames out of order or far apart); 3 = the short-frame kernel (every set on the flat
+#   chunk list)
 ENC_PATHS = [(1, 0), (2, 1), (2, 2), (2, 4), (2, -1), (3, 0)]
 
 
