@@ -142,7 +142,11 @@ int rsk_get_tag_mode(const rsk_ctx *ctx);
  *   RSK_ENC_PATH_PER_SET  one kernel, 64 packets per wave (every batch shape);
  *   RSK_ENC_PATH_TWO_PASS a header pass (MD5 tags 64 to a wave, 32-B records in the stream's scratch),
  *                         then copy waves of 1, 2 or 4 packets: 4 below a mean payload of 880 B, 2 below
- *                         1160 B, 1 above (batches of long frames);
+ *                         1160 B, 1 above (batches of long frames); below 880 B, when the sampled frames
+ *                         lie back to back sharing their boundary 16-B chunks (byte-packed, no pad),
+ *                         an output-stationary copy instead (waves own 2-KB blocks of the frame arena
+ *                         and write each shared chunk once; frames out of packet order or more than
+ *                         32 KB apart are copied packet by packet by the same launch);
  *   RSK_ENC_PATH_SHORT    the per-set kernel with every set on the flat chunk list (batches of short
  *                         frames).
  * Read when a call is issued, as the tag mode; RSK_EINVAL for an unknown path. */
@@ -160,7 +164,8 @@ int rsk_set_encode_path(rsk_ctx *ctx, int path);
  *
  * Pre-size the scratch of `stream` (rsk_reserve: the legacy default stream, NULL) for batches of up
  * to n packets: the compaction state and, for n >= 16384, the header records of the two-pass encode
- * and wire build (max(32 n, 96 min(n, 2^20)) bytes) -- only for a context that encodes: one held to RSK_ENC_PATH_TWO_PASS, or an AUTO
+ * and wire build (max(40 n + 24, 96 min(n, 2^20)) bytes: 32-B records and the output-stationary
+ * copy's block map) -- only for a context that encodes: one held to RSK_ENC_PATH_TWO_PASS, or an AUTO
  * context that has already run an rsk_encode_batch call (so a decode- or demux-only context pays
  * nothing for them; a failed records allocation is not an error: eager calls allocate them on demand,
  * a captured call then takes the per-set kernel).  Batch calls grow the scratch on demand, which waits
