@@ -193,6 +193,11 @@ int rsk_release_stream(rsk_ctx *ctx, void *stream);
  * set it returns RSK_EDEVICE and re-initialises the context's look-back state on every stream at its
  * next call there (graphs captured earlier must be captured again). */
 #define RSK_DEVERR_LOOKBACK 0x1u
+/* RSK_DEVERR_TABLE: a demux key probe walked the whole key table without finding its key or a free
+ * slot (the table is kept all-ones between calls, each call clearing the slots it claimed; a table
+ * left dirty -- which no completed call does -- would otherwise hang the probe): that call's demux
+ * outputs are wrong, and the table is filled again at the next call. */
+#define RSK_DEVERR_TABLE 0x2u
 int rsk_check_device_errors(rsk_ctx *ctx, uint32_t *flags);
 /* The caller has destroyed every graph that captured this context's calls (or replays them only on
  * streams this context has scratch on): rsk_check_device_errors waits for the context's streams

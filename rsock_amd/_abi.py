@@ -37,6 +37,7 @@ PARSE_HAS_ACK_POOL, PARSE_IS_SERVER = 0x1, 0x2
 FILTER_MAX_PORTS = 64
 TAG_MD5, TAG_TABLE = 0, 1
 DEVERR_LOOKBACK = 0x1
+DEVERR_TABLE = 0x2
 DEMUX_ID, DEMUX_CONN_KEY, DEMUX_CONV, DEMUX_DST, DEMUX_CMD_BARRIER = 0x01, 0x02, 0x04, 0x08, 0x10
 DEMUX_GROUP_BARRIER = 0x20
 

@@ -23,7 +23,9 @@ enum WsKind { WS_COMPACT = 0, WS_SEQ = 1, WS_DEMUX = 2, WS_ENC = 3, WS_KINDS = 4
 struct WsBuf {
     void *p = nullptr;
     size_t bytes = 0;
-    bool zeroed = false;  // WS_COMPACT: zero-filled since (re)allocation (see stream_compact)
+    // WS_COMPACT: zero-filled since (re)allocation (see stream_compact); WS_DEMUX: its table flag word
+    // was initialised (rsk_demux.hip k_dm_fill / k_dm_final keep it from there)
+    bool zeroed = false;
 };
 }  // namespace rsk
 
@@ -43,7 +45,7 @@ struct rsk_ctx {
     // host-mapped word the batch statistic is stored to (enc_sample: k_encode_heads, k_enc_sample) and
     // its device address; read without synchronisation by later calls (a stale value only picks the
     // slower path, never different bytes)
-    uint32_t *enc_stat_host = nullptr;
+    uint32_t *enc_stat_host = nullptr;  // [2]: the batch statistic, then the demux's table hint (rsk_demux.hip)
     uint32_t *enc_stat_dev = nullptr;
     std::vector<uint8_t> key;
     rsk::KeySched ks;
@@ -178,7 +180,20 @@ inline int stream_compact(rsk_ctx *c, hipStream_t s, size_t words, unsigned long
 // call's epoch: every stream's compaction state is zeroed again at its next use.
 inline void invalidate_compact(rsk_ctx *c) {
     std::lock_guard<std::mutex> lk(c->ws_mu);
-    for (auto &kv : c->ws) kv.second[WS_COMPACT].zeroed = false;
+    for (auto &kv : c->ws) {
+        kv.second[WS_COMPACT].zeroed = false;
+        kv.second[WS_DEMUX].zeroed = false;  // a demux call that gave up may leave slots claimed: fill again
+    }
+}
+
+// The `zeroed` flag of stream s's `kind` scratch (after stream_ws sized it), under the lock.
+inline bool ws_clean(rsk_ctx *c, hipStream_t s, int kind) {
+    std::lock_guard<std::mutex> lk(c->ws_mu);
+    return c->ws[s][kind].zeroed;
+}
+inline void set_ws_clean(rsk_ctx *c, hipStream_t s, int kind, bool v) {
+    std::lock_guard<std::mutex> lk(c->ws_mu);
+    c->ws[s][kind].zeroed = v;
 }
 
 // Wait for the work whose device error flags rsk_check_device_errors reads.  Normally the streams

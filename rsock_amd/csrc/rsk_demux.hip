@@ -11,7 +11,9 @@
 // Pipeline (all stream-ordered, no host sync; n_valid and the segment count stay on the device),
 // 5 + passes launches after one fill (round 2: the block scans are decoupled look-backs inside the
 // kernels that produce the counts, and the radix sort is onesweep, one launch per pass):
-//   fill            key table + look-back state words to all-ones
+//   k_dm_fill       look-back state words to all-ones, and the key table unless the previous call on
+//                   this scratch left it clean (round 6: k_dm_final clears the slots of batches with
+//                   few segments)
 //   k_dm_flags_prep per-wave ballots of VALID and VALID-control packets, block offsets by look-back;
 //                   cidx[j] = packet of compacted slot j; with CMD_BARRIER pep[packet] = its epoch
 //                   (CTRL for singletons; without, every epoch is 0 and nothing is stored)
@@ -276,14 +278,18 @@ __device__ __forceinline__ uint64_t key_hash(const Key &k) {
 // epoch, so its epoch is checked by its index instead of a third gather (round 5)
 __device__ __forceinline__ uint32_t global_probe(const DmIn &a,
                                                  unsigned long long *slots, uint32_t mask, const Key &k,
-                                                 uint64_t hv, uint32_t j, uint32_t es, uint32_t ee) {
+                                                 uint64_t hv, uint32_t j, uint32_t es, uint32_t ee, uint32_t *err) {
     // j is the packet index (monotone with the compacted index, so the minimum is the same packet):
     // a slot's owner is confirmed on the inputs at that index directly (round 5: one dependent
     // gather less than through the compacted index, C3 0.400 -> 0.372 ms with the 512-packet tiles)
     const uint32_t fp = (uint32_t)(hv >> 32);
     const unsigned long long mine = ((unsigned long long)fp << 32) | j;
     uint32_t h = (uint32_t)hv & mask;
-    for (;;) {
+    for (uint32_t walked = 0;; ++walked) {
+        if (walked > mask) {  // the whole table: it was not clean (RSK_DEVERR_TABLE), give up, no hang
+            __hip_atomic_fetch_or(err, RSK_DEVERR_TABLE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return h;
+        }
         unsigned long long e = __hip_atomic_load(slots + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (e == ~0ull) {
             e = atomicCAS(slots + h, ~0ull, mine);
@@ -321,7 +327,7 @@ constexpr uint32_t kLtab = 2 * kInsTile;           // LDS table slots (power of 
 
 __global__ __launch_bounds__(kBlock) void k_dm_insert(DmIn a, const uint32_t *nvp, const uint32_t *cidx,
                                                       unsigned long long *slots,
-                                                      uint32_t mask, uint32_t *hslot) {
+                                                      uint32_t mask, uint32_t *hslot, uint32_t *err) {
     __shared__ unsigned long long ltab[kLtab];
     __shared__ uint32_t lmin[kLtab];  // block-minimum index per key, then (phase 2b) the key's global slot
     __shared__ uint32_t elo, ehi;     // epochs of the tile's first and last data packets
@@ -418,7 +424,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_insert(DmIn a, const uint32_t *nv
         const Key &k = kr[it];
         const bool lo = k.ep == elo;
         lmin[lpos[it]] = (lo || k.ep == ehi)
-                             ? global_probe(a, slots, mask, k, key_hash(k), j, erng[lo ? 0 : 2], erng[lo ? 1 : 3])
+                             ? global_probe(a, slots, mask, k, key_hash(k), j, erng[lo ? 0 : 2], erng[lo ? 1 : 3], err)
                              : kLeadTag | j;
     }
     __syncthreads();
@@ -551,8 +557,9 @@ __global__ __launch_bounds__(kBlock) void k_dm_flags_prep(DmIn a, unsigned long 
 __global__ __launch_bounds__(kBlock) void k_dm_leader_rank(const uint32_t *nvp, const uint32_t *hslot,
                                                            const unsigned long long *slots, const uint32_t *cidx,
                                                            unsigned long long *st_l, uint32_t *fkey, uint32_t *fval,
-                                                           uint32_t *rank_at, uint32_t *seg_first, uint32_t *nsegp,
-                                                           uint32_t *ghist, uint32_t *err) {
+                                                           uint32_t *rank_at, uint32_t *seg_first, uint32_t *seg_slot,
+                                                           uint32_t tsize, uint32_t *nsegp, uint32_t *ghist,
+                                                           uint32_t *err) {
     __shared__ uint64_t ml[kRows][kWaves];
     __shared__ uint32_t pre;
     const uint32_t nv = *nvp;
@@ -613,6 +620,9 @@ __global__ __launch_bounds__(kBlock) void k_dm_leader_rank(const uint32_t *nvp, 
         if ((isl >> r) & 1u) {
             rank_at[pk] = before;  // by packet index: followers name their leader by it
             seg_first[before] = pk;
+            // the table slot its key claimed (k_dm_final clears it), if the key went to the table; past
+            // the clearing limit (k_dm_final: n_seg <= tsize / 16) the next call fills the table instead
+            if (before <= (tsize >> 4)) seg_slot[before] = hs[r] == kNone || (hs[r] & kLeadTag) ? kNone : hs[r];
         } else {
             fkey[j - before] = lead[r];
             fval[j - before] = pk;
@@ -821,17 +831,25 @@ __global__ __launch_bounds__(kBlock) void k_dm_final(const uint32_t *nvp, const 
                                                      const uint32_t *vA, const uint32_t *kB, const uint32_t *vB,
                                                      const uint32_t *seg_first, uint32_t *perm, uint32_t *seg_off,
                                                      uint32_t *n_seg, uint32_t *n_valid, const uint8_t *gcmd,
-                                                     uint32_t *gflag, uint32_t *gseg) {
+                                                     uint32_t *gflag, uint32_t *gseg, const uint32_t *seg_slot,
+                                                     unsigned long long *slots, uint32_t tsize, uint32_t *tflag,
+                                                     uint32_t *hint) {
     const uint32_t nv = *nvp, ns = *nsegp, nf = nv - ns;
     const uint32_t passes = n_passes(ns);  // effective passes; pass p writes B when p is even
     const bool inB = nf > kSmallF && ((passes - 1u) & 1u) == 0u;  // small: sorted in place in A
     const uint32_t *keys = inB ? kB : kA;
     const uint32_t *vals = inB ? vB : vA;
     const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
+    // few segments: clear the slots their keys claimed and mark the table clean for the next call of
+    // this size; many (up to one per packet): leave it to the next call's fill (scattered 8-B clears
+    // of 3.4 M slots cost more than the 64-MB fill: server shape 0.474 -> 0.500 ms)
+    const bool clear = ns <= (tsize >> 4);
     if (k == 0) {
         *n_seg = ns;
         *n_valid = nv;
         seg_off[ns] = nv;
+        *tflag = clear ? tsize : 0u;
+        if (hint) __hip_atomic_store(hint, clear ? tsize : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     if (k < ns) {
         uint32_t lo = 0, hi = nf;  // followers with segment id < k
@@ -842,6 +860,12 @@ __global__ __launch_bounds__(kBlock) void k_dm_final(const uint32_t *nvp, const 
         }
         seg_off[k] = k + lo;
         perm[k + lo] = seg_first[k];
+        // every slot the call claimed belongs to one key, hence one leader: all-ones again for the
+        // next call (round 6: instead of a fill of the whole table, 12.5 us for C3's 64 MB)
+        if (clear) {
+            const uint32_t ss = seg_slot[k];
+            if (ss != kNone) slots[ss] = ~0ull;
+        }
         if (gflag) {  // GROUP_BARRIER's first pass: per position, control flag and segment id
             gflag[k + lo] = gcmd[seg_first[k]] != RSK_CMD_DATA ? 1u : 0u;
             gseg[k + lo] = k;
@@ -856,14 +880,27 @@ __global__ __launch_bounds__(kBlock) void k_dm_final(const uint32_t *nvp, const 
     }
 }
 
+// The per-call fill: the look-back state words always, the key table unless the last call on this
+// scratch left it clean for this table size (*tflag == tsize, k_dm_final).  16-B stores, grid-stride.
+__global__ __launch_bounds__(kBlock) void k_dm_fill(const uint32_t *tflag, uint32_t tsize, uint4 *slots,
+                                                    uint64_t slot16, uint4 *states, uint64_t state16) {
+    const bool table = *tflag != tsize;  // uniform
+    const uint4 ones = make_uint4(~0u, ~0u, ~0u, ~0u);
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < state16; i += stride) states[i] = ones;
+    if (table)
+        for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < slot16; i += stride) slots[i] = ones;
+}
+
 // ---- workspace ------------------------------------------------------------------------------
 struct DmWs {
-    uint32_t *cidx, *hslot, *rank_at, *pep, *cpos;
+    uint32_t *cidx, *hslot, *rank_at, *pep, *cpos, *seg_slot;
     uint32_t *kA, *vA, *kB, *vB;
     uint32_t *ghist;
-    unsigned long long *slots;  // slots | look-back states: one 0xff fill per call
+    unsigned long long *slots;  // the key table, then the look-back states (k_dm_fill)
     unsigned long long *st_v, *st_c, *st_l, *st_r;
-    size_t fill_bytes;
+    size_t state_bytes;
+    uint32_t *tflag;  // == tsize: the table is all-ones for this size (k_dm_final), else the fill writes it
     uint32_t *nv, *nseg;
     uint32_t nb, nt, tsize;
 };
@@ -883,11 +920,13 @@ size_t dm_layout(uint32_t n, uint8_t *base, DmWs *w) {
         return p;
     };
     DmWs d;
+    d.tflag = (uint32_t *)take(8);  // first, at a fixed place for every batch size
     d.cidx = (uint32_t *)take(4ull * n);
     d.hslot = (uint32_t *)take(4ull * n);
     d.rank_at = (uint32_t *)take(4ull * n);
     d.pep = (uint32_t *)take(4ull * n);
     d.cpos = (uint32_t *)take(4ull * n + 4ull);
+    d.seg_slot = (uint32_t *)take(4ull * n);
     d.kA = (uint32_t *)take(4ull * n);
     d.vA = (uint32_t *)take(4ull * n);
     d.kB = (uint32_t *)take(4ull * n);
@@ -895,13 +934,13 @@ size_t dm_layout(uint32_t n, uint8_t *base, DmWs *w) {
     d.ghist = (uint32_t *)take(4ull * 4 * 256);
     d.nv = (uint32_t *)take(8);
     d.nseg = (uint32_t *)take(8);
-    const size_t fill0 = off;
     d.slots = (unsigned long long *)take(8ull * T);
+    const size_t st0 = off;
     d.st_v = (unsigned long long *)take(8ull * nt);
     d.st_c = (unsigned long long *)take(8ull * nt);
     d.st_l = (unsigned long long *)take(8ull * nt);
     d.st_r = (unsigned long long *)take(8ull * 4 * 256 * nt);
-    d.fill_bytes = off - fill0;
+    d.state_bytes = off - st0;
     d.nb = nb;
     d.nt = nt;
     d.tsize = T;
@@ -930,16 +969,36 @@ __global__ __launch_bounds__(kBlock) void k_dm_gep(const uint32_t *nvp, const ui
 int demux_pass(rsk_ctx *c, const DmIn &a, const DmWs &w, const rsk_demux_out *out, hipStream_t s,
                uint32_t *gflag = nullptr, uint32_t *gseg = nullptr) {
     const uint32_t n = a.n;
-    // one fill: the key table and every look-back state word start as all-ones
-    hipError_t e = hipMemsetAsync(w.slots, 0xff, w.fill_bytes, s);
-    if (e != hipSuccess) { rsk::set_error("hipMemsetAsync(table)", e); return RSK_EDEVICE; }
     int r;
+    // the look-back state words start as all-ones, and so does the key table, unless the last call
+    // left it clean for this size (k_dm_final clears the slots of batches with few segments); fresh
+    // scratch (or scratch after a device error) gets its flag word reset first
+    if (!rsk::ws_clean(c, s, rsk::WS_DEMUX)) {
+        hipError_t e = hipMemsetAsync(w.tflag, 0, 4, s);
+        if (e != hipSuccess) { rsk::set_error("hipMemsetAsync(table flag)", e); return RSK_EDEVICE; }
+        rsk::set_ws_clean(c, s, rsk::WS_DEMUX, true);
+    }
+    // the host-mapped hint (k_dm_final's last verdict, read without synchronisation) picks the form:
+    // likely dirty -> one memset of table and states (a blit, faster than the kernel: C4 0.080 vs
+    // 0.085 ms); likely clean -> k_dm_fill, which checks the device flag itself (a stale hint is only
+    // slower, never wrong)
+    uint32_t *hint = c->enc_stat_dev ? c->enc_stat_dev + 1 : nullptr;
+    const bool likely_clean = c->enc_stat_host && __atomic_load_n(c->enc_stat_host + 1, __ATOMIC_RELAXED) == w.tsize;
+    if (!likely_clean) {
+        hipError_t e = hipMemsetAsync(w.slots, 0xff, (size_t)w.tsize * 8u + w.state_bytes, s);
+        if (e != hipSuccess) { rsk::set_error("hipMemsetAsync(table)", e); return RSK_EDEVICE; }
+    } else {
+        const uint64_t slot16 = ((uint64_t)w.tsize * 8u) / 16u, state16 = w.state_bytes / 16u;
+        const unsigned fg = (unsigned)std::min<uint64_t>(4096u, (slot16 + kBlock - 1) / kBlock);
+        hipLaunchKernelGGL(k_dm_fill, dim3(fg), dim3(kBlock), 0, s, w.tflag, w.tsize, reinterpret_cast<uint4 *>(w.slots),
+                           slot16, reinterpret_cast<uint4 *>(w.st_v), state16);
+    }
     hipLaunchKernelGGL(k_dm_flags_prep, dim3(w.nt), dim3(kBlock), 0, s, a, w.st_v, w.st_c, w.cidx, w.nv,
                        c->err_dev);
     hipLaunchKernelGGL(k_dm_insert, dim3((n + kInsTile - 1) / kInsTile), dim3(kBlock), 0, s, a, w.nv, w.cidx,
-                       w.slots, w.tsize - 1u, w.hslot);
+                       w.slots, w.tsize - 1u, w.hslot, c->err_dev);
     hipLaunchKernelGGL(k_dm_leader_rank, dim3(w.nt), dim3(kBlock), 0, s, w.nv, w.hslot, w.slots, w.cidx, w.st_l,
-                       w.kA, w.vA, w.rank_at, out->seg_first, w.nseg, w.ghist, c->err_dev);
+                       w.kA, w.vA, w.rank_at, out->seg_first, w.seg_slot, w.tsize, w.nseg, w.ghist, c->err_dev);
     hipLaunchKernelGGL(k_dm_segof_hist, dim3(w.nt), dim3(kBlock), 0, s, w.nv, w.nseg, w.rank_at, w.kA, w.vA,
                        w.ghist);
     if ((r = rsk::launch_check("k_dm_segof_hist"))) return r;
@@ -955,7 +1014,8 @@ int demux_pass(rsk_ctx *c, const DmIn &a, const DmWs &w, const rsk_demux_out *ou
         if ((r = rsk::launch_check("k_dm_onesweep"))) return r;
     }
     hipLaunchKernelGGL(k_dm_final, dim3(w.nb), dim3(kBlock), 0, s, w.nv, w.nseg, w.kA, w.vA, w.kB, w.vB,
-                       out->seg_first, out->perm, out->seg_off, out->n_seg, out->n_valid, a.cmd, gflag, gseg);
+                       out->seg_first, out->perm, out->seg_off, out->n_seg, out->n_valid, a.cmd, gflag, gseg,
+                       w.seg_slot, w.slots, w.tsize, w.tflag, hint);
     return rsk::launch_check("k_dm_final");
 }
 

@@ -3045,9 +3045,11 @@ rsk_ctx *rsk_create(const uint8_t *key, uint32_t key_len, int device) {
     if (e == hipSuccess) e = hipMemset(c->err_dev, 0, sizeof(uint32_t));
     // the encode path statistic's host-mapped word (enc_path); without it every call takes the per-set
     // kernel unless a path is forced -- not an error
-    if (e == hipSuccess && hipHostMalloc(reinterpret_cast<void **>(&c->enc_stat_host), sizeof(uint32_t),
+    // (word 1: the demux's table hint, rsk_demux.hip demux_pass)
+    if (e == hipSuccess && hipHostMalloc(reinterpret_cast<void **>(&c->enc_stat_host), 2 * sizeof(uint32_t),
                                          hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
-        *c->enc_stat_host = 0u;
+        c->enc_stat_host[0] = 0u;
+        c->enc_stat_host[1] = 0u;
         if (hipHostGetDevicePointer(reinterpret_cast<void **>(&c->enc_stat_dev), c->enc_stat_host, 0) != hipSuccess) {
             (void)hipHostFree(c->enc_stat_host);
             c->enc_stat_host = nullptr;
@@ -3168,7 +3170,9 @@ int rsk_check_device_errors(rsk_ctx *c, uint32_t *flags) {
     if (flags) *flags = f;
     if (!f) return RSK_OK;
     rsk::invalidate_compact(c);
-    snprintf(g_last_error, sizeof g_last_error, "device error flags 0x%x (RSK_DEVERR_LOOKBACK: a look-back gave up)", f);
+    snprintf(g_last_error, sizeof g_last_error,
+             "device error flags 0x%x (RSK_DEVERR_LOOKBACK: a look-back gave up; RSK_DEVERR_TABLE: a demux "
+             "probe found no slot)", f);
     return RSK_EDEVICE;
 }
 

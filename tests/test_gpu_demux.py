@@ -239,3 +239,19 @@ def test_demux_group_barrier_server_shapes(codec, gpu, oracle, n, groups, p_ctrl
     assert got == exp[0]
     if groups >= 64 and p_ctrl >= 0.002:
         assert len(got) < len(oracle.demux_batch(status, cmd, D.SERVER_FIELDS, ids, conv, ckey, dst)[0]) // 2
+
+
+def test_demux_table_reuse(codec, gpu, oracle):
+    """The key table is filled only when it is not known clean: every call clears the slots its keys
+    claimed (k_dm_final), so back-to-back calls reuse it.  Same size with other keys, a larger batch
+    (the table moves in the scratch), the first size again, and the group barrier's two passes in
+    between: every result equals the oracle."""
+    seq = [(70000, 300, ALL), (70000, 5000, ALL | A.DEMUX_CMD_BARRIER), (70000, 70000, A.DEMUX_CONN_KEY),
+           (150000, 40, ALL | A.DEMUX_GROUP_BARRIER), (70000, 300, ALL), (1000, 10, A.DEMUX_CONV),
+           (70000, 2000, ALL | A.DEMUX_CMD_BARRIER)]
+    for k, (n, nkeys, fields) in enumerate(seq):
+        rng = np.random.default_rng(100 + k)
+        case = make_case(rng, n, nkeys, 0.02, 0.9)
+        got = run_gpu(codec, gpu, *case[:2], fields, *case[2:])
+        exp = oracle.demux_batch(case[0], case[1], fields, *case[2:])
+        assert got[1] == exp[1] and got[0] == exp[0], (k, n, fields)
