@@ -253,9 +253,9 @@ typedef struct rsk_encode_out {
  * calls issued back to back see it late, which only delays a switch of traffic mix); the first such call
  * on a context, which has no statistic yet, samples its own batch with one 64-thread launch on
  * `stream` and waits for an event recorded behind it -- i.e. for `stream`'s work up to that launch,
- * since a stream runs in order; a failed wait returns RSK_EDEVICE.  A call being captured does not
- * wait (it takes the per-set kernel); on the legacy NULL stream, as for any launch there, no other
- * stream may be capturing in hipStreamCaptureModeGlobal meanwhile.  A call
+ * since a stream runs in order (with this thread's capture mode relaxed for the wait); a failed
+ * wait returns RSK_EDEVICE.  A call being captured, or issued on the legacy NULL stream, does not
+ * wait: it takes the per-set kernel, and the sample launched behind it decides the next calls.  A call
  * captured into a hipGraph keeps the path it was captured with, and one captured on a stream without
  * reserved records takes the per-set kernel.  rsk_set_encode_path fixes the path for a context
  * (e.g. one fed alternating long- and short-frame batches). */

@@ -3238,13 +3238,22 @@ static int copy_k(rsk_ctx *c) {
 static int enc_path(rsk_ctx *c, uint32_t n, const uint16_t *pay_len, hipStream_t st,
                     const uint64_t *frame_off = nullptr, uint32_t pad = 0u) {
     if (c->enc_path) return c->enc_path;
-    if (n >= kTwoPassMinPackets && c->enc_stat_dev && !(sampled_mean(c) & kStatValid) && !rsk::capturing(st)) {
+    // Not on the legacy NULL stream: work there synchronises with every blocking stream, so
+    // the wait could join -- and invalidate -- another stream's capture; its first call takes the
+    // per-set kernel and the sample launched behind it serves the next calls.  Elsewhere the wait runs
+    // with this thread's capture mode relaxed, so another thread's global-mode capture does not turn it
+    // into an error (the event and the sample are on this call's own, uncaptured stream).
+    if (n >= kTwoPassMinPackets && c->enc_stat_dev && !(sampled_mean(c) & kStatValid) && st != nullptr &&
+        !rsk::capturing(st)) {
         hipLaunchKernelGGL(k_enc_sample, dim3(1), dim3(64), 0, st, pay_len, n, c->enc_stat_dev, frame_off, pad);
+        hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+        const bool swapped = hipThreadExchangeStreamCaptureMode(&mode) == hipSuccess;
         hipEvent_t ev = nullptr;
         hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventRecord(ev, st);
         if (e == hipSuccess) e = hipEventSynchronize(ev);
         if (ev) (void)hipEventDestroy(ev);
+        if (swapped) (void)hipThreadExchangeStreamCaptureMode(&mode);  // restore the caller's mode
         if (e != hipSuccess) { set_error("enc_path: waiting for the batch sample", e); return RSK_EDEVICE; }
     }
     const uint32_t s = sampled_mean(c);

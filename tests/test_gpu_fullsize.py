@@ -92,14 +92,32 @@ def test_encode_path_first_call(gpu, cfg):
     d = workload.describe(cfg, 0, 40_000, n=40_000)
     w = workload.DeviceWorkload(d, gpu)
     path, k = AUTO_EXPECT[cfg]
+    s = torch.cuda.Stream(gpu)
+    torch.cuda.synchronize()
     c = Codec(b"hello135", 0)
     try:
         for call in range(3):
             c.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
-                           w.status, id_uniform=workload.ID_UNIFORM, pad16=True)
+                           w.status, id_uniform=workload.ID_UNIFORM, pad16=True, stream=s)
             assert c.last_encode_path == path, (cfg, call, c.last_encode_path)
             if path == 2:
                 assert c.last_copy_k == k, (cfg, call, c.last_copy_k)
+        torch.cuda.synchronize()
+        assert torch.equal(w.status.to(torch.int64), (w.pay_len.to(torch.int64) & 0xFFFF) + 31)
+    finally:
+        c.close()
+    # on the legacy NULL stream the first call does not wait: it takes the per-set kernel
+    # (same bytes), and once its sample has landed the table's path follows
+    c = Codec(b"hello135", 0)
+    try:
+        null = 0  # the legacy NULL stream
+        c.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
+                       w.status, id_uniform=workload.ID_UNIFORM, pad16=True, stream=null)
+        assert c.last_encode_path == 1, (cfg, c.last_encode_path)
+        torch.cuda.synchronize()
+        c.output_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, w.frame, w.frame_off,
+                       w.status, id_uniform=workload.ID_UNIFORM, pad16=True, stream=null)
+        assert c.last_encode_path == path, (cfg, c.last_encode_path)
         torch.cuda.synchronize()
         assert torch.equal(w.status.to(torch.int64), (w.pay_len.to(torch.int64) & 0xFFFF) + 31)
     finally:

@@ -204,12 +204,14 @@ def test_wire_auto_path(gpu, cfg, eth, exp):
     woff = torch.arange(n, device=gpu, dtype=torch.int64) * pitch
     st = torch.empty(n, dtype=torch.int32, device=gpu)
     cx = Codec(KEY, 0)
+    s = torch.cuda.Stream(gpu)  # (on the legacy NULL stream a fresh context's first call does not wait)
+    torch.cuda.synchronize()
     try:
         for _ in range(2):
             cx.output_wire_batch(w.payload, w.pay_off, w.pay_len, w.cmd, w.conv, w.conn_key, z(torch.int32),
                                  z(torch.int32), z(torch.int16), z(torch.int16), z(torch.int32), z(torch.int32),
                                  z(torch.uint8), z(torch.int16), wire, woff, st, eth=bytes(14) if eth else None,
-                                 id_uniform=workload.ID_UNIFORM, pad128=True)
+                                 id_uniform=workload.ID_UNIFORM, pad128=True, stream=s)
             got = (cx.last_encode_path, cx.last_copy_k if cx.last_encode_path == 2 else 0)
             assert got == exp, (cfg, eth, got)
         torch.cuda.synchronize()
