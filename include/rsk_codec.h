@@ -470,7 +470,8 @@ typedef struct rsk_demux_out {
     uint32_t *n_valid;   /* [1]                                                                   */
 } rsk_demux_out;
 /* n <= 2^30.  Workspace (per stream, grown on demand): about 75 B per packet.  GROUP_BARRIER runs
- * two group-bys (by IdBuf, then by the key with each DATA packet's epoch inside its IdBuf), writing
+ * two group-bys (the control packets by IdBuf, then every packet by the key with each DATA packet's
+ * epoch inside its IdBuf), writing
  * the first one's result to `out` before the second overwrites it. */
 int rsk_demux_batch(rsk_ctx *ctx, uint32_t n, const rsk_demux_in *in, uint32_t fields,
                     const rsk_demux_out *out, void *stream);

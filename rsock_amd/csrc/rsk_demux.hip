@@ -830,10 +830,9 @@ __global__ __launch_bounds__(kBlock) void k_dm_onesweep(uint32_t pass, const uin
 __global__ __launch_bounds__(kBlock) void k_dm_final(const uint32_t *nvp, const uint32_t *nsegp, const uint32_t *kA,
                                                      const uint32_t *vA, const uint32_t *kB, const uint32_t *vB,
                                                      const uint32_t *seg_first, uint32_t *perm, uint32_t *seg_off,
-                                                     uint32_t *n_seg, uint32_t *n_valid, const uint8_t *gcmd,
-                                                     uint32_t *gflag, uint32_t *gseg, const uint32_t *seg_slot,
-                                                     unsigned long long *slots, uint32_t tsize, uint32_t *tflag,
-                                                     uint32_t *hint) {
+                                                     uint32_t *n_seg, uint32_t *n_valid, const uint32_t *seg_slot,
+                                                     unsigned long long *slots, uint32_t tsize, uint32_t clear_max,
+                                                     uint32_t *tflag, uint32_t *hint) {
     const uint32_t nv = *nvp, ns = *nsegp, nf = nv - ns;
     const uint32_t passes = n_passes(ns);  // effective passes; pass p writes B when p is even
     const bool inB = nf > kSmallF && ((passes - 1u) & 1u) == 0u;  // small: sorted in place in A
@@ -843,7 +842,7 @@ __global__ __launch_bounds__(kBlock) void k_dm_final(const uint32_t *nvp, const 
     // few segments: clear the slots their keys claimed and mark the table clean for the next call of
     // this size; many (up to one per packet): leave it to the next call's fill (scattered 8-B clears
     // of 3.4 M slots cost more than the 64-MB fill: server shape 0.474 -> 0.500 ms)
-    const bool clear = ns <= (tsize >> 4);
+    const bool clear = ns <= clear_max;
     if (k == 0) {
         *n_seg = ns;
         *n_valid = nv;
@@ -866,18 +865,8 @@ __global__ __launch_bounds__(kBlock) void k_dm_final(const uint32_t *nvp, const 
             const uint32_t ss = seg_slot[k];
             if (ss != kNone) slots[ss] = ~0ull;
         }
-        if (gflag) {  // GROUP_BARRIER's first pass: per position, control flag and segment id
-            gflag[k + lo] = gcmd[seg_first[k]] != RSK_CMD_DATA ? 1u : 0u;
-            gseg[k + lo] = k;
-        }
     }
-    if (k < nf) {
-        perm[keys[k] + 1u + k] = vals[k];
-        if (gflag) {
-            gflag[keys[k] + 1u + k] = gcmd[vals[k]] != RSK_CMD_DATA ? 1u : 0u;
-            gseg[keys[k] + 1u + k] = keys[k];
-        }
-    }
+    if (k < nf) perm[keys[k] + 1u + k] = vals[k];
 }
 
 // The per-call fill: the look-back state words always, the key table unless the last call on this
@@ -949,25 +938,57 @@ size_t dm_layout(uint32_t n, uint8_t *base, DmWs *w) {
 }
 
 // ---- GROUP_BARRIER: each DATA packet's epoch inside its IdBuf -------------------------------
-// After the first pass (key = IdBuf alone, no barrier) perm lists every IdBuf's packets in arrival
-// order, segment by segment, and k_dm_final wrote gflag[j] = perm[j] is a control packet and gseg[j]
-// = its segment.  An exclusive scan of gflag over perm order minus its value at the segment's start
-// counts the control packets of the same IdBuf before each packet: that count is a DATA packet's key
-// word in the second pass, and a control packet gets kLeadTag | its own index, a key no other packet
-// has (a singleton segment).
-__global__ __launch_bounds__(kBlock) void k_dm_gep(const uint32_t *nvp, const uint32_t *perm, const uint32_t *seg_off,
-                                                   const uint32_t *gflag, const uint32_t *gseg, const uint32_t *pre,
-                                                   uint32_t *xep) {
-    const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
-    if (j >= *nvp) return;
-    const uint32_t p = perm[j];
-    xep[p] = gflag[j] ? (kLeadTag | p) : pre[j] - pre[seg_off[gseg[j]]];
+// The first pass groups only the VALID CONTROL packets by IdBuf (k_dm_gstatus hides every other
+// packet), so its table maps an IdBuf to the first control packet of that IdBuf and its segments list
+// each IdBuf's control packets in arrival order.  k_dm_gep then gives every VALID DATA packet i the
+// number of its IdBuf's control packets before it -- a probe of that table by IdBuf, the segment of
+// the owner, a binary search of i among the segment's packet indices -- as its key word for the
+// second pass; a control packet gets kLeadTag | its own index, a key no other packet has (a
+// singleton segment).  (First build: a group-by of every packet by IdBuf and a scan, 0.82 ms on the
+// server shape.)
+__global__ __launch_bounds__(kBlock) void k_dm_gstatus(const int8_t *status, const uint8_t *cmd, uint32_t n,
+                                                       int8_t *st2) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) st2[i] = status[i] == RSK_RECV_VALID && cmd[i] != RSK_CMD_DATA ? (int8_t)RSK_RECV_VALID
+                                                                            : (int8_t)RSK_RECV_DROP;
+}
+__global__ __launch_bounds__(kBlock) void k_dm_gep(DmIn a, const unsigned long long *slots, uint32_t mask,
+                                                   const uint32_t *rank_at, const uint32_t *perm,
+                                                   const uint32_t *seg_off, uint32_t *xep, uint32_t *err) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= a.n || a.status[i] != RSK_RECV_VALID) return;
+    if (a.cmd[i] != RSK_CMD_DATA) {
+        xep[i] = kLeadTag | i;
+        return;
+    }
+    const Key k = load_key(a, i, 0u);  // the IdBuf alone (a.fields = RSK_DEMUX_ID, no epoch, no word)
+    const uint64_t hv = key_hash(k);
+    const uint32_t fp = (uint32_t)(hv >> 32);
+    uint32_t h = (uint32_t)hv & mask, cnt = 0;
+    for (uint32_t walked = 0; walked <= mask; ++walked) {  // read-only probe: the table is complete
+        const unsigned long long e = slots[h];
+        if (e == ~0ull) break;  // no control packet of this IdBuf
+        if ((uint32_t)(e >> 32) == fp && a.id[(uint32_t)e] == k.id) {
+            const uint32_t sg = rank_at[(uint32_t)e];
+            uint32_t lo = seg_off[sg], hi = seg_off[sg + 1u];  // the IdBuf's control packets, in order
+            while (lo < hi) {  // how many of them precede i
+                const uint32_t mid = (lo + hi) >> 1;
+                if (perm[mid] < i) lo = mid + 1u;
+                else hi = mid;
+            }
+            cnt = lo - seg_off[sg];
+            break;
+        }
+        h = (h + 1u) & mask;
+        if (walked == mask) __hip_atomic_fetch_or(err, RSK_DEVERR_TABLE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    xep[i] = cnt;
 }
 
-// One group-by pass over the batch (the whole rsk_demux_batch without GROUP_BARRIER); with gflag,
-// k_dm_final also writes each position's control flag and segment id (GROUP_BARRIER's first pass).
+// One group-by pass over the batch (the whole rsk_demux_batch without GROUP_BARRIER); keep_table:
+// k_dm_final leaves the key table as it is (GROUP_BARRIER's first pass: k_dm_gep reads it).
 int demux_pass(rsk_ctx *c, const DmIn &a, const DmWs &w, const rsk_demux_out *out, hipStream_t s,
-               uint32_t *gflag = nullptr, uint32_t *gseg = nullptr) {
+               bool keep_table = false) {
     const uint32_t n = a.n;
     int r;
     // the look-back state words start as all-ones, and so does the key table, unless the last call
@@ -1014,8 +1035,8 @@ int demux_pass(rsk_ctx *c, const DmIn &a, const DmWs &w, const rsk_demux_out *ou
         if ((r = rsk::launch_check("k_dm_onesweep"))) return r;
     }
     hipLaunchKernelGGL(k_dm_final, dim3(w.nb), dim3(kBlock), 0, s, w.nv, w.nseg, w.kA, w.vA, w.kB, w.vB,
-                       out->seg_first, out->perm, out->seg_off, out->n_seg, out->n_valid, a.cmd, gflag, gseg,
-                       w.seg_slot, w.slots, w.tsize, w.tflag, hint);
+                       out->seg_first, out->perm, out->seg_off, out->n_seg, out->n_valid, w.seg_slot, w.slots,
+                       w.tsize, keep_table ? 0u : w.tsize >> 4, w.tflag, hint);
     return rsk::launch_check("k_dm_final");
 }
 
@@ -1062,20 +1083,19 @@ extern "C" int rsk_demux_batch(rsk_ctx *c, uint32_t n, const rsk_demux_in *in, u
     a.cpos = (fields & RSK_DEMUX_CMD_BARRIER) ? w.cpos : nullptr;
     a.xep = nullptr;
     if (!group) return demux_pass(c, a, w, out, s);
-    // GROUP_BARRIER: by IdBuf first (into out), the epochs inside each IdBuf into pep (unused by
-    // either pass: neither has CMD_BARRIER), then the key with that epoch (over out again).  Between
-    // the passes every per-packet scratch array is free: k_dm_final of the first pass writes each
-    // position's control flag and segment id into rank_at / hslot, the scan goes to cidx and its
-    // chunk sums to cpos (positions past n_valid hold stale words; no kept value depends on them).
+    // GROUP_BARRIER: the control packets alone by IdBuf (into out; their VALID mask in pep, which
+    // neither pass uses otherwise), each DATA packet's epoch inside its IdBuf into pep (k_dm_gep, over
+    // the first pass's table and segments), then the key with that epoch (over out again)
+    int8_t *st2 = reinterpret_cast<int8_t *>(w.pep);
+    hipLaunchKernelGGL(k_dm_gstatus, dim3(w.nb), dim3(kBlock), 0, s, a.status, a.cmd, n, st2);
     DmIn ga = a;
+    ga.status = st2;
     ga.fields = RSK_DEMUX_ID;
-    if ((r = demux_pass(c, ga, w, out, s, w.rank_at, w.hslot))) return r;
-    ScanWs sw;
-    sw.sums = w.cpos;
-    sw.sum_off = w.cpos + (n + kScanChunk - 1) / kScanChunk;
-    if ((r = scan_u32(w.rank_at, w.cidx, n, nullptr, sw, s))) return r;
-    hipLaunchKernelGGL(k_dm_gep, dim3(w.nb), dim3(kBlock), 0, s, out->n_valid, out->perm, out->seg_off, w.rank_at,
-                       w.hslot, w.cidx, w.pep);
+    if ((r = demux_pass(c, ga, w, out, s, true))) return r;
+    DmIn gk = a;  // the batch's own VALID mask (st2 is overwritten by the epochs), the IdBuf as the key
+    gk.fields = RSK_DEMUX_ID;
+    hipLaunchKernelGGL(k_dm_gep, dim3(w.nb), dim3(kBlock), 0, s, gk, w.slots, w.tsize - 1u, w.rank_at, out->perm,
+                       out->seg_off, w.pep, c->err_dev);
     if ((r = rsk::launch_check("k_dm_gep"))) return r;
     a.xep = w.pep;
     return demux_pass(c, a, w, out, s);
