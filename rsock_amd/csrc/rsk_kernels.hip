@@ -1020,11 +1020,10 @@ __global__ __launch_bounds__(kBlock) void k_encode_heads_os(EncArgs a, KeySched 
         __hip_atomic_store(m.ctl, m.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Lane view of one frame of the window: start address, bytes written (padded), payload geometry.
+// The frame a lane's chunk takes bytes from: payload offset and length, packet index (its record).
 struct OsFrame {
-    uint64_t s, e;        // [s, e): the frame's bytes in the arena (absolute addresses)
-    uint64_t po;          // payload offset
-    uint32_t P, p;        // payload length, packet index
+    uint64_t po;
+    uint32_t P, p;
 };
 
 // The 16 bytes of frame F's image at image offset t (t >= 0): header words from its record for
